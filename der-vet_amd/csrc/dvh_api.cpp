@@ -1,0 +1,485 @@
+// dvh_api.cpp -- C ABI of libdervet_hip (declared in include/dervet_hip.h).
+//
+// Replaces the per-window solve of storagevet Scenario.solve_optimization (dervet/MicrogridScenario.py:319)
+// for a whole batch of windows: validates and packs host LPs, moves them to HBM, runs the setup and PDHG
+// kernels chunk by chunk on the handle's stream, and copies primal/dual solutions and statistics back.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/dervet_hip.h"
+#include "dvh_internal.h"
+
+#define DVH_VERSION_STRING "dervet_hip 0.1.0 (gfx950, restarted reflected-Halpern PDHG)"
+
+namespace {
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  hipError_t ensure(size_t want) {
+    if (want <= bytes) return hipSuccess;
+    if (p) hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    want = std::max<size_t>(want, 256);
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) bytes = want;
+    return e;
+  }
+  void release() {
+    if (p) hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  template <class T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+constexpr int kChunkWindows = 32768;
+
+}  // namespace
+
+struct dvh_handle {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  dvh_options opts{};
+  std::string err;
+  // packed inputs / outputs for the host API
+  DevBuf d_desc, d_indptr, d_indices, d_data, d_c, d_c0, d_q, d_l, d_u, d_x, d_y, d_stats, d_istats;
+  // workspace
+  DevBuf w_tptr, w_tind, w_tval, w_kval, w_rowof, w_perm, w_dr, w_dc, w_cs, w_ls, w_us, w_qs, w_vbuf, w_wbuf,
+      w_tmpc, w_tmpr, w_longk, w_longt, w_scal;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  double timing[3] = {0, 0, 0};
+  int last_variant = -1;
+};
+
+static int fail(dvh_handle* h, int code, const std::string& msg) {
+  if (h) h->err = msg;
+  return code;
+}
+
+static int hip_fail(dvh_handle* h, hipError_t e, const char* where) {
+  return fail(h, DVH_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+#define DVH_HIP(h, call)                                 \
+  do {                                                   \
+    hipError_t e_ = (call);                              \
+    if (e_ != hipSuccess) return hip_fail(h, e_, #call); \
+  } while (0)
+
+extern "C" {
+
+const char* dvh_version(void) { return DVH_VERSION_STRING; }
+
+void dvh_default_options(dvh_options* o) {
+  if (!o) return;
+  std::memset(o, 0, sizeof(*o));
+  o->eps = 1e-6;
+  o->max_iters = 100000;
+  o->check_every = 64;
+  o->ruiz_iters = 10;
+  o->power_iters = 64;
+  o->step_safety = 0.998;
+  o->reflection = 1.0;
+  o->restart_sufficient = 0.2;
+  o->restart_necessary = 0.8;
+  o->restart_artificial = 0.36;
+  o->primal_weight_theta = 0.5;
+  o->verbose = 0;
+}
+
+static std::string check_options(const dvh_options* o) {
+  if (!(o->eps > 0.0)) return "eps must be > 0";
+  if (o->max_iters <= 0) return "max_iters must be > 0";
+  if (o->check_every <= 0) return "check_every must be > 0";
+  if (o->ruiz_iters < 0 || o->power_iters <= 0) return "ruiz_iters must be >= 0 and power_iters > 0";
+  if (!(o->step_safety > 0.0 && o->step_safety < 1.0)) return "step_safety must be in (0, 1)";
+  if (!(o->reflection >= 0.0 && o->reflection <= 1.0)) return "reflection must be in [0, 1]";
+  return "";
+}
+
+int dvh_create(int device_mask, const dvh_options* opts, dvh_handle** out) {
+  if (!out) return DVH_ERR_ARG;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return DVH_ERR_HIP;
+  int dev = 0;
+  if (device_mask > 0) {
+    while (dev < 31 && !((device_mask >> dev) & 1)) ++dev;
+  }
+  if (dev >= ndev) return DVH_ERR_ARG;
+  dvh_handle* h = new dvh_handle();
+  h->device = dev;
+  dvh_default_options(&h->opts);
+  if (opts) {
+    std::string m = check_options(opts);
+    if (!m.empty()) {
+      delete h;
+      return DVH_ERR_ARG;
+    }
+    h->opts = *opts;
+  }
+  if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete h;
+    return DVH_ERR_HIP;
+  }
+  for (auto& e : h->ev) hipEventCreate(&e);
+  *out = h;
+  return DVH_OK;
+}
+
+int dvh_set_options(dvh_handle* h, const dvh_options* opts) {
+  if (!h || !opts) return DVH_ERR_ARG;
+  std::string m = check_options(opts);
+  if (!m.empty()) return fail(h, DVH_ERR_ARG, m);
+  h->opts = *opts;
+  return DVH_OK;
+}
+
+int dvh_destroy(dvh_handle* h) {
+  if (!h) return DVH_ERR_ARG;
+  hipSetDevice(h->device);
+  if (h->stream) hipStreamSynchronize(h->stream);
+  DevBuf* bufs[] = {&h->d_desc, &h->d_indptr, &h->d_indices, &h->d_data, &h->d_c, &h->d_c0, &h->d_q, &h->d_l,
+                    &h->d_u, &h->d_x, &h->d_y, &h->d_stats, &h->d_istats, &h->w_tptr, &h->w_tind, &h->w_tval,
+                    &h->w_kval, &h->w_rowof, &h->w_perm, &h->w_dr, &h->w_dc, &h->w_cs, &h->w_ls, &h->w_us,
+                    &h->w_qs, &h->w_vbuf, &h->w_wbuf, &h->w_tmpc, &h->w_tmpr, &h->w_longk, &h->w_longt, &h->w_scal};
+  for (DevBuf* b : bufs) b->release();
+  for (auto& e : h->ev)
+    if (e) hipEventDestroy(e);
+  if (h->stream) hipStreamDestroy(h->stream);
+  delete h;
+  return DVH_OK;
+}
+
+const char* dvh_last_error(const dvh_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
+int dvh_synchronize(dvh_handle* h) {
+  if (!h) return DVH_ERR_ARG;
+  DVH_HIP(h, hipStreamSynchronize(h->stream));
+  float a = 0, b = 0;
+  h->timing[0] = 0;
+  if (hipEventElapsedTime(&a, h->ev[0], h->ev[3]) == hipSuccess) h->timing[0] = a;
+  (void)b;
+  return DVH_OK;
+}
+
+int dvh_last_timing(const dvh_handle* h, double* ms3) {
+  if (!h || !ms3) return DVH_ERR_ARG;
+  for (int i = 0; i < 3; ++i) ms3[i] = h->timing[i];
+  return DVH_OK;
+}
+
+}  // extern "C"
+
+// Solve a packed device batch given a host copy of its descriptors.
+static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<int64_t>& desc, hipStream_t s) {
+  const int count = bt->count;
+  dvh::Opts o;
+  o.eps = h->opts.eps;
+  o.step_safety = h->opts.step_safety;
+  o.rho = h->opts.reflection;
+  o.b_suff = h->opts.restart_sufficient;
+  o.b_nec = h->opts.restart_necessary;
+  o.b_art = h->opts.restart_artificial;
+  o.theta = h->opts.primal_weight_theta;
+  o.max_iters = h->opts.max_iters;
+  o.check_every = h->opts.check_every;
+  o.ruiz_iters = h->opts.ruiz_iters;
+  o.power_iters = h->opts.power_iters;
+  dvh::Batch b{bt->desc, bt->indptr, bt->indices, bt->data, bt->c, bt->c0, bt->q, bt->l, bt->u,
+               bt->x, bt->y, bt->stats, bt->istats};
+  // chunking + workspace sizing
+  struct C {
+    dvh::Chunk ch;
+    int64_t sn, sm, snz;
+    int mn, mm;
+    int64_t mnz;
+  };
+  std::vector<C> chunks;
+  int64_t wn = 0, wm = 0, wnz = 0;
+  int wc = 0;
+  for (int first = 0; first < count; first += kChunkWindows) {
+    C c{};
+    c.ch.first = first;
+    c.ch.count = std::min(kChunkWindows, count - first);
+    const int64_t* d0 = &desc[8 * (size_t)first];
+    c.ch.base_n = d0[6];
+    c.ch.base_m = d0[7];
+    c.ch.base_nz = d0[5];
+    for (int k = first; k < first + c.ch.count; ++k) {
+      const int64_t* d = &desc[8 * (size_t)k];
+      c.sn = std::max(c.sn, d[6] + d[0] - c.ch.base_n);
+      c.sm = std::max(c.sm, d[7] + d[1] - c.ch.base_m);
+      c.snz = std::max(c.snz, d[5] + d[3] - c.ch.base_nz);
+      c.mn = std::max<int>(c.mn, (int)d[0]);
+      c.mm = std::max<int>(c.mm, (int)d[1]);
+      c.mnz = std::max(c.mnz, d[3]);
+    }
+    wn = std::max(wn, c.sn);
+    wm = std::max(wm, c.sm);
+    wnz = std::max(wnz, c.snz);
+    wc = std::max(wc, c.ch.count);
+    chunks.push_back(c);
+  }
+  const size_t D = sizeof(double), I = sizeof(int32_t);
+  DVH_HIP(h, h->w_tptr.ensure(I * (wn + wc)));
+  DVH_HIP(h, h->w_tind.ensure(I * wnz));
+  DVH_HIP(h, h->w_tval.ensure(D * wnz));
+  DVH_HIP(h, h->w_kval.ensure(D * wnz));
+  DVH_HIP(h, h->w_rowof.ensure(I * wnz));
+  DVH_HIP(h, h->w_perm.ensure(I * wnz));
+  DVH_HIP(h, h->w_dr.ensure(D * wm));
+  DVH_HIP(h, h->w_dc.ensure(D * wn));
+  DVH_HIP(h, h->w_cs.ensure(D * wn));
+  DVH_HIP(h, h->w_ls.ensure(D * wn));
+  DVH_HIP(h, h->w_us.ensure(D * wn));
+  DVH_HIP(h, h->w_qs.ensure(D * wm));
+  DVH_HIP(h, h->w_vbuf.ensure(D * wn));
+  DVH_HIP(h, h->w_wbuf.ensure(D * wm));
+  DVH_HIP(h, h->w_tmpc.ensure(D * wn));
+  DVH_HIP(h, h->w_tmpr.ensure(D * wm));
+  DVH_HIP(h, h->w_longk.ensure(I * (size_t)wc * dvh::kLMax));
+  DVH_HIP(h, h->w_longt.ensure(I * (size_t)wc * dvh::kLMax));
+  DVH_HIP(h, h->w_scal.ensure(D * (size_t)wc * dvh::kScal));
+  dvh::Work w{h->w_tptr.as<int32_t>(), h->w_tind.as<int32_t>(), h->w_tval.as<double>(), h->w_kval.as<double>(),
+              h->w_rowof.as<int32_t>(), h->w_perm.as<int32_t>(), h->w_dr.as<double>(), h->w_dc.as<double>(),
+              h->w_cs.as<double>(), h->w_ls.as<double>(), h->w_us.as<double>(), h->w_qs.as<double>(),
+              h->w_vbuf.as<double>(), h->w_wbuf.as<double>(), h->w_tmpc.as<double>(), h->w_tmpr.as<double>(),
+              h->w_longk.as<int32_t>(), h->w_longt.as<int32_t>(), h->w_scal.as<double>()};
+  const bool single = chunks.size() == 1;
+  DVH_HIP(h, hipEventRecord(h->ev[0], s));
+  for (const C& c : chunks) {
+    if (c.mn + 1 > 40000) return fail(h, DVH_ERR_UNSUPPORTED, "window with more than 40000 variables (large-LP path not built yet)");
+    DVH_HIP(h, dvh::launch_setup(b, w, c.ch, o, c.mn, s));
+    if (single) DVH_HIP(h, hipEventRecord(h->ev[1], s));
+    int variant = -1;
+    hipError_t e = dvh::launch_pdhg(b, w, c.ch, o, c.mn, c.mm, c.mnz, s, &variant);
+    if (e == hipErrorInvalidValue)
+      return fail(h, DVH_ERR_UNSUPPORTED, "window too large for the on-chip PDHG kernel (n or m > 4096)");
+    if (e != hipSuccess) return hip_fail(h, e, "launch_pdhg");
+    h->last_variant = variant;
+  }
+  if (single) DVH_HIP(h, hipEventRecord(h->ev[2], s));
+  DVH_HIP(h, hipEventRecord(h->ev[3], s));
+  return DVH_OK;
+}
+
+static int finish_timing(dvh_handle* h) {
+  DVH_HIP(h, hipStreamSynchronize(h->stream));
+  float t = 0;
+  h->timing[0] = h->timing[1] = h->timing[2] = 0;
+  if (hipEventElapsedTime(&t, h->ev[0], h->ev[3]) == hipSuccess) h->timing[0] = t;
+  if (hipEventElapsedTime(&t, h->ev[0], h->ev[1]) == hipSuccess) h->timing[1] = t;
+  if (hipEventElapsedTime(&t, h->ev[1], h->ev[2]) == hipSuccess) h->timing[2] = t;
+  return DVH_OK;
+}
+
+static std::string validate(const dvh_lp& lp, int k) {
+  char buf[256];
+  const int m = lp.m_eq + lp.m_ineq;
+  if (lp.n <= 0 || lp.m_eq < 0 || lp.m_ineq < 0 || lp.nnz < 0) {
+    snprintf(buf, sizeof buf, "window %d: invalid sizes n=%d m_eq=%d m_ineq=%d nnz=%d", k, lp.n, lp.m_eq, lp.m_ineq,
+             lp.nnz);
+    return buf;
+  }
+  if (!lp.indptr || (lp.nnz > 0 && (!lp.indices || !lp.data)) || !lp.c || (m > 0 && !lp.q) || !lp.l || !lp.u) {
+    snprintf(buf, sizeof buf, "window %d: null array", k);
+    return buf;
+  }
+  if (lp.indptr[0] != 0 || lp.indptr[m] != lp.nnz) {
+    snprintf(buf, sizeof buf, "window %d: indptr[0] must be 0 and indptr[m] == nnz", k);
+    return buf;
+  }
+  for (int i = 0; i < m; ++i)
+    if (lp.indptr[i + 1] < lp.indptr[i]) {
+      snprintf(buf, sizeof buf, "window %d: indptr not monotone at row %d", k, i);
+      return buf;
+    }
+  for (int p = 0; p < lp.nnz; ++p) {
+    if (lp.indices[p] < 0 || lp.indices[p] >= lp.n) {
+      snprintf(buf, sizeof buf, "window %d: column index %d out of range at nnz %d", k, lp.indices[p], p);
+      return buf;
+    }
+    if (!std::isfinite(lp.data[p])) {
+      snprintf(buf, sizeof buf, "window %d: non-finite matrix value at nnz %d", k, p);
+      return buf;
+    }
+  }
+  for (int i = 0; i < m; ++i) {
+    // duplicate column within a row makes the transpose ambiguous for nothing; reject
+    for (int p = lp.indptr[i] + 1; p < lp.indptr[i + 1]; ++p)
+      for (int r = lp.indptr[i]; r < p; ++r)
+        if (lp.indices[r] == lp.indices[p]) {
+          snprintf(buf, sizeof buf, "window %d: duplicate column %d in row %d", k, lp.indices[p], i);
+          return buf;
+        }
+    if (!std::isfinite(lp.q[i])) {
+      snprintf(buf, sizeof buf, "window %d: non-finite rhs at row %d", k, i);
+      return buf;
+    }
+  }
+  for (int j = 0; j < lp.n; ++j) {
+    if (!std::isfinite(lp.c[j]) || std::isnan(lp.l[j]) || std::isnan(lp.u[j]) || lp.l[j] > lp.u[j] ||
+        lp.l[j] == INFINITY || lp.u[j] == -INFINITY) {
+      snprintf(buf, sizeof buf, "window %d: invalid objective or bounds at variable %d", k, j);
+      return buf;
+    }
+  }
+  if (!std::isfinite(lp.c0)) {
+    snprintf(buf, sizeof buf, "window %d: non-finite c0", k);
+    return buf;
+  }
+  return "";
+}
+
+extern "C" int dvh_solve_batch(dvh_handle* h, const dvh_lp* lps, int32_t count, dvh_result* out) {
+  if (!h) return DVH_ERR_ARG;
+  if (count < 0 || (count > 0 && (!lps || !out))) return fail(h, DVH_ERR_ARG, "null lps/out or negative count");
+  if (count == 0) return DVH_OK;
+  DVH_HIP(h, hipSetDevice(h->device));
+  std::vector<int64_t> desc(8 * (size_t)count);
+  int64_t tn = 0, tm = 0, tz = 0, tr = 0;
+  for (int k = 0; k < count; ++k) {
+    std::string msg = validate(lps[k], k);
+    if (!msg.empty()) return fail(h, DVH_ERR_ARG, msg);
+    const dvh_lp& lp = lps[k];
+    const int m = lp.m_eq + lp.m_ineq;
+    int64_t* d = &desc[8 * (size_t)k];
+    d[0] = lp.n;
+    d[1] = m;
+    d[2] = lp.m_eq;
+    d[3] = lp.nnz;
+    d[4] = tr;
+    d[5] = tz;
+    d[6] = tn;
+    d[7] = tm;
+    tr += m + 1;
+    tz += lp.nnz;
+    tn += lp.n;
+    tm += m;
+  }
+  std::vector<int32_t> indptr(tr), indices(tz);
+  std::vector<double> data(tz), c(tn), l(tn), u(tn), q(tm), c0(count);
+  for (int k = 0; k < count; ++k) {
+    const dvh_lp& lp = lps[k];
+    const int64_t* d = &desc[8 * (size_t)k];
+    const int m = (int)d[1];
+    std::memcpy(&indptr[d[4]], lp.indptr, sizeof(int32_t) * (m + 1));
+    if (lp.nnz) {
+      std::memcpy(&indices[d[5]], lp.indices, sizeof(int32_t) * lp.nnz);
+      std::memcpy(&data[d[5]], lp.data, sizeof(double) * lp.nnz);
+    }
+    std::memcpy(&c[d[6]], lp.c, sizeof(double) * lp.n);
+    std::memcpy(&l[d[6]], lp.l, sizeof(double) * lp.n);
+    std::memcpy(&u[d[6]], lp.u, sizeof(double) * lp.n);
+    if (m) std::memcpy(&q[d[7]], lp.q, sizeof(double) * m);
+    c0[k] = lp.c0;
+  }
+  const size_t D = sizeof(double), I = sizeof(int32_t);
+  DVH_HIP(h, h->d_desc.ensure(desc.size() * sizeof(int64_t)));
+  DVH_HIP(h, h->d_indptr.ensure(I * tr));
+  DVH_HIP(h, h->d_indices.ensure(I * std::max<int64_t>(tz, 1)));
+  DVH_HIP(h, h->d_data.ensure(D * std::max<int64_t>(tz, 1)));
+  DVH_HIP(h, h->d_c.ensure(D * tn));
+  DVH_HIP(h, h->d_l.ensure(D * tn));
+  DVH_HIP(h, h->d_u.ensure(D * tn));
+  DVH_HIP(h, h->d_x.ensure(D * tn));
+  DVH_HIP(h, h->d_q.ensure(D * std::max<int64_t>(tm, 1)));
+  DVH_HIP(h, h->d_y.ensure(D * std::max<int64_t>(tm, 1)));
+  DVH_HIP(h, h->d_c0.ensure(D * count));
+  DVH_HIP(h, h->d_stats.ensure(D * 4 * count));
+  DVH_HIP(h, h->d_istats.ensure(I * 2 * count));
+  hipStream_t s = h->stream;
+  DVH_HIP(h, hipMemcpyAsync(h->d_desc.p, desc.data(), desc.size() * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  DVH_HIP(h, hipMemcpyAsync(h->d_indptr.p, indptr.data(), I * tr, hipMemcpyHostToDevice, s));
+  if (tz) {
+    DVH_HIP(h, hipMemcpyAsync(h->d_indices.p, indices.data(), I * tz, hipMemcpyHostToDevice, s));
+    DVH_HIP(h, hipMemcpyAsync(h->d_data.p, data.data(), D * tz, hipMemcpyHostToDevice, s));
+  }
+  DVH_HIP(h, hipMemcpyAsync(h->d_c.p, c.data(), D * tn, hipMemcpyHostToDevice, s));
+  DVH_HIP(h, hipMemcpyAsync(h->d_l.p, l.data(), D * tn, hipMemcpyHostToDevice, s));
+  DVH_HIP(h, hipMemcpyAsync(h->d_u.p, u.data(), D * tn, hipMemcpyHostToDevice, s));
+  if (tm) DVH_HIP(h, hipMemcpyAsync(h->d_q.p, q.data(), D * tm, hipMemcpyHostToDevice, s));
+  DVH_HIP(h, hipMemcpyAsync(h->d_c0.p, c0.data(), D * count, hipMemcpyHostToDevice, s));
+  dvh_packed bt{};
+  bt.count = count;
+  bt.total_n = tn;
+  bt.total_m = tm;
+  bt.total_nnz = tz;
+  bt.total_rows = tr;
+  bt.desc = h->d_desc.as<int64_t>();
+  bt.indptr = h->d_indptr.as<int32_t>();
+  bt.indices = h->d_indices.as<int32_t>();
+  bt.data = h->d_data.as<double>();
+  bt.c = h->d_c.as<double>();
+  bt.c0 = h->d_c0.as<double>();
+  bt.q = h->d_q.as<double>();
+  bt.l = h->d_l.as<double>();
+  bt.u = h->d_u.as<double>();
+  bt.x = h->d_x.as<double>();
+  bt.y = h->d_y.as<double>();
+  bt.stats = h->d_stats.as<double>();
+  bt.istats = h->d_istats.as<int32_t>();
+  int rc = solve_packed(h, &bt, desc, s);
+  if (rc != DVH_OK) return rc;
+  std::vector<double> x(tn), y(tm), stats(4 * (size_t)count);
+  std::vector<int32_t> ist(2 * (size_t)count);
+  DVH_HIP(h, hipMemcpyAsync(x.data(), h->d_x.p, D * tn, hipMemcpyDeviceToHost, s));
+  if (tm) DVH_HIP(h, hipMemcpyAsync(y.data(), h->d_y.p, D * tm, hipMemcpyDeviceToHost, s));
+  DVH_HIP(h, hipMemcpyAsync(stats.data(), h->d_stats.p, D * 4 * count, hipMemcpyDeviceToHost, s));
+  DVH_HIP(h, hipMemcpyAsync(ist.data(), h->d_istats.p, I * 2 * count, hipMemcpyDeviceToHost, s));
+  rc = finish_timing(h);
+  if (rc != DVH_OK) return rc;
+  for (int k = 0; k < count; ++k) {
+    const int64_t* d = &desc[8 * (size_t)k];
+    dvh_result& r = out[k];
+    if (r.x) std::memcpy(r.x, &x[d[6]], D * d[0]);
+    if (r.y && d[1]) std::memcpy(r.y, &y[d[7]], D * d[1]);
+    r.obj = stats[4 * k];
+    r.primal_res_rel = stats[4 * k + 1];
+    r.dual_res_rel = stats[4 * k + 2];
+    r.gap_rel = stats[4 * k + 3];
+    r.status = ist[2 * k];
+    r.iters = ist[2 * k + 1];
+  }
+  return DVH_OK;
+}
+
+extern "C" int dvh_solve_packed_device(dvh_handle* h, const dvh_packed* bt, void* stream) {
+  if (!h) return DVH_ERR_ARG;
+  if (!bt || bt->count < 0) return fail(h, DVH_ERR_ARG, "null or negative batch");
+  if (bt->count == 0) return DVH_OK;
+  if (!bt->desc || !bt->indptr || !bt->c || !bt->c0 || !bt->l || !bt->u || !bt->x || !bt->stats || !bt->istats)
+    return fail(h, DVH_ERR_ARG, "null device array in packed batch");
+  DVH_HIP(h, hipSetDevice(h->device));
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->stream;
+  std::vector<int64_t> desc(8 * (size_t)bt->count);
+  DVH_HIP(h, hipMemcpyAsync(desc.data(), bt->desc, desc.size() * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  DVH_HIP(h, hipStreamSynchronize(s));
+  // host-side sanity of the descriptors (no device data is read beyond desc)
+  for (int k = 0; k < bt->count; ++k) {
+    const int64_t* d = &desc[8 * (size_t)k];
+    if (d[0] <= 0 || d[1] < 0 || d[2] < 0 || d[2] > d[1] || d[3] < 0 || d[4] < 0 || d[5] < 0 || d[6] < 0 || d[7] < 0 ||
+        d[4] + d[1] + 1 > bt->total_rows || d[5] + d[3] > bt->total_nnz || d[6] + d[0] > bt->total_n ||
+        d[7] + d[1] > bt->total_m)
+      return fail(h, DVH_ERR_ARG, "packed descriptor " + std::to_string(k) + " out of range");
+    if (k > 0) {
+      const int64_t* p = &desc[8 * (size_t)(k - 1)];
+      if (d[5] < p[5] || d[6] < p[6] || d[7] < p[7])
+        return fail(h, DVH_ERR_ARG, "packed descriptors must have non-decreasing offsets");
+    }
+  }
+  int rc = solve_packed(h, bt, desc, s);
+  if (rc != DVH_OK) return rc;
+  if (!stream) return finish_timing(h);
+  return DVH_OK;
+}

@@ -1,0 +1,74 @@
+// Internal declarations shared by the C-ABI layer (dvh_api.cpp) and the HIP kernels (dvh_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dvh {
+
+constexpr int kWave = 64;
+constexpr int kLongRow = 32;   // CSR rows longer than this are reduced by a whole wave
+constexpr int kLMax = 64;      // long rows per matrix per window handled on chip
+constexpr int kScal = 8;       // per-window scalars written by the setup kernel
+
+// Kernel-side copy of dvh_options (POD, passed by value).
+struct Opts {
+  double eps, step_safety, rho, b_suff, b_nec, b_art, theta;
+  int max_iters, check_every, ruiz_iters, power_iters;
+};
+
+// Inputs of one chunk of the packed batch (device pointers, global offsets from desc).
+struct Batch {
+  const int64_t* desc;
+  const int32_t* indptr;
+  const int32_t* indices;
+  const double* data;
+  const double* c;
+  const double* c0;
+  const double* q;
+  const double* l;
+  const double* u;
+  double* x;
+  double* y;
+  double* stats;
+  int32_t* istats;
+};
+
+// Per-chunk device workspace.  Window k of the chunk uses offsets (desc offsets - chunk base).
+struct Work {
+  int32_t* tptr;    // [sum(n+1)]   K^T row pointers        at (off_n - base_n) + (k - first)
+  int32_t* tind;    // [sum nnz]    K^T column (= K row) ids
+  double* tval;     // [sum nnz]    scaled K^T values
+  double* kval;     // [sum nnz]    scaled K values
+  int32_t* rowof;   // [sum nnz]    K entry -> row
+  int32_t* perm;    // [sum nnz]    K entry -> K^T slot
+  double* dr;       // [sum m]
+  double* dc;       // [sum n]
+  double* cs;       // [sum n]  Dc c
+  double* ls;       // [sum n]  l / Dc
+  double* us;       // [sum n]  u / Dc
+  double* qs;       // [sum m]  Dr q
+  double* vbuf;     // [sum n]
+  double* wbuf;     // [sum m]
+  double* tmpc;     // [sum n]
+  double* tmpr;     // [sum m]
+  int32_t* longk;   // [count * kLMax]  long rows of K
+  int32_t* longt;   // [count * kLMax]  long rows of K^T (dense columns, e.g. the DCM tau)
+  double* scal;     // [count * kScal]  eta, w0, ||c||, ||q||, nlong(K), nlong(K^T), flag, ||K||
+};
+
+struct Chunk {
+  int first;        // first window index (global)
+  int count;
+  int64_t base_n, base_m, base_nz;
+};
+
+// Launchers (dvh_kernels.hip).  Return hipError_t.
+hipError_t launch_setup(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n,
+                        hipStream_t s);
+// Solve kernel selection is made from the chunk maxima; returns hipErrorInvalidValue when no
+// instantiation covers the sizes (the caller reports DVH_ERR_UNSUPPORTED).
+hipError_t launch_pdhg(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n, int max_m,
+                       int64_t max_nnz, hipStream_t s, int* variant_out);
+size_t setup_lds_bytes(int max_n);
+
+}  // namespace dvh

@@ -1,0 +1,775 @@
+// dvh_kernels.hip -- batched restarted reflected-Halpern PDHG for DER-VET dispatch-window LPs (gfx950).
+//
+// Replaces the per-window ECOS/GLPK solve behind storagevet Scenario.solve_optimization
+// (dervet/MicrogridScenario.py:319); algorithm restated for tests in oracle/pdlp_ref.py.
+//
+// Two kernels per chunk of windows, ONE WORKGROUP PER WINDOW:
+//   setup_kernel : deterministic CSR transpose, Ruiz + Pock-Chambolle scaling, power iteration for ||K||_2
+//   pdhg_kernel  : the whole iteration loop in one launch.  Every primal / dual component is owned by one
+//                  lane and lives in VGPRs for the life of the solve; the only per-iteration traffic is the
+//                  two SpMV gathers through LDS (x-bar and y images) and, when the window fits (monthly
+//                  windows do), the scaled K and K^T themselves are LDS-resident too, so an iteration
+//                  touches no HBM at all.  Rows with more than kLongRow entries (the DCM tau column) are
+//                  reduced by a whole wave with a shuffle tree.
+// All reductions are fixed-order (wave butterflies + per-wave slots summed in wave order), so results
+// are bitwise reproducible run to run.
+#include "dvh_internal.h"
+
+#include <math.h>
+
+namespace dvh {
+
+namespace {
+
+constexpr int kOptimal = 0, kIterLimit = 3, kNumerical = 4;
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+
+// Block reduction of NV doubles; red must hold (NW + 1) * NV doubles.  Result identical in all threads.
+template <int B, int NV>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double* red) {
+  constexpr int NW = B / kWave;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = wave_sum(v[k]);
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) red[wid * NV + k] = v[k];
+  }
+  __syncthreads();
+  if (tid < NV) {
+    double s = 0.0;
+    for (int w = 0; w < NW; ++w) s += red[w * NV + tid];
+    red[NW * NV + tid] = s;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = red[NW * NV + k];
+  __syncthreads();
+}
+
+struct WinOff {
+  int n, m, meq, nnz;
+  int64_t row, nz, on, om;     // global offsets (inputs / outputs)
+  int64_t wn, wm, wz, wtr;     // chunk-relative workspace offsets
+};
+
+__device__ __forceinline__ WinOff win_offsets(const Batch& b, const Chunk& ch, int k) {
+  const int64_t* d = b.desc + 8 * (int64_t)k;
+  WinOff o;
+  o.n = (int)d[0];
+  o.m = (int)d[1];
+  o.meq = (int)d[2];
+  o.nnz = (int)d[3];
+  o.row = d[4];
+  o.nz = d[5];
+  o.on = d[6];
+  o.om = d[7];
+  o.wn = o.on - ch.base_n;
+  o.wm = o.om - ch.base_m;
+  o.wz = o.nz - ch.base_nz;
+  o.wtr = o.wn + (k - ch.first);
+  return o;
+}
+
+// ------------------------------------------------------------------------------------------------
+// setup kernel
+// ------------------------------------------------------------------------------------------------
+constexpr int kSetupB = 256;
+
+// Row reductions over a CSR matrix: short rows one per thread, long rows one per wave.
+// f(e, row) -> contribution; MAXR selects max instead of sum.  out[row] = g(row, reduced).
+template <bool MAXR, class F, class G>
+__device__ __forceinline__ void rows_reduce(const int32_t* ptr, int rows, const int32_t* longl, int nlong,
+                                            F f, G g) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  constexpr int NW = kSetupB / kWave;
+  for (int i = tid; i < rows; i += kSetupB) {
+    const int s = ptr[i], e = ptr[i + 1];
+    if (e - s > kLongRow) continue;
+    double acc = 0.0;
+    for (int p = s; p < e; ++p) {
+      const double v = f(p, i);
+      acc = MAXR ? fmax(acc, v) : acc + v;
+    }
+    g(i, acc);
+  }
+  for (int L = wid; L < nlong; L += NW) {
+    const int i = longl[L];
+    const int s = ptr[i], e = ptr[i + 1];
+    double acc = 0.0;
+    for (int p = s + lane; p < e; p += kWave) {
+      const double v = f(p, i);
+      acc = MAXR ? fmax(acc, v) : acc + v;
+    }
+    acc = MAXR ? wave_max(acc) : wave_sum(acc);
+    if (lane == 0) g(i, acc);
+  }
+}
+
+__global__ __launch_bounds__(kSetupB) void setup_kernel(const Batch b, const Work w, const Chunk ch, const Opts o) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ double red[(kSetupB / kWave + 1) * 4];
+  __shared__ int sh_part[kSetupB];
+  __shared__ int sh_cnt[2];
+  const int k = ch.first + blockIdx.x;
+  const int kl = blockIdx.x;
+  const WinOff W = win_offsets(b, ch, k);
+  const int n = W.n, m = W.m, nnz = W.nnz;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  int32_t* cursor = reinterpret_cast<int32_t*>(smem);  // [n + 1]
+
+  const int32_t* Kp = b.indptr + W.row;
+  const int32_t* Kc = b.indices + W.nz;
+  const double* Kv = b.data + W.nz;
+  int32_t* Tp = w.tptr + W.wtr;
+  int32_t* Ti = w.tind + W.wz;
+  double* Tv = w.tval + W.wz;
+  double* KV = w.kval + W.wz;
+  int32_t* rowof = w.rowof + W.wz;
+  int32_t* perm = w.perm + W.wz;
+  double* Dr = w.dr + W.wm;
+  double* Dc = w.dc + W.wn;
+  double* tmpr = w.tmpr + W.wm;
+  double* tmpc = w.tmpc + W.wn;
+  int32_t* longk = w.longk + (int64_t)kl * kLMax;
+  int32_t* longt = w.longt + (int64_t)kl * kLMax;
+  double* scal = w.scal + (int64_t)kl * kScal;
+
+  // 1. column counts, entry -> row map
+  for (int j = tid; j <= n; j += kSetupB) cursor[j] = 0;
+  __syncthreads();
+  for (int i = tid; i < m; i += kSetupB)
+    for (int p = Kp[i]; p < Kp[i + 1]; ++p) rowof[p] = i;
+  for (int p = tid; p < nnz; p += kSetupB) atomicAdd(&cursor[Kc[p]], 1);
+  __syncthreads();
+  // 2. exclusive scan of the n counts -> Tp (chunked per thread, partials scanned by thread 0)
+  {
+    const int per = (n + kSetupB - 1) / kSetupB;
+    const int s = tid * per, e = min(n, s + per);
+    int acc = 0;
+    for (int j = s; j < e; ++j) acc += cursor[j];
+    sh_part[tid] = acc;
+    __syncthreads();
+    if (tid == 0) {
+      int run = 0;
+      for (int t = 0; t < kSetupB; ++t) {
+        const int v = sh_part[t];
+        sh_part[t] = run;
+        run += v;
+      }
+    }
+    __syncthreads();
+    int run = sh_part[tid];
+    for (int j = s; j < e; ++j) {
+      const int v = cursor[j];
+      Tp[j] = run;
+      cursor[j] = run;
+      run += v;
+    }
+    if (tid == 0) Tp[n] = nnz;
+  }
+  __syncthreads();
+  // 3. stable fill of K^T by wave 0 (entries visited in row-major order; ties ranked by lane).
+  if (wid == 0) {
+    for (int base = 0; base < nnz; base += kWave) {
+      const int p = base + lane;
+      const bool v = p < nnz;
+      const int j = v ? Kc[p] : -1 - lane;
+      int rank = 0, cnt = 0;
+      for (int l = 0; l < kWave; ++l) {
+        const int jj = __shfl(j, l, kWave);
+        if (jj == j) {
+          ++cnt;
+          rank += (l < lane);
+        }
+      }
+      int pos = 0;
+      if (v) pos = cursor[j] + rank;
+      __builtin_amdgcn_wave_barrier();
+      if (v) {
+        Ti[pos] = rowof[p];
+        Tv[pos] = Kv[p];
+        perm[p] = pos;
+        if (rank == cnt - 1) cursor[j] = pos + 1;
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    // 4. long-row lists (deterministic ballot compaction)
+    int nk = 0, nt = 0;
+    for (int base = 0; base < m; base += kWave) {
+      const int i = base + lane;
+      const bool isl = i < m && (Kp[i + 1] - Kp[i]) > kLongRow;
+      const unsigned long long bal = __ballot(isl);
+      const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+      if (isl && nk + pre < kLMax) longk[nk + pre] = i;
+      nk += __popcll(bal);
+    }
+    for (int base = 0; base < n; base += kWave) {
+      const int j = base + lane;
+      const bool isl = j < n && (Tp[j + 1] - Tp[j]) > kLongRow;
+      const unsigned long long bal = __ballot(isl);
+      const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+      if (isl && nt + pre < kLMax) longt[nt + pre] = j;
+      nt += __popcll(bal);
+    }
+    if (lane == 0) {
+      sh_cnt[0] = nk;
+      sh_cnt[1] = nt;
+    }
+  }
+  __syncthreads();
+  const int nlk = sh_cnt[0], nlt = sh_cnt[1];
+  if (nlk > kLMax || nlt > kLMax) {  // unsupported structure: more dense rows than the on-chip lists
+    if (tid == 0) {
+      scal[0] = 0.0;
+      scal[6] = 1.0;
+    }
+    return;
+  }
+  // 5. Ruiz (inf-norm) passes, then one Pock-Chambolle (alpha = 1) pass
+  for (int j = tid; j < n; j += kSetupB) Dc[j] = 1.0;
+  for (int i = tid; i < m; i += kSetupB) Dr[i] = 1.0;
+  __syncthreads();
+  for (int pass = 0; pass <= o.ruiz_iters; ++pass) {
+    const bool pc = pass == o.ruiz_iters;
+    auto fr = [&](int p, int i) { return fabs(Kv[p]) * Dr[i] * Dc[Kc[p]]; };
+    auto gr = [&](int i, double a) { tmpr[i] = a > 0.0 ? 1.0 / sqrt(a) : 1.0; };
+    auto fc = [&](int p, int j) { return fabs(Tv[p]) * Dc[j] * Dr[Ti[p]]; };
+    auto gc = [&](int j, double a) { tmpc[j] = a > 0.0 ? 1.0 / sqrt(a) : 1.0; };
+    if (pc) {
+      rows_reduce<false>(Kp, m, longk, nlk, fr, gr);
+      rows_reduce<false>(Tp, n, longt, nlt, fc, gc);
+    } else {
+      rows_reduce<true>(Kp, m, longk, nlk, fr, gr);
+      rows_reduce<true>(Tp, n, longt, nlt, fc, gc);
+    }
+    __syncthreads();
+    for (int j = tid; j < n; j += kSetupB) Dc[j] *= tmpc[j];
+    for (int i = tid; i < m; i += kSetupB) Dr[i] *= tmpr[i];
+    __syncthreads();
+  }
+  // 6. scaled data
+  for (int p = tid; p < nnz; p += kSetupB) {
+    const double v = Kv[p] * Dr[rowof[p]] * Dc[Kc[p]];
+    KV[p] = v;
+    Tv[perm[p]] = v;
+  }
+  double nrm[4] = {0.0, 0.0, 0.0, 0.0};  // ||cs||^2, ||qs||^2, ||c||^2, ||q||^2
+  for (int j = tid; j < n; j += kSetupB) {
+    const double cj = b.c[W.on + j], d = Dc[j];
+    w.cs[W.wn + j] = cj * d;
+    w.ls[W.wn + j] = b.l[W.on + j] / d;
+    w.us[W.wn + j] = b.u[W.on + j] / d;
+    nrm[0] += cj * d * cj * d;
+    nrm[2] += cj * cj;
+  }
+  for (int i = tid; i < m; i += kSetupB) {
+    const double qi = b.q[W.om + i], d = Dr[i];
+    w.qs[W.wm + i] = qi * d;
+    nrm[1] += qi * d * qi * d;
+    nrm[3] += qi * qi;
+  }
+  block_sum<kSetupB, 4>(nrm, red);
+  // 7. power iteration on Kt'Kt
+  double* v = w.vbuf + W.wn;
+  double* wv = w.wbuf + W.wm;
+  const double v0 = 1.0 / sqrt((double)(n > 0 ? n : 1));
+  for (int j = tid; j < n; j += kSetupB) v[j] = v0;
+  __syncthreads();
+  double sig = 0.0;
+  for (int it = 0; it < o.power_iters; ++it) {
+    rows_reduce<false>(Kp, m, longk, nlk, [&](int p, int) { return KV[p] * v[Kc[p]]; },
+                       [&](int i, double a) { wv[i] = a; });
+    __syncthreads();
+    double s2[1] = {0.0};
+    rows_reduce<false>(Tp, n, longt, nlt, [&](int p, int) { return Tv[p] * wv[Ti[p]]; },
+                       [&](int j, double a) { tmpc[j] = a; });
+    __syncthreads();
+    for (int j = tid; j < n; j += kSetupB) s2[0] += tmpc[j] * tmpc[j];
+    block_sum<kSetupB, 1>(s2, red);
+    const double nv = sqrt(s2[0]);
+    sig = sqrt(nv);
+    const double inv = nv > 0.0 ? 1.0 / nv : 0.0;
+    for (int j = tid; j < n; j += kSetupB) v[j] = tmpc[j] * inv;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const double ncs = sqrt(nrm[0]), nqs = sqrt(nrm[1]);
+    scal[0] = sig > 0.0 ? o.step_safety / sig : 1.0;
+    scal[1] = (ncs > 1e-10 && nqs > 1e-10) ? ncs / nqs : 1.0;
+    scal[2] = sqrt(nrm[2]);
+    scal[3] = sqrt(nrm[3]);
+    scal[4] = (double)nlk;
+    scal[5] = (double)nlt;
+    scal[6] = 0.0;
+    scal[7] = sig;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// PDHG kernel
+// ------------------------------------------------------------------------------------------------
+constexpr int kNRed = 9;
+
+template <bool MLDS>
+struct MatView;
+
+template <>
+struct MatView<true> {  // LDS-resident scaled matrices (16-bit column indices)
+  const int32_t* kp;
+  const uint16_t* kc;
+  const double* kv;
+  const int32_t* tp;
+  const uint16_t* tc;
+  const double* tv;
+};
+template <>
+struct MatView<false> {  // matrices read from the workspace (L2 / Infinity Cache)
+  const int32_t* kp;
+  const int32_t* kc;
+  const double* kv;
+  const int32_t* tp;
+  const int32_t* tc;
+  const double* tv;
+};
+
+__host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
+
+// LDS bytes needed by the PDHG kernel for a window (layout in pdhg_kernel).
+__host__ __device__ inline size_t pdhg_lds_bytes(int n, int m, int nnz, bool mlds, int nwaves) {
+  size_t s = align16(sizeof(double) * ((size_t)n + m + (size_t)kNRed * (nwaves + 1) + 10 * kLMax));
+  s += align16(sizeof(int32_t) * 2 * kLMax);
+  if (mlds) {
+    s += align16(sizeof(double) * 2 * (size_t)nnz);
+    s += align16(sizeof(int32_t) * ((size_t)n + m + 2));
+    s += align16(sizeof(uint16_t) * 2 * (size_t)nnz);
+  }
+  return s;
+}
+
+template <int B, int XS, int YS, bool MLDS>
+__global__ __launch_bounds__(B) void pdhg_kernel(const Batch b, const Work w, const Chunk ch, const Opts o) {
+  constexpr int NW = B / kWave;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int k = ch.first + blockIdx.x;
+  const int kl = blockIdx.x;
+  const WinOff W = win_offsets(b, ch, k);
+  const int n = W.n, m = W.m, meq = W.meq, nnz = W.nnz;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const double* scal = w.scal + (int64_t)kl * kScal;
+  const int nlk = (int)scal[4], nlt = (int)scal[5];
+  if (scal[6] != 0.0 || n > XS * B || m > YS * B || (MLDS && (n > 65535 || m > 65535))) {
+    if (tid == 0) {
+      b.istats[2 * k] = kNumerical;
+      b.istats[2 * k + 1] = 0;
+      for (int t = 0; t < 4; ++t) b.stats[4 * k + t] = NAN;
+    }
+    return;
+  }
+  // ---- LDS carve (all double arrays first, 16-byte aligned sections)
+  double* X = reinterpret_cast<double*>(smem);
+  double* Y = X + n;
+  double* red = Y + m;
+  double* lx = red + kNRed * (NW + 1);  // long columns: x, xa, c, lo, hi, xp   [6][kLMax]
+  double* ly = lx + 6 * kLMax;          // long rows:    y, ya, q, yp           [4][kLMax]
+  unsigned char* cur = smem + align16(sizeof(double) * ((size_t)n + m + (size_t)kNRed * (NW + 1) + 10 * kLMax));
+  int32_t* lxi = reinterpret_cast<int32_t*>(cur);
+  int32_t* lyi = lxi + kLMax;
+  cur += align16(sizeof(int32_t) * 2 * kLMax);
+  MatView<MLDS> M;
+  if constexpr (MLDS) {
+    double* kv = reinterpret_cast<double*>(cur);
+    double* tv = kv + nnz;
+    cur += align16(sizeof(double) * 2 * (size_t)nnz);
+    int32_t* kp = reinterpret_cast<int32_t*>(cur);
+    int32_t* tp = kp + (m + 1);
+    cur += align16(sizeof(int32_t) * ((size_t)n + m + 2));
+    uint16_t* kc = reinterpret_cast<uint16_t*>(cur);
+    uint16_t* tc = kc + nnz;
+    const int32_t* gkp = b.indptr + W.row;
+    const int32_t* gkc = b.indices + W.nz;
+    const int32_t* gtp = w.tptr + W.wtr;
+    const int32_t* gtc = w.tind + W.wz;
+    const double* gkv = w.kval + W.wz;
+    const double* gtv = w.tval + W.wz;
+    for (int p = tid; p < nnz; p += B) {
+      kv[p] = gkv[p];
+      tv[p] = gtv[p];
+      kc[p] = (uint16_t)gkc[p];
+      tc[p] = (uint16_t)gtc[p];
+    }
+    for (int i = tid; i <= m; i += B) kp[i] = gkp[i];
+    for (int j = tid; j <= n; j += B) tp[j] = gtp[j];
+    M.kp = kp; M.kc = kc; M.kv = kv; M.tp = tp; M.tc = tc; M.tv = tv;
+  } else {
+    M.kp = b.indptr + W.row;
+    M.kc = b.indices + W.nz;
+    M.kv = w.kval + W.wz;
+    M.tp = w.tptr + W.wtr;
+    M.tc = w.tind + W.wz;
+    M.tv = w.tval + W.wz;
+  }
+  const int32_t* glk = w.longk + (int64_t)kl * kLMax;
+  const int32_t* glt = w.longt + (int64_t)kl * kLMax;
+  const double* cs = w.cs + W.wn;
+  const double* ls = w.ls + W.wn;
+  const double* us = w.us + W.wn;
+  const double* qs = w.qs + W.wm;
+  const double* dcv = w.dc + W.wn;
+  const double* drv = w.dr + W.wm;
+  for (int L = tid; L < nlt; L += B) {
+    const int j = glt[L];
+    lxi[L] = j;
+    const double lo = ls[j], hi = us[j];
+    const double x0 = fmin(fmax(0.0, lo), hi);
+    lx[0 * kLMax + L] = x0;
+    lx[1 * kLMax + L] = x0;
+    lx[2 * kLMax + L] = cs[j];
+    lx[3 * kLMax + L] = lo;
+    lx[4 * kLMax + L] = hi;
+    lx[5 * kLMax + L] = x0;
+  }
+  for (int L = tid; L < nlk; L += B) {
+    const int i = glk[L];
+    lyi[L] = i;
+    ly[0 * kLMax + L] = 0.0;
+    ly[1 * kLMax + L] = 0.0;
+    ly[2 * kLMax + L] = qs[i];
+    ly[3 * kLMax + L] = 0.0;
+  }
+  __syncthreads();
+
+  // ---- register-resident state of the lane-owned (short) columns and rows
+  double x[XS], xa[XS], cc[XS], lo[XS], hi[XS];
+  double* xo_g = b.x + W.on;  // x+ (scaled) at check iterations, final unscaled x
+  double* yo_g = b.y + W.om;
+  int ts[XS], te[XS];
+#pragma unroll
+  for (int s = 0; s < XS; ++s) {
+    const int j = tid + s * B;
+    ts[s] = te[s] = 0;
+    x[s] = xa[s] = cc[s] = lo[s] = hi[s] = 0.0;
+    if (j < n) {
+      const int a0 = M.tp[j], a1 = M.tp[j + 1];
+      if (a1 - a0 <= kLongRow) {
+        ts[s] = a0;
+        te[s] = a1;
+        cc[s] = cs[j];
+        lo[s] = ls[j];
+        hi[s] = us[j];
+        x[s] = xa[s] = fmin(fmax(0.0, lo[s]), hi[s]);
+        xo_g[j] = x[s];
+      } else {
+        ts[s] = te[s] = -1;  // long column: owned by a wave
+      }
+    } else {
+      ts[s] = te[s] = -1;
+    }
+  }
+  double y[YS], ya[YS], qq[YS];
+  int ks[YS], ke[YS];
+#pragma unroll
+  for (int s = 0; s < YS; ++s) {
+    const int i = tid + s * B;
+    y[s] = ya[s] = qq[s] = 0.0;
+    ks[s] = ke[s] = -1;
+    if (i < m) {
+      const int a0 = M.kp[i], a1 = M.kp[i + 1];
+      if (a1 - a0 <= kLongRow) {
+        ks[s] = a0;
+        ke[s] = a1;
+        qq[s] = qs[i];
+        yo_g[i] = 0.0;
+      }
+      Y[i] = 0.0;
+    }
+  }
+  __syncthreads();
+
+  double eta = scal[0], pw = scal[1];
+  const double cnorm = scal[2], qnorm = scal[3], c0 = b.c0[k];
+  const double rho = o.rho;
+  int it = 0, kin = 0, status = kIterLimit;
+  double r0 = -1.0, rprev = -1.0;
+  double fin[4] = {NAN, NAN, NAN, NAN};  // obj, pres, dres, gap at the last check
+  const int chk = o.check_every > 0 ? o.check_every : 64;
+
+  while (it < o.max_iters) {
+    const double tau = eta / pw, sigma = eta * pw;
+    const bool check = ((it + 1) % chk) == 0;
+    const double ca = (kin + 1.0) / (kin + 2.0), cb = 1.0 / (kin + 2.0);
+    double acc[kNRed];
+#pragma unroll
+    for (int t = 0; t < kNRed; ++t) acc[t] = 0.0;
+    // ---------------- primal half-step: x+ = proj(x - tau (c - K'y)), X <- 2x+ - x
+#pragma unroll
+    for (int s = 0; s < XS; ++s) {
+      if (ts[s] >= 0) {
+        const int j = tid + s * B;
+        double kty = 0.0;
+        for (int p = ts[s]; p < te[s]; ++p) kty += M.tv[p] * Y[M.tc[p]];
+        const double p1 = fmin(fmax(x[s] - tau * (cc[s] - kty), lo[s]), hi[s]);
+        X[j] = 2.0 * p1 - x[s];
+        if (check) {
+          const double d = x[s] - p1, da = p1 - xa[s];
+          acc[0] += d * d;
+          acc[1] += da * da;
+          xo_g[j] = p1;
+        }
+        x[s] = ca * ((1.0 + rho) * p1 - rho * x[s]) + cb * xa[s];
+      }
+    }
+    for (int L = wid; L < nlt; L += NW) {
+      const int j = lxi[L];
+      double kty = 0.0;
+      for (int p = M.tp[j] + lane; p < M.tp[j + 1]; p += kWave) kty += M.tv[p] * Y[M.tc[p]];
+      kty = wave_sum(kty);
+      if (lane == 0) {
+        const double xo = lx[L], xan = lx[kLMax + L];
+        const double p1 = fmin(fmax(xo - tau * (lx[2 * kLMax + L] - kty), lx[3 * kLMax + L]), lx[4 * kLMax + L]);
+        X[j] = 2.0 * p1 - xo;
+        if (check) {
+          const double d = xo - p1, da = p1 - xan;
+          acc[0] += d * d;
+          acc[1] += da * da;
+          lx[5 * kLMax + L] = p1;
+        }
+        lx[L] = ca * ((1.0 + rho) * p1 - rho * xo) + cb * xan;
+      }
+    }
+    __syncthreads();
+    // ---------------- dual half-step: y+ = proj(y + sigma (q - K X)); Y <- Halpern(y)
+#pragma unroll
+    for (int s = 0; s < YS; ++s) {
+      if (ks[s] >= 0) {
+        const int i = tid + s * B;
+        double kx = 0.0;
+        for (int p = ks[s]; p < ke[s]; ++p) kx += M.kv[p] * X[M.kc[p]];
+        double p1 = y[s] + sigma * (qq[s] - kx);
+        if (i >= meq) p1 = fmax(p1, 0.0);
+        if (check) {
+          const double d = y[s] - p1, da = p1 - ya[s];
+          acc[2] += d * d;
+          acc[3] += da * da;
+          yo_g[i] = p1;
+        }
+        y[s] = ca * ((1.0 + rho) * p1 - rho * y[s]) + cb * ya[s];
+        Y[i] = y[s];
+      }
+    }
+    for (int L = wid; L < nlk; L += NW) {
+      const int i = lyi[L];
+      double kx = 0.0;
+      for (int p = M.kp[i] + lane; p < M.kp[i + 1]; p += kWave) kx += M.kv[p] * X[M.kc[p]];
+      kx = wave_sum(kx);
+      if (lane == 0) {
+        const double yo = ly[L], yan = ly[kLMax + L];
+        double p1 = yo + sigma * (ly[2 * kLMax + L] - kx);
+        if (i >= meq) p1 = fmax(p1, 0.0);
+        if (check) {
+          const double d = yo - p1, da = p1 - yan;
+          acc[2] += d * d;
+          acc[3] += da * da;
+          ly[3 * kLMax + L] = p1;
+        }
+        const double yn = ca * ((1.0 + rho) * p1 - rho * yo) + cb * yan;
+        ly[L] = yn;
+        Y[i] = yn;
+      }
+    }
+    ++it;
+    ++kin;
+    __syncthreads();
+    if (!check) continue;
+
+    // ---------------- check: KKT of T(z) = (x+, y+) in the unscaled space, restart test
+#pragma unroll
+    for (int s = 0; s < XS; ++s)
+      if (ts[s] >= 0) X[tid + s * B] = xo_g[tid + s * B];
+#pragma unroll
+    for (int s = 0; s < YS; ++s)
+      if (ks[s] >= 0) Y[tid + s * B] = yo_g[tid + s * B];
+    for (int L = tid; L < nlt; L += B) X[lxi[L]] = lx[5 * kLMax + L];
+    for (int L = tid; L < nlk; L += B) Y[lyi[L]] = ly[3 * kLMax + L];
+    __syncthreads();
+    // acc[4] = ||r_p||^2, acc[5] = ||r_d||^2, acc[6] = c'x, acc[7] = q'y, acc[8] = bound term
+    auto col_kkt = [&](int j, double kty, double cj, double loj, double hij, double xj) {
+      const double d = dcv[j];
+      const double rc = (cj - kty) / d;
+      const bool fl = isfinite(loj), fh = isfinite(hij);
+      const double lam = (fl && fh) ? rc : (fl ? fmax(rc, 0.0) : (fh ? fmin(rc, 0.0) : 0.0));
+      const double rd = rc - lam;
+      acc[5] += rd * rd;
+      acc[6] += cj * xj;
+      acc[8] += (fl ? loj * d * fmax(lam, 0.0) : 0.0) + (fh ? hij * d * fmin(lam, 0.0) : 0.0);
+    };
+    auto row_kkt = [&](int i, double kx, double qi, double yi) {
+      double r = (qi - kx) / drv[i];
+      if (i >= meq) r = fmax(r, 0.0);
+      acc[4] += r * r;
+      acc[7] += qi * yi;
+    };
+#pragma unroll
+    for (int s = 0; s < XS; ++s) {
+      if (ts[s] >= 0) {
+        double kty = 0.0;
+        for (int p = ts[s]; p < te[s]; ++p) kty += M.tv[p] * Y[M.tc[p]];
+        col_kkt(tid + s * B, kty, cc[s], lo[s], hi[s], X[tid + s * B]);
+      }
+    }
+    for (int L = wid; L < nlt; L += NW) {
+      const int j = lxi[L];
+      double kty = 0.0;
+      for (int p = M.tp[j] + lane; p < M.tp[j + 1]; p += kWave) kty += M.tv[p] * Y[M.tc[p]];
+      kty = wave_sum(kty);
+      if (lane == 0) col_kkt(j, kty, lx[2 * kLMax + L], lx[3 * kLMax + L], lx[4 * kLMax + L], lx[5 * kLMax + L]);
+    }
+#pragma unroll
+    for (int s = 0; s < YS; ++s) {
+      if (ks[s] >= 0) {
+        double kx = 0.0;
+        for (int p = ks[s]; p < ke[s]; ++p) kx += M.kv[p] * X[M.kc[p]];
+        row_kkt(tid + s * B, kx, qq[s], Y[tid + s * B]);
+      }
+    }
+    for (int L = wid; L < nlk; L += NW) {
+      const int i = lyi[L];
+      double kx = 0.0;
+      for (int p = M.kp[i] + lane; p < M.kp[i + 1]; p += kWave) kx += M.kv[p] * X[M.kc[p]];
+      kx = wave_sum(kx);
+      if (lane == 0) row_kkt(i, kx, ly[2 * kLMax + L], ly[3 * kLMax + L]);
+    }
+    block_sum<B, kNRed>(acc, red);
+    const double pobj = acc[6] + c0, dobj = acc[7] + acc[8] + c0;
+    const double pres = sqrt(acc[4]) / (1.0 + qnorm), dres = sqrt(acc[5]) / (1.0 + cnorm);
+    const double gap = fabs(pobj - dobj) / (1.0 + fabs(pobj) + fabs(dobj));
+    fin[0] = pobj;
+    fin[1] = pres;
+    fin[2] = dres;
+    fin[3] = gap;
+    if (pres <= o.eps && dres <= o.eps && gap <= o.eps) {
+      status = kOptimal;
+      break;
+    }
+    if (!(isfinite(pobj) && isfinite(dobj))) {
+      status = kNumerical;
+      break;
+    }
+    const double r = sqrt(pw * acc[0] + acc[2] / pw);
+    if (r0 < 0.0) r0 = r;
+    const bool restart = (r <= o.b_suff * r0) || (r <= o.b_nec * r0 && rprev >= 0.0 && r > rprev) ||
+                         ((double)kin >= o.b_art * (double)it);
+    if (restart) {
+      const double ddx = sqrt(acc[1]), ddy = sqrt(acc[3]);
+      if (ddx > 1e-10 && ddy > 1e-10) pw = exp(o.theta * log(ddy / ddx) + (1.0 - o.theta) * log(pw));
+#pragma unroll
+      for (int s = 0; s < XS; ++s)
+        if (ts[s] >= 0) x[s] = xa[s] = xo_g[tid + s * B];
+#pragma unroll
+      for (int s = 0; s < YS; ++s)
+        if (ks[s] >= 0) y[s] = ya[s] = yo_g[tid + s * B];
+      for (int L = tid; L < nlt; L += B) lx[L] = lx[kLMax + L] = lx[5 * kLMax + L];
+      for (int L = tid; L < nlk; L += B) ly[L] = ly[kLMax + L] = ly[3 * kLMax + L];
+      // Y already holds y+ = the new iterate
+      kin = 0;
+      r0 = r;
+      rprev = -1.0;
+    } else {
+      rprev = r;
+#pragma unroll
+      for (int s = 0; s < YS; ++s)
+        if (ks[s] >= 0) Y[tid + s * B] = y[s];
+      for (int L = tid; L < nlk; L += B) Y[lyi[L]] = ly[L];
+    }
+    __syncthreads();
+  }
+  // ---- outputs: the last checked candidate T(z), unscaled
+#pragma unroll
+  for (int s = 0; s < XS; ++s)
+    if (ts[s] >= 0) {
+      const int j = tid + s * B;
+      xo_g[j] *= dcv[j];
+    }
+  for (int L = tid; L < nlt; L += B) b.x[W.on + lxi[L]] = lx[5 * kLMax + L] * dcv[lxi[L]];
+#pragma unroll
+  for (int s = 0; s < YS; ++s)
+    if (ks[s] >= 0) {
+      const int i = tid + s * B;
+      yo_g[i] *= drv[i];
+    }
+  for (int L = tid; L < nlk; L += B) b.y[W.om + lyi[L]] = ly[3 * kLMax + L] * drv[lyi[L]];
+  if (tid == 0) {
+    b.istats[2 * k] = status;
+    b.istats[2 * k + 1] = it;
+    for (int t = 0; t < 4; ++t) b.stats[4 * k + t] = fin[t];
+  }
+}
+
+template <int B, int XS, int YS, bool MLDS>
+hipError_t launch_one(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, size_t lds, hipStream_t s) {
+  auto kern = pdhg_kernel<B, XS, YS, MLDS>;
+  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(kern, dim3(ch.count), dim3(B), lds, s, b, w, ch, o);
+  return hipGetLastError();
+}
+
+// 512-thread workgroups (8 waves, up to 256 VGPRs per lane): each lane owns up to 8 columns and 8 rows,
+// so windows with n, m <= 4096 run with the whole iterate in registers.
+template <bool MLDS>
+hipError_t dispatch_xy(int xs, int ys, const Batch& b, const Work& w, const Chunk& ch, const Opts& o, size_t lds,
+                       hipStream_t s) {
+  constexpr int B = 512;
+#define DVH_CASE(X_, Y_) \
+  if (xs <= X_ && ys <= Y_) return launch_one<B, X_, Y_, MLDS>(b, w, ch, o, lds, s);
+  DVH_CASE(1, 1)
+  DVH_CASE(2, 1)
+  DVH_CASE(2, 2)
+  DVH_CASE(3, 2)
+  DVH_CASE(4, 3)
+  DVH_CASE(5, 3)
+  DVH_CASE(5, 4)
+  DVH_CASE(6, 4)
+  DVH_CASE(8, 6)
+  DVH_CASE(8, 8)
+#undef DVH_CASE
+  return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+size_t setup_lds_bytes(int max_n) { return align16(sizeof(int32_t) * ((size_t)max_n + 1)); }
+
+hipError_t launch_setup(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n, hipStream_t s) {
+  const size_t lds = setup_lds_bytes(max_n);
+  hipError_t e = hipFuncSetAttribute((const void*)setup_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(setup_kernel, dim3(ch.count), dim3(kSetupB), lds, s, b, w, ch, o);
+  return hipGetLastError();
+}
+
+hipError_t launch_pdhg(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n, int max_m,
+                       int64_t max_nnz, hipStream_t s, int* variant_out) {
+  constexpr int B = 512;
+  constexpr size_t kLdsCap = 160 * 1024;
+  const int xs = (max_n + B - 1) / B, ys = (max_m + B - 1) / B;
+  if (xs > 8 || ys > 8) return hipErrorInvalidValue;
+  const size_t lds_m = pdhg_lds_bytes(max_n, max_m, (int)max_nnz, true, B / kWave);
+  const bool mlds = lds_m <= kLdsCap && max_n < 65536 && max_m < 65536;
+  const size_t lds = mlds ? lds_m : pdhg_lds_bytes(max_n, max_m, 0, false, B / kWave);
+  if (lds > kLdsCap) return hipErrorInvalidValue;
+  if (variant_out) *variant_out = (mlds ? 1000 : 0) + xs * 10 + ys;
+  return mlds ? dispatch_xy<true>(xs, ys, b, w, ch, o, lds, s) : dispatch_xy<false>(xs, ys, b, w, ch, o, lds, s);
+}
+
+}  // namespace dvh

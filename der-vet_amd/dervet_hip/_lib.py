@@ -1,0 +1,96 @@
+"""ctypes binding of libdervet_hip (include/dervet_hip.h).
+
+The library is the product path: there is no CPU fallback.  Loading fails loudly when the shared object
+is missing, and every solve fails loudly when no GPU is present.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libdervet_hip.so")
+
+DVH_OK, DVH_ERR_ARG, DVH_ERR_HIP, DVH_ERR_UNSUPPORTED = 0, -1, -2, -3
+OPTIMAL, PRIMAL_INFEASIBLE, DUAL_INFEASIBLE, ITER_LIMIT, NUMERICAL = 0, 1, 2, 3, 4
+STATUS_NAMES = {OPTIMAL: "optimal", PRIMAL_INFEASIBLE: "infeasible", DUAL_INFEASIBLE: "unbounded",
+                ITER_LIMIT: "optimal_inaccurate", NUMERICAL: "solver_error"}
+
+c_int32_p = ctypes.POINTER(ctypes.c_int32)
+c_double_p = ctypes.POINTER(ctypes.c_double)
+c_int64_p = ctypes.POINTER(ctypes.c_int64)
+
+
+class Options(ctypes.Structure):
+    _fields_ = [("eps", ctypes.c_double), ("max_iters", ctypes.c_int32), ("check_every", ctypes.c_int32),
+                ("ruiz_iters", ctypes.c_int32), ("power_iters", ctypes.c_int32), ("step_safety", ctypes.c_double),
+                ("reflection", ctypes.c_double), ("restart_sufficient", ctypes.c_double),
+                ("restart_necessary", ctypes.c_double), ("restart_artificial", ctypes.c_double),
+                ("primal_weight_theta", ctypes.c_double), ("verbose", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 7)]
+
+
+class LP(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int32), ("m_eq", ctypes.c_int32), ("m_ineq", ctypes.c_int32), ("nnz", ctypes.c_int32),
+                ("indptr", c_int32_p), ("indices", c_int32_p), ("data", c_double_p), ("c", c_double_p),
+                ("c0", ctypes.c_double), ("q", c_double_p), ("l", c_double_p), ("u", c_double_p),
+                ("structure", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class Result(ctypes.Structure):
+    _fields_ = [("x", c_double_p), ("y", c_double_p), ("obj", ctypes.c_double), ("primal_res_rel", ctypes.c_double),
+                ("dual_res_rel", ctypes.c_double), ("gap_rel", ctypes.c_double), ("status", ctypes.c_int32),
+                ("iters", ctypes.c_int32)]
+
+
+class Packed(ctypes.Structure):
+    _fields_ = [("count", ctypes.c_int32), ("reserved", ctypes.c_int32), ("total_n", ctypes.c_int64),
+                ("total_m", ctypes.c_int64), ("total_nnz", ctypes.c_int64), ("total_rows", ctypes.c_int64),
+                ("desc", ctypes.c_void_p), ("indptr", ctypes.c_void_p), ("indices", ctypes.c_void_p),
+                ("data", ctypes.c_void_p), ("c", ctypes.c_void_p), ("c0", ctypes.c_void_p), ("q", ctypes.c_void_p),
+                ("l", ctypes.c_void_p), ("u", ctypes.c_void_p), ("x", ctypes.c_void_p), ("y", ctypes.c_void_p),
+                ("stats", ctypes.c_void_p), ("istats", ctypes.c_void_p)]
+
+
+# symbol -> (restype, argtypes); every symbol declared in include/dervet_hip.h
+SYMBOLS = {
+    "dvh_version": (ctypes.c_char_p, []),
+    "dvh_default_options": (None, [ctypes.POINTER(Options)]),
+    "dvh_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(Options), ctypes.POINTER(ctypes.c_void_p)]),
+    "dvh_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "dvh_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
+    "dvh_set_options": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Options)]),
+    "dvh_solve_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(LP), ctypes.c_int32, ctypes.POINTER(Result)]),
+    "dvh_solve_packed_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Packed), ctypes.c_void_p]),
+    "dvh_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
+    "dvh_last_timing": (ctypes.c_int, [ctypes.c_void_p, c_double_p]),
+}
+
+_lib = None
+
+
+def load(path=None):
+    """Load libdervet_hip.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise RuntimeError(f"libdervet_hip.so not found at {p}: build it with `python -m dervet_hip.build` "
+                           "(there is no CPU fallback)")
+    lib = ctypes.CDLL(p)
+    for name, (res, args) in SYMBOLS.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def default_options(**kw):
+    o = Options()
+    load().dvh_default_options(ctypes.byref(o))
+    for k, v in kw.items():
+        if not hasattr(o, k):
+            raise KeyError(f"unknown option {k}")
+        setattr(o, k, v)
+    return o

@@ -1,0 +1,164 @@
+"""Host-side API over libdervet_hip: batch solve of window LPs.
+
+``BatchSolver.solve(lps)`` is the batched replacement of the per-window
+``storagevet Scenario.solve_optimization(functions, constraints)`` call made at
+``dervet/MicrogridScenario.py:319``: it takes every window's canonical LP (CSR K with equality rows first,
+then >= rows; c, c0, q, l, u) and returns per-window primal/dual solutions, objective and status.
+``BatchSolver.solve_packed`` runs a batch that is already resident in HBM (torch tensors), which is what
+``bench.py`` times.
+"""
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+
+
+@dataclass
+class WindowLP:
+    """One window's LP:  min c'x + c0  s.t.  K[:m_eq] x = q[:m_eq],  K[m_eq:] x >= q[m_eq:],  l <= x <= u."""
+    indptr: np.ndarray
+    indices: np.ndarray
+    data: np.ndarray
+    c: np.ndarray
+    q: np.ndarray
+    l: np.ndarray
+    u: np.ndarray
+    m_eq: int
+    c0: float = 0.0
+    structure: int = 0
+    meta: dict = field(default_factory=dict)
+
+    @property
+    def n(self):
+        return len(self.c)
+
+    @property
+    def m(self):
+        return len(self.q)
+
+    @classmethod
+    def from_csr(cls, K, q, c, l, u, m_eq, c0=0.0, **kw):
+        K = K.tocsr()
+        K.sort_indices()
+        return cls(np.ascontiguousarray(K.indptr, np.int32), np.ascontiguousarray(K.indices, np.int32),
+                   np.ascontiguousarray(K.data, np.float64), np.ascontiguousarray(c, np.float64),
+                   np.ascontiguousarray(q, np.float64), np.ascontiguousarray(l, np.float64),
+                   np.ascontiguousarray(u, np.float64), int(m_eq), float(c0), **kw)
+
+
+@dataclass
+class WindowResult:
+    x: np.ndarray
+    y: np.ndarray
+    obj: float
+    status: int
+    iters: int
+    primal_res_rel: float
+    dual_res_rel: float
+    gap_rel: float
+
+    @property
+    def status_name(self):
+        return _lib.STATUS_NAMES.get(self.status, "solver_error")
+
+
+class SolverError(RuntimeError):
+    pass
+
+
+class BatchSolver:
+    """One GPU, one HIP stream.  Options are dvh_options fields (eps, max_iters, ...)."""
+
+    def __init__(self, device=0, **options):
+        self._lib = _lib.load()
+        self._opts = _lib.default_options(**options)
+        h = ctypes.c_void_p()
+        rc = self._lib.dvh_create(1 << int(device), ctypes.byref(self._opts), ctypes.byref(h))
+        if rc != 0:
+            raise SolverError(f"dvh_create failed ({rc}): no usable GPU device {device} or invalid options")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.dvh_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc, what):
+        if rc != 0:
+            msg = self._lib.dvh_last_error(self._h)
+            raise SolverError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+    def set_options(self, **options):
+        for k, v in options.items():
+            setattr(self._opts, k, v)
+        self._check(self._lib.dvh_set_options(self._h, ctypes.byref(self._opts)), "dvh_set_options")
+
+    def timing(self):
+        t = (ctypes.c_double * 3)()
+        self._check(self._lib.dvh_last_timing(self._h, t), "dvh_last_timing")
+        return {"total_ms": t[0], "setup_ms": t[1], "pdhg_ms": t[2]}
+
+    def solve(self, lps):
+        """Solve a list of WindowLP on the GPU; returns a list of WindowResult (same order)."""
+        count = len(lps)
+        if count == 0:
+            return []
+        keep = []
+        arr = (_lib.LP * count)()
+        res = (_lib.Result * count)()
+        outs = []
+
+        def ptr(a, t, ct):
+            a = np.ascontiguousarray(a, dtype=t)
+            keep.append(a)
+            return a.ctypes.data_as(ct)
+
+        for k, lp in enumerate(lps):
+            m = lp.m
+            if len(lp.indptr) != m + 1:
+                raise ValueError(f"window {k}: indptr has {len(lp.indptr)} entries, expected m+1={m + 1}")
+            L = arr[k]
+            L.n, L.m_eq, L.m_ineq, L.nnz = lp.n, lp.m_eq, m - lp.m_eq, len(lp.indices)
+            L.indptr = ptr(lp.indptr, np.int32, _lib.c_int32_p)
+            L.indices = ptr(lp.indices, np.int32, _lib.c_int32_p)
+            L.data = ptr(lp.data, np.float64, _lib.c_double_p)
+            L.c = ptr(lp.c, np.float64, _lib.c_double_p)
+            L.q = ptr(lp.q, np.float64, _lib.c_double_p)
+            L.l = ptr(lp.l, np.float64, _lib.c_double_p)
+            L.u = ptr(lp.u, np.float64, _lib.c_double_p)
+            L.c0 = lp.c0
+            L.structure = lp.structure
+            x = np.empty(lp.n)
+            y = np.empty(m)
+            outs.append((x, y))
+            res[k].x = x.ctypes.data_as(_lib.c_double_p)
+            res[k].y = y.ctypes.data_as(_lib.c_double_p) if m else None
+        self._check(self._lib.dvh_solve_batch(self._h, arr, count, res), "dvh_solve_batch")
+        return [WindowResult(outs[k][0], outs[k][1], res[k].obj, res[k].status, res[k].iters, res[k].primal_res_rel,
+                             res[k].dual_res_rel, res[k].gap_rel) for k in range(count)]
+
+    def solve_packed(self, pb, stream=None, sync=True):
+        """Solve a device-resident packed batch (``dervet_hip.packed.PackedBatch`` of torch tensors)."""
+        p = pb.as_ctypes()
+        s = ctypes.c_void_p(stream) if stream else None
+        self._check(self._lib.dvh_solve_packed_device(self._h, ctypes.byref(p), s), "dvh_solve_packed_device")
+        if sync and stream:
+            self._check(self._lib.dvh_synchronize(self._h), "dvh_synchronize")
+
+
+def version():
+    return _lib.load().dvh_version().decode()

@@ -1,0 +1,148 @@
+/*
+ * dervet_hip.h -- C ABI of libdervet_hip, the MI355X batched dispatch-LP solver.
+ *
+ * Drop-in boundary.  In the reference every optimization window is solved by
+ *   storagevet Scenario.solve_optimization(functions, constraints) -> (cvx_problem, obj_expressions, cvx_error_msg)
+ * called once per window from the serial loop at dervet/MicrogridScenario.py:310-320 (optimize_problem_loop,
+ * :281), i.e. CVXPY 1.0.31 canonicalisation + ECOS 2.0.7 / GLPK (cvxopt 1.2.5) in C (requirements.txt:1,2,5).
+ * This library replaces that solve for LP windows: the caller exports every window's canonical LP
+ *     min c'x + c0   s.t.  K_E x = q_E,  K_I x >= q_I,  l <= x <= u      (rows ordered E then I)
+ * and solves all windows of all scenarios as ONE batch with a restarted reflected-Halpern PDHG
+ * (PDLP family) in hand-written HIP for gfx950.  No pointers are retained after a call returns.
+ *
+ * Entry point  <->  reference interface it replaces
+ *   dvh_create / dvh_destroy   : solver construction (cvx.Problem(...).solve(solver=...) picks ECOS/GLPK;
+ *                                storagevet Scenario.solve_optimization, called at MicrogridScenario.py:319)
+ *   dvh_solve_batch            : the per-window prob.solve() of MicrogridScenario.py:319, for `count`
+ *                                windows at once (host buffers in / out)
+ *   dvh_solve_packed_device    : same, on a batch already resident in HBM (bench / torch callers)
+ *   dvh_last_error             : cvx_error_msg (errors travel as a message, MicrogridScenario.py:319-320)
+ *   result.status              : maps to the cvxpy status strings read by save_optimization_results
+ *                                (MicrogridScenario.py:348-363): OPTIMAL->"optimal",
+ *                                PRIMAL_INFEASIBLE->"infeasible", DUAL_INFEASIBLE->"unbounded",
+ *                                ITER_LIMIT->"optimal_inaccurate", NUMERICAL->"solver_error".
+ *
+ * Threading: one handle per host thread.  A handle drives one GPU (the lowest set bit of device_mask);
+ * multi-GPU runs use one process (rank) per GPU, each with its own handle.
+ * Return codes: 0 = OK, negative = usage / HIP error (message via dvh_last_error).
+ */
+#ifndef DERVET_HIP_H
+#define DERVET_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DVH_OK 0
+#define DVH_ERR_ARG (-1)
+#define DVH_ERR_HIP (-2)
+#define DVH_ERR_UNSUPPORTED (-3)
+
+/* per-window status */
+#define DVH_OPTIMAL 0
+#define DVH_PRIMAL_INFEASIBLE 1
+#define DVH_DUAL_INFEASIBLE 2
+#define DVH_ITER_LIMIT 3
+#define DVH_NUMERICAL 4
+
+/* structure hints (dvh_lp.structure) */
+#define DVH_STRUCT_GENERIC_CSR 0
+#define DVH_STRUCT_BATTERY_BANDED 1
+
+typedef struct dvh_options {
+  double eps;                 /* relative KKT tolerance (primal, dual, gap), default 1e-6          */
+  int32_t max_iters;          /* per window, default 200000                                       */
+  int32_t check_every;        /* restart / termination check period, default 64                   */
+  int32_t ruiz_iters;         /* Ruiz equilibration passes, default 10                            */
+  int32_t power_iters;        /* power-iteration steps for ||K||_2, default 64                    */
+  double step_safety;         /* eta = step_safety / ||K||_2, default 0.998                       */
+  double reflection;          /* Halpern reflection rho in [0,1], default 1                       */
+  double restart_sufficient;  /* default 0.2  */
+  double restart_necessary;   /* default 0.8  */
+  double restart_artificial;  /* default 0.36 */
+  double primal_weight_theta; /* default 0.5  */
+  int32_t verbose;            /* 0 silent                                                           */
+  int32_t reserved[7];
+} dvh_options;
+
+typedef struct dvh_lp {
+  int32_t n;                  /* variables                          */
+  int32_t m_eq;               /* equality rows (first)              */
+  int32_t m_ineq;             /* >= rows (after the equalities)     */
+  int32_t nnz;
+  const int32_t* indptr;      /* [m_eq + m_ineq + 1] CSR row pointers (0-based)                  */
+  const int32_t* indices;     /* [nnz] column indices                                           */
+  const double* data;         /* [nnz]                                                          */
+  const double* c;            /* [n] objective                                                  */
+  double c0;                  /* objective constant                                             */
+  const double* q;            /* [m] right-hand side                                            */
+  const double* l;            /* [n] lower bounds (-INFINITY allowed)                           */
+  const double* u;            /* [n] upper bounds (+INFINITY allowed)                           */
+  int32_t structure;          /* DVH_STRUCT_* hint (informational)                              */
+  int32_t reserved;
+} dvh_lp;
+
+typedef struct dvh_result {
+  double* x;                  /* caller-allocated [n] or NULL                                   */
+  double* y;                  /* caller-allocated [m] or NULL (duals; >= rows have y >= 0)       */
+  double obj;                 /* c'x + c0                                                       */
+  double primal_res_rel;      /* ||(q - Kx)_proj||_2 / (1 + ||q||_2)                            */
+  double dual_res_rel;        /* ||c - K'y - lambda||_2 / (1 + ||c||_2)                         */
+  double gap_rel;             /* |pobj - dobj| / (1 + |pobj| + |dobj|)                          */
+  int32_t status;             /* DVH_OPTIMAL ...                                                */
+  int32_t iters;
+} dvh_result;
+
+/* A batch already resident in device memory ("packed" layout).
+ * desc[8*k + 0..7] = {n, m, m_eq, nnz, off_row, off_nz, off_n, off_m} (int64) for window k:
+ *   indptr[off_row .. off_row+m]   (window-local row pointers, int32)
+ *   indices/data[off_nz .. +nnz]   (window-local column indices int32 / values f64)
+ *   c,l,u[off_n .. +n], q[off_m .. +m], c0[k]
+ * Outputs: x[off_n..], y[off_m..], stats[4k..4k+3] = {obj, primal_res_rel, dual_res_rel, gap_rel},
+ *          istats[2k..2k+1] = {status, iters}.  All pointers are device pointers. */
+typedef struct dvh_packed {
+  int32_t count;
+  int32_t reserved;
+  int64_t total_n, total_m, total_nnz, total_rows; /* sizes of the concatenated arrays (rows = sum(m+1)) */
+  const int64_t* desc;
+  const int32_t* indptr;
+  const int32_t* indices;
+  const double* data;
+  const double* c;
+  const double* c0;
+  const double* q;
+  const double* l;
+  const double* u;
+  double* x;
+  double* y;
+  double* stats;
+  int32_t* istats;
+} dvh_packed;
+
+typedef struct dvh_handle dvh_handle;
+
+const char* dvh_version(void);
+void dvh_default_options(dvh_options* opts);
+int dvh_create(int device_mask, const dvh_options* opts, dvh_handle** out);
+int dvh_destroy(dvh_handle* h);
+const char* dvh_last_error(const dvh_handle* h);
+int dvh_set_options(dvh_handle* h, const dvh_options* opts);
+
+/* Host buffers in / out.  Blocks until the batch is solved. */
+int dvh_solve_batch(dvh_handle* h, const dvh_lp* lps, int32_t count, dvh_result* out);
+
+/* Device-resident batch; `stream` is a hipStream_t (NULL = the handle's own stream).  Asynchronous
+ * w.r.t. the host when stream != NULL; call dvh_synchronize / hipStreamSynchronize before reading. */
+int dvh_solve_packed_device(dvh_handle* h, const dvh_packed* batch, void* stream);
+int dvh_synchronize(dvh_handle* h);
+
+/* Timing of the most recent solve on the handle's stream (HIP events, milliseconds):
+ * [0] whole solve, [1] setup kernel (transpose + scaling + power iteration), [2] PDHG kernel. */
+int dvh_last_timing(const dvh_handle* h, double* ms3);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DERVET_HIP_H */

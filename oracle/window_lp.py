@@ -1,0 +1,197 @@
+"""ORACLE (test infrastructure only): restated per-window dispatch LP + HiGHS solve.
+
+Restates what storagevet's ``Scenario.set_up_optimization`` builds for one optimization window and what
+``Scenario.solve_optimization`` (called at ``dervet/MicrogridScenario.py:319``) solves, for the in-scope
+DER / value-stream set:
+
+  objective terms (one per key of the ``functions`` dict):
+    retailETS       = sum_t p_t dt (L_t - G_t + ch_t - dis_t)                (pinned, Appendix B P1-P3)
+    DCM             = sum_j d_j tau_j,  tau_j >= net_t for t in M_j          (pinned)
+    DA              = sum_t pi_t dt (net_t)  (= -pi dt (dis - ch) with no load) (evaluation pinned, P9)
+    <es> fixed_om   = fixedOM * P_dis (constant every window)                 (pinned, ESSSizing.py:265-278)
+    <es> var_om     = OMexpenses/1000 * dt * sum dis                          (UNPINNED: 0 in goldens)
+  constraints:
+    ene_0 = target;  ene_{t+1} = ene_t + dt (eta ch_t - dis_t) - dt sdr/100 ene_t;  final step reaches target
+    max(llsoc E, a_min_t) <= ene_t <= min(ulsoc E, a_max_t);  0 <= ch <= P_ch;  0 <= dis <= P_dis
+  optional (unpinned): curtailable PV 0 <= pv_t <= pv_max_t; LP-relaxed ICE (elec_t, on_t in [0,1]).
+
+Variable order: [ch(T), dis(T), ene(T), tau(J), pv(T)?, elec(T)?, on(T)?].  Rows: equalities then >= rows.
+This per-window scipy.sparse restatement is deliberately independent of the product's vectorised
+batch builder (``der-vet_amd/dervet_hip/lp/builder.py``); tests compare the two.
+"""
+import numpy as np
+import scipy.sparse as sp
+from scipy.optimize import linprog
+
+
+def build(win):
+    """win: dict with keys
+         T, dt, load (L_t, kW), gen (fixed generation G_t, kW), retail_price (or None), da_price (or None),
+         demand: list of (d_j $/kW, bool mask length T), ene_min, ene_max (arrays or None),
+         bat: dict(E, Pch, Pdis, rte, sdr, soc_target, ulsoc, llsoc, fixedOM, OMexpenses, hp, name),
+         pv_curtail_max (array or None), ice (dict or None).
+    Returns dict(K csr, q, c, c0, l, u, m_eq, funcs{name: (coef, const)}, layout)."""
+    T = int(win["T"])
+    dt = float(win["dt"])
+    b = win["bat"]
+    E, pch, pdis = float(b["E"]), float(b["Pch"]), float(b["Pdis"])
+    eta, sdr = float(b["rte"]), float(b["sdr"]) / 100.0
+    target = float(b["soc_target"]) * E
+    demand = [(float(d), np.asarray(m, bool)) for d, m in win.get("demand", []) if np.any(m)]
+    J = len(demand)
+    pvmax = win.get("pv_curtail_max")
+    ice = win.get("ice")
+    off = {"ch": 0, "dis": T, "ene": 2 * T, "tau": 3 * T}
+    n = 3 * T + J
+    if pvmax is not None:
+        off["pv"] = n
+        n += T
+    if ice is not None:
+        off["elec"] = n
+        off["on"] = n + T
+        n += 2 * T
+    hp = float(b.get("hp", 0.0))
+    base = np.asarray(win["load"], float) - np.asarray(win.get("gen", np.zeros(T)), float) + hp
+
+    # net_t = base_t + ch_t - dis_t - pv_t - elec_t, as (coef rows over x, const)
+    def net_coefs(t):
+        cols = [off["ch"] + t, off["dis"] + t]
+        vals = [1.0, -1.0]
+        if pvmax is not None:
+            cols.append(off["pv"] + t)
+            vals.append(-1.0)
+        if ice is not None:
+            cols.append(off["elec"] + t)
+            vals.append(-1.0)
+        return cols, vals
+
+    rows, cols, vals, q = [], [], [], []
+    r = 0
+    # equality rows: ene_0 = target
+    rows.append(r); cols.append(off["ene"]); vals.append(1.0); q.append(target); r += 1
+    # recurrence t = 0..T-2:  ene_{t+1} - (1 - dt sdr) ene_t - dt eta ch_t + dt dis_t = 0
+    for t in range(T - 1):
+        rows += [r] * 4
+        cols += [off["ene"] + t + 1, off["ene"] + t, off["ch"] + t, off["dis"] + t]
+        vals += [1.0, -(1.0 - dt * sdr), -dt * eta, dt]
+        q.append(0.0)
+        r += 1
+    # final: (1 - dt sdr) ene_{T-1} + dt eta ch_{T-1} - dt dis_{T-1} = target
+    rows += [r] * 3
+    cols += [off["ene"] + T - 1, off["ch"] + T - 1, off["dis"] + T - 1]
+    vals += [1.0 - dt * sdr, dt * eta, -dt]
+    q.append(target)
+    r += 1
+    m_eq = r
+    # >= rows: tau_j - (ch - dis - pv - elec)_t >= base_t   for t in M_j
+    for j, (d, mask) in enumerate(demand):
+        for t in np.nonzero(mask)[0]:
+            cc, vv = net_coefs(t)
+            rows += [r] * (1 + len(cc))
+            cols += [off["tau"] + j] + cc
+            vals += [1.0] + [-v for v in vv]
+            q.append(base[t])
+            r += 1
+    if ice is not None:
+        # elec_t <= rated*n*on_t  ->  rated*n*on_t - elec_t >= 0 ; elec_t >= min_power*n*on_t
+        cap = float(ice["rated_power"]) * float(ice["n"])
+        pmin = float(ice["min_power"]) * float(ice["n"])
+        for t in range(T):
+            rows += [r, r]; cols += [off["on"] + t, off["elec"] + t]; vals += [cap, -1.0]; q.append(0.0); r += 1
+            rows += [r, r]; cols += [off["elec"] + t, off["on"] + t]; vals += [1.0, -pmin]; q.append(0.0); r += 1
+    m = r
+    K = sp.csr_matrix((vals, (rows, cols)), shape=(m, n))
+    K.sum_duplicates()
+
+    lo = np.zeros(n)
+    hi = np.full(n, np.inf)
+    hi[off["ch"]:off["ch"] + T] = pch
+    hi[off["dis"]:off["dis"] + T] = pdis
+    elo = np.full(T, float(b.get("llsoc", 0.0)) * E)
+    ehi = np.full(T, float(b.get("ulsoc", 1.0)) * E)
+    if win.get("ene_min") is not None:
+        elo = np.maximum(elo, np.asarray(win["ene_min"], float))
+    if win.get("ene_max") is not None:
+        ehi = np.minimum(ehi, np.asarray(win["ene_max"], float))
+    lo[off["ene"]:off["ene"] + T] = elo
+    hi[off["ene"]:off["ene"] + T] = ehi
+    lo[off["tau"]:off["tau"] + J] = -np.inf
+    if pvmax is not None:
+        hi[off["pv"]:off["pv"] + T] = np.asarray(pvmax, float)
+    if ice is not None:
+        hi[off["on"]:off["on"] + T] = 1.0
+
+    funcs = {}
+
+    def net_term(price):
+        coef = np.zeros(n)
+        coef[off["ch"]:off["ch"] + T] = price * dt
+        coef[off["dis"]:off["dis"] + T] = -price * dt
+        if pvmax is not None:
+            coef[off["pv"]:off["pv"] + T] = -price * dt
+        if ice is not None:
+            coef[off["elec"]:off["elec"] + T] = -price * dt
+        return coef, float(np.sum(price * dt * base))
+
+    if win.get("da_price") is not None:
+        funcs["DA"] = net_term(np.asarray(win["da_price"], float))
+    if J:
+        coef = np.zeros(n)
+        coef[off["tau"]:off["tau"] + J] = [d for d, _ in demand]
+        funcs["DCM"] = (coef, 0.0)
+    if win.get("retail_price") is not None:
+        funcs["retailETS"] = net_term(np.asarray(win["retail_price"], float))
+    name = b.get("name", "es")
+    funcs[f"{name} fixed_om"] = (np.zeros(n), float(b.get("fixedOM", 0.0)) * pdis)
+    coef = np.zeros(n)
+    coef[off["dis"]:off["dis"] + T] = float(b.get("OMexpenses", 0.0)) / 1000.0 * dt
+    funcs[f"{name} var_om"] = (coef, 0.0)
+    if ice is not None:
+        coef = np.zeros(n)
+        coef[off["elec"]:off["elec"] + T] = (float(ice["efficiency"]) * float(ice["fuel_cost"])
+                                             + float(ice.get("variable_om_cost", 0.0))) * dt
+        funcs["ice fuel_cost"] = (coef, 0.0)
+
+    c = np.zeros(n)
+    c0 = 0.0
+    for coef, const in funcs.values():
+        c += coef
+        c0 += const
+    return dict(K=K, q=np.asarray(q, float), c=c, c0=c0, l=lo, u=hi, m_eq=m_eq, funcs=funcs, layout=off,
+                T=T, J=J)
+
+
+def solve_highs(lp, tol=1e-9):
+    """Solve the restated LP with HiGHS (scipy).  Returns dict(x, obj, status, terms)."""
+    K, q, m_eq = lp["K"], lp["q"], lp["m_eq"]
+    A_eq, b_eq = K[:m_eq], q[:m_eq]
+    A_ub, b_ub = -K[m_eq:], -q[m_eq:]
+    bounds = np.stack([np.where(np.isfinite(lp["l"]), lp["l"], -np.inf),
+                       np.where(np.isfinite(lp["u"]), lp["u"], np.inf)], axis=1)
+    bounds = [(None if not np.isfinite(a) else a, None if not np.isfinite(b) else b) for a, b in bounds]
+    res = linprog(lp["c"], A_ub=A_ub if A_ub.shape[0] else None, b_ub=b_ub if A_ub.shape[0] else None,
+                  A_eq=A_eq, b_eq=b_eq, bounds=bounds, method="highs",
+                  options={"primal_feasibility_tolerance": tol, "dual_feasibility_tolerance": tol})
+    out = dict(status=res.status, message=res.message)
+    if res.status == 0:
+        x = res.x
+        out["x"] = x
+        out["obj"] = float(lp["c"] @ x + lp["c0"])
+        out["terms"] = {k: float(coef @ x + const) for k, (coef, const) in lp["funcs"].items()}
+        # duals (scipy sign convention: eqlin.marginals = d obj / d b_eq; ineqlin for A_ub x <= b_ub)
+        y = np.concatenate([res.eqlin.marginals, -res.ineqlin.marginals if A_ub.shape[0] else np.zeros(0)])
+        out["y"] = y
+    return out
+
+
+def evaluate_terms(lp, x):
+    return {k: float(coef @ x + const) for k, (coef, const) in lp["funcs"].items()}
+
+
+def primal_residual_rel(lp, x):
+    """PDLP-convention relative primal residual ||(q - Kx) projected||_2 / (1 + ||q||_2) and abs l_inf."""
+    r = lp["q"] - lp["K"] @ x
+    r[lp["m_eq"]:] = np.maximum(r[lp["m_eq"]:], 0.0)
+    bv = np.maximum(lp["l"] - x, 0) + np.maximum(x - lp["u"], 0)
+    return (float(np.sqrt(r @ r + bv @ bv)) / (1.0 + float(np.linalg.norm(lp["q"]))),
+            float(max(np.abs(r).max(initial=0), bv.max(initial=0))))

@@ -1,0 +1,151 @@
+"""Extract small golden fixtures from the reference's own test data (run in the build container only).
+
+This script reads CSV *data* files shipped in the reference's test tree and data/ folder and writes
+compact numpy/JSON fixtures.  It never imports or executes reference code (the reference cannot be
+imported here: storagevet, cvxpy, ecos and cvxopt are absent -- SURVEY.md section 0).
+
+Sources (all paths relative to /root/reference):
+  * test/test_validation_report_sept1/datasets/uc2/<case>/hourly_timeseries_ref_<case>_step2.csv  (inputs)
+  * test/test_validation_report_sept1/Results/Usecase2/<case>/step2/objective_values*.csv         (golden per-window objective)
+  * test/test_validation_report_sept1/Results/Usecase2/<case>/step2/timeseries_results*.csv       (golden dispatch + tariff price)
+  * test/test_validation_report_sept1/Model_params/Usecase2/Model_Parameters_Template_Usecase3_*_Step2.csv (params)
+  * test/test_validation_report_sept1/datasets/tariff_refernce_case_1.csv                        (tariff)
+  * data/multi_der_hourly_timeseries.csv, data/hourly_timeseries.csv, data/tariff.csv              (bench inputs)
+  * test/datasets/000-004-timeseries_5min_negprices.csv                                           (config-3 input)
+
+Usage:  python tests/golden/make_fixtures.py [/root/reference]
+"""
+import csv
+import json
+import os
+import sys
+
+import numpy as np
+
+REF = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_DATA = os.path.join(HERE, "..", "..", "der-vet_amd", "dervet_hip", "data")
+VR = os.path.join(REF, "test", "test_validation_report_sept1")
+
+CASES = {
+    # name: (input ts csv, results dir, result suffix, model params csv)
+    "es": ("datasets/uc2/es/hourly_timeseries_ref_es_step2.csv", "Results/Usecase2/es/step2", "uc3_es_step2",
+           "Model_params/Usecase2/Model_Parameters_Template_Usecase3_Planned_ES_Step2.csv"),
+    "es+pv+dg": ("datasets/uc2/es+pv+dg/hourly_timeseries_ref_es+pv+dg_step2.csv", "Results/Usecase2/es+pv+dg/step2",
+                 "uc3_es+pv+dg_step2",
+                 "Model_params/Usecase2/Model_Parameters_Template_Usecase3_UnPlanned_ES+PV+DG_Step2.csv"),
+    "es+pv": ("datasets/uc2/es+pv/hourly_timeseries_ref_es+pv_step2.csv", "Results/Usecase2/es+pv/step2",
+              "uc3_es+pv_step2", "Model_params/Usecase2/Model_Parameters_Template_Usecase3_UnPlanned_ES+PV_Step2.csv"),
+}
+
+
+def read_csv_cols(path):
+    with open(path, encoding="utf-8-sig") as f:
+        rows = list(csv.reader(f))
+    head = [h.strip() for h in rows[0]]
+    cols = {h: [r[i] if i < len(r) else "" for r in rows[1:]] for i, h in enumerate(head)}
+    return head, cols
+
+
+def fcol(cols, name):
+    return np.array([float(v) if v.strip() != "" else np.nan for v in cols[name]], dtype=np.float64)
+
+
+def read_params(path):
+    """Active model parameters (Tag, Key) -> Optimization Value, from a model-parameter CSV."""
+    with open(path, encoding="utf-8-sig") as f:
+        rows = list(csv.DictReader(f))
+    # the Active flag is set on (at least) one row of a tag block; every row of an active tag applies
+    active = {r["Tag"].strip() for r in rows if r.get("Active", "").strip().lower() in ("yes", "y", "1")}
+    out = {}
+    for r in rows:
+        if r["Tag"].strip() in active and r["Key"] is not None:
+            out.setdefault(r["Tag"].strip(), {})[r["Key"].strip()] = (r["Optimization Value"] or "").strip()
+    return out
+
+
+def read_tariff(path):
+    _, c = read_csv_cols(path)
+    n = len(c["Billing Period"])
+
+    def num(v):
+        return float(v) if v.strip() != "" else np.nan
+    return {
+        "billing_period": [int(float(v)) for v in c["Billing Period"]],
+        "start_month": [int(float(v)) for v in c["Start Month"]],
+        "end_month": [int(float(v)) for v in c["End Month"]],
+        "start_time": [int(float(v)) for v in c["Start Time"]],
+        "end_time": [int(float(v)) for v in c["End Time"]],
+        "excl_start": [num(v) for v in c["Excluding Start Time"]],
+        "excl_end": [num(v) for v in c["Excluding End Time"]],
+        "weekday": [int(float(v)) for v in c["Weekday?"]],
+        "value": [float(v) for v in c["Value"]],
+        "charge": [c["Charge"][i].strip().lower() for i in range(n)],
+    }
+
+
+def make_golden_cases():
+    for name, (ts, resdir, suf, mp) in CASES.items():
+        _, inp = read_csv_cols(os.path.join(VR, ts))
+        _, gts = read_csv_cols(os.path.join(VR, resdir, f"timeseries_results{suf}.csv"))
+        _, gobj = read_csv_cols(os.path.join(VR, resdir, f"objective_values{suf}.csv"))
+        params = read_params(os.path.join(VR, mp))
+        keys = [k for k in gobj if k != ""]
+        obj = np.stack([fcol(gobj, k) for k in keys], axis=1)
+        bp = [v.strip("[]").split(",") for v in gts["Demand Charge Billing Periods"]]
+        bp = np.array([int(v[0]) if v[0].strip() else 0 for v in bp], dtype=np.int32)
+        arrays = dict(
+            site_load=fcol(inp, "Site Load (kW)"),
+            pv_profile=fcol(inp, "PV Gen (kW/rated kW)"),
+            agg_emin=fcol(inp, "Aggregate Energy Min (kWh)"),
+            agg_emax=fcol(inp, "Aggregate Energy Max (kWh)"),
+            golden_price=fcol(gts, "Tariff Energy Price ($/kWh)"),
+            golden_demand_period=bp,
+            golden_ch=fcol(gts, "BATTERY: es Charge (kW)"),
+            golden_dis=fcol(gts, "BATTERY: es Discharge (kW)"),
+            golden_ene=fcol(gts, "BATTERY: es State of Energy (kWh)"),
+            golden_netload=fcol(gts, "Net Load (kW)"),
+            golden_objective=obj,
+        )
+        np.savez_compressed(os.path.join(HERE, f"uc2_{name}.npz"), **arrays)
+        meta = {
+            "case": name,
+            "source_results": os.path.join("test/test_validation_report_sept1", resdir),
+            "objective_keys": keys,
+            "start": gts["Start Datetime (hb)"][0],
+            "params": {t: params[t] for t in ("Scenario", "Battery", "PV") if t in params},
+            "active_tags": sorted(params.keys()),
+            "tariff": read_tariff(os.path.join(VR, "datasets", "tariff_refernce_case_1.csv")),
+        }
+        with open(os.path.join(HERE, f"uc2_{name}.json"), "w") as f:
+            json.dump(meta, f, indent=1, sort_keys=True)
+        print("wrote", name, obj.shape)
+
+
+def make_bench_data():
+    os.makedirs(PKG_DATA, exist_ok=True)
+    _, md = read_csv_cols(os.path.join(REF, "data", "multi_der_hourly_timeseries.csv"))
+    _, hd = read_csv_cols(os.path.join(REF, "data", "hourly_timeseries.csv"))
+    _, fm = read_csv_cols(os.path.join(REF, "test", "datasets", "000-004-timeseries_5min_negprices.csv"))
+    np.savez_compressed(
+        os.path.join(PKG_DATA, "reference_inputs.npz"),
+        # config 2 / config 4 base scenario (data/multi_der_hourly_timeseries.csv, 2017 hourly)
+        multi_der_site_load=fcol(md, "Site Load (kW)"),
+        multi_der_pv_profile=fcol(md, "PV Gen (kW/rated kW)/1"),
+        # config 1 (data/hourly_timeseries.csv)
+        hourly_da_price=fcol(hd, "DA Price ($/kWh)"),
+        hourly_site_load=fcol(hd, "Site Load (kW)"),
+        # config 3 (test/datasets/000-004-timeseries_5min_negprices.csv, 2019 5-minute)
+        fivemin_da_price=fcol(fm, "DA Price ($/kWh)"),
+        fivemin_site_load=fcol(fm, "Site Load (kW)"),
+    )
+    with open(os.path.join(PKG_DATA, "tariff_data_tariff.json"), "w") as f:
+        json.dump(read_tariff(os.path.join(REF, "data", "tariff.csv")), f, indent=1)
+    with open(os.path.join(PKG_DATA, "tariff_reference_case_1.json"), "w") as f:
+        json.dump(read_tariff(os.path.join(VR, "datasets", "tariff_refernce_case_1.csv")), f, indent=1)
+    print("wrote bench data")
+
+
+if __name__ == "__main__":
+    make_golden_cases()
+    make_bench_data()
