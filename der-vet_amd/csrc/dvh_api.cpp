@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -41,7 +42,7 @@ struct DevBuf {
   T* as() const { return static_cast<T*>(p); }
 };
 
-constexpr int kChunkWindows = 32768;
+constexpr int kChunkWindows = 262144;
 
 }  // namespace
 
@@ -55,9 +56,13 @@ struct dvh_handle {
   // workspace
   DevBuf w_tptr, w_tind, w_tval, w_kval, w_rowof, w_perm, w_dr, w_dc, w_cs, w_ls, w_us, w_qs, w_vbuf, w_wbuf,
       w_tmpc, w_tmpr, w_longk, w_longt, w_scal;
+  DevBuf d_list;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  std::vector<std::array<hipEvent_t, 3>> chunk_events;
   double timing[3] = {0, 0, 0};
   int last_variant = -1;
+  int n_ell = 0, n_generic = 0;
+  bool disable_ell = false;
 };
 
 static int fail(dvh_handle* h, int code, const std::string& msg) {
@@ -84,15 +89,16 @@ void dvh_default_options(dvh_options* o) {
   std::memset(o, 0, sizeof(*o));
   o->eps = 1e-6;
   o->max_iters = 100000;
-  o->check_every = 64;
+  o->check_every = 16;
+  o->kkt_every = 4;
   o->ruiz_iters = 10;
   o->power_iters = 64;
   o->step_safety = 0.998;
   o->reflection = 1.0;
   o->restart_sufficient = 0.2;
   o->restart_necessary = 0.8;
-  o->restart_artificial = 0.36;
-  o->primal_weight_theta = 0.5;
+  o->restart_artificial = 0.1;
+  o->primal_weight_theta = 1.0;
   o->verbose = 0;
 }
 
@@ -100,6 +106,7 @@ static std::string check_options(const dvh_options* o) {
   if (!(o->eps > 0.0)) return "eps must be > 0";
   if (o->max_iters <= 0) return "max_iters must be > 0";
   if (o->check_every <= 0) return "check_every must be > 0";
+  if (o->kkt_every <= 0) return "kkt_every must be > 0";
   if (o->ruiz_iters < 0 || o->power_iters <= 0) return "ruiz_iters must be >= 0 and power_iters > 0";
   if (!(o->step_safety > 0.0 && o->step_safety < 1.0)) return "step_safety must be in (0, 1)";
   if (!(o->reflection >= 0.0 && o->reflection <= 1.0)) return "reflection must be in [0, 1]";
@@ -149,7 +156,7 @@ int dvh_destroy(dvh_handle* h) {
   hipSetDevice(h->device);
   if (h->stream) hipStreamSynchronize(h->stream);
   DevBuf* bufs[] = {&h->d_desc, &h->d_indptr, &h->d_indices, &h->d_data, &h->d_c, &h->d_c0, &h->d_q, &h->d_l,
-                    &h->d_u, &h->d_x, &h->d_y, &h->d_stats, &h->d_istats, &h->w_tptr, &h->w_tind, &h->w_tval,
+                    &h->d_u, &h->d_list, &h->d_x, &h->d_y, &h->d_stats, &h->d_istats, &h->w_tptr, &h->w_tind, &h->w_tval,
                     &h->w_kval, &h->w_rowof, &h->w_perm, &h->w_dr, &h->w_dc, &h->w_cs, &h->w_ls, &h->w_us,
                     &h->w_qs, &h->w_vbuf, &h->w_wbuf, &h->w_tmpc, &h->w_tmpr, &h->w_longk, &h->w_longt, &h->w_scal};
   for (DevBuf* b : bufs) b->release();
@@ -165,10 +172,21 @@ const char* dvh_last_error(const dvh_handle* h) { return h ? h->err.c_str() : "n
 int dvh_synchronize(dvh_handle* h) {
   if (!h) return DVH_ERR_ARG;
   DVH_HIP(h, hipStreamSynchronize(h->stream));
-  float a = 0, b = 0;
-  h->timing[0] = 0;
-  if (hipEventElapsedTime(&a, h->ev[0], h->ev[3]) == hipSuccess) h->timing[0] = a;
-  (void)b;
+  return DVH_OK;
+}
+
+int dvh_last_stats(const dvh_handle* h, int32_t* out4) {
+  if (!h || !out4) return DVH_ERR_ARG;
+  out4[0] = h->n_ell;
+  out4[1] = h->n_generic;
+  out4[2] = h->last_variant;
+  out4[3] = h->disable_ell ? 1 : 0;
+  return DVH_OK;
+}
+
+int dvh_set_kernel_path(dvh_handle* h, int generic_only) {
+  if (!h) return DVH_ERR_ARG;
+  h->disable_ell = generic_only != 0;
   return DVH_OK;
 }
 
@@ -193,6 +211,7 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
   o.theta = h->opts.primal_weight_theta;
   o.max_iters = h->opts.max_iters;
   o.check_every = h->opts.check_every;
+  o.kkt_every = h->opts.kkt_every;
   o.ruiz_iters = h->opts.ruiz_iters;
   o.power_iters = h->opts.power_iters;
   dvh::Batch b{bt->desc, bt->indptr, bt->indices, bt->data, bt->c, bt->c0, bt->q, bt->l, bt->u,
@@ -255,31 +274,82 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
               h->w_cs.as<double>(), h->w_ls.as<double>(), h->w_us.as<double>(), h->w_qs.as<double>(),
               h->w_vbuf.as<double>(), h->w_wbuf.as<double>(), h->w_tmpc.as<double>(), h->w_tmpr.as<double>(),
               h->w_longk.as<int32_t>(), h->w_longt.as<int32_t>(), h->w_scal.as<double>()};
-  const bool single = chunks.size() == 1;
+  DVH_HIP(h, h->d_list.ensure(I * (size_t)wc));
+  h->n_ell = h->n_generic = 0;
+  h->chunk_events.clear();
   DVH_HIP(h, hipEventRecord(h->ev[0], s));
+  std::vector<double> scal;
+  std::vector<int32_t> ist;
   for (const C& c : chunks) {
-    if (c.mn + 1 > 40000) return fail(h, DVH_ERR_UNSUPPORTED, "window with more than 40000 variables (large-LP path not built yet)");
+    if (c.mn + 1 > 40000)
+      return fail(h, DVH_ERR_UNSUPPORTED, "window with more than 40000 variables (large-LP path not built yet)");
+    hipEvent_t e0, e1, e2;
+    DVH_HIP(h, hipEventCreate(&e0));
+    DVH_HIP(h, hipEventCreate(&e1));
+    DVH_HIP(h, hipEventCreate(&e2));
+    h->chunk_events.push_back({e0, e1, e2});
+    DVH_HIP(h, hipEventRecord(e0, s));
     DVH_HIP(h, dvh::launch_setup(b, w, c.ch, o, c.mn, s));
-    if (single) DVH_HIP(h, hipEventRecord(h->ev[1], s));
+    DVH_HIP(h, hipEventRecord(e1, s));
+    // ELL widths from the setup statistics (one small D2H per chunk)
+    scal.resize((size_t)c.ch.count * dvh::kScal);
+    DVH_HIP(h, hipMemcpyAsync(scal.data(), w.scal, sizeof(double) * scal.size(), hipMemcpyDeviceToHost, s));
+    DVH_HIP(h, hipStreamSynchronize(s));
+    int wx = 0, wy = 0;
+    for (int k = 0; k < c.ch.count; ++k) {
+      const double* sc = &scal[(size_t)k * dvh::kScal];
+      if (sc[6] != 0.0) continue;
+      wy = std::max(wy, (int)sc[8]);
+      wx = std::max(wx, (int)sc[9]);
+    }
     int variant = -1;
-    hipError_t e = dvh::launch_pdhg(b, w, c.ch, o, c.mn, c.mm, c.mnz, s, &variant);
-    if (e == hipErrorInvalidValue)
-      return fail(h, DVH_ERR_UNSUPPORTED, "window too large for the on-chip PDHG kernel (n or m > 4096)");
-    if (e != hipSuccess) return hip_fail(h, e, "launch_pdhg");
+    hipError_t e = h->disable_ell ? hipErrorInvalidValue
+                                  : dvh::launch_pdhg_ell(b, w, c.ch, o, c.mn, c.mm, wx, wy, s, &variant);
+    std::vector<int32_t> generic;
+    if (e == hipSuccess) {
+      h->n_ell += c.ch.count;
+      ist.resize(2 * (size_t)c.ch.count);
+      DVH_HIP(h, hipMemcpyAsync(ist.data(), bt->istats + 2 * (size_t)c.ch.first, I * ist.size(),
+                                hipMemcpyDeviceToHost, s));
+      DVH_HIP(h, hipStreamSynchronize(s));
+      for (int k = 0; k < c.ch.count; ++k)
+        if (ist[2 * (size_t)k] < 0) generic.push_back(c.ch.first + k);
+      h->n_ell -= (int)generic.size();
+    } else if (e == hipErrorInvalidValue) {
+      (void)hipGetLastError();
+      for (int k = 0; k < c.ch.count; ++k) generic.push_back(c.ch.first + k);
+    } else {
+      return hip_fail(h, e, "launch_pdhg_ell");
+    }
+    if (!generic.empty()) {
+      DVH_HIP(h, hipMemcpyAsync(h->d_list.p, generic.data(), I * generic.size(), hipMemcpyHostToDevice, s));
+      int gv = -1;
+      e = dvh::launch_pdhg(b, w, c.ch, o, c.mn, c.mm, c.mnz, s, &gv, h->d_list.as<int32_t>(), (int)generic.size());
+      if (e == hipErrorInvalidValue)
+        return fail(h, DVH_ERR_UNSUPPORTED, "window too large for the on-chip PDHG kernels (n or m > 4096)");
+      if (e != hipSuccess) return hip_fail(h, e, "launch_pdhg");
+      h->n_generic += (int)generic.size();
+      if (variant < 0) variant = gv;
+      DVH_HIP(h, hipStreamSynchronize(s));  // d_list is reused by the next chunk
+    }
+    DVH_HIP(h, hipEventRecord(e2, s));
     h->last_variant = variant;
   }
-  if (single) DVH_HIP(h, hipEventRecord(h->ev[2], s));
   DVH_HIP(h, hipEventRecord(h->ev[3], s));
   return DVH_OK;
 }
 
-static int finish_timing(dvh_handle* h) {
-  DVH_HIP(h, hipStreamSynchronize(h->stream));
+static int finish_timing(dvh_handle* h, hipStream_t s) {
+  DVH_HIP(h, hipStreamSynchronize(s));
   float t = 0;
   h->timing[0] = h->timing[1] = h->timing[2] = 0;
   if (hipEventElapsedTime(&t, h->ev[0], h->ev[3]) == hipSuccess) h->timing[0] = t;
-  if (hipEventElapsedTime(&t, h->ev[0], h->ev[1]) == hipSuccess) h->timing[1] = t;
-  if (hipEventElapsedTime(&t, h->ev[1], h->ev[2]) == hipSuccess) h->timing[2] = t;
+  for (auto& ce : h->chunk_events) {
+    if (hipEventElapsedTime(&t, ce[0], ce[1]) == hipSuccess) h->timing[1] += t;
+    if (hipEventElapsedTime(&t, ce[1], ce[2]) == hipSuccess) h->timing[2] += t;
+    for (hipEvent_t e : ce) hipEventDestroy(e);
+  }
+  h->chunk_events.clear();
   return DVH_OK;
 }
 
@@ -437,7 +507,7 @@ extern "C" int dvh_solve_batch(dvh_handle* h, const dvh_lp* lps, int32_t count, 
   if (tm) DVH_HIP(h, hipMemcpyAsync(y.data(), h->d_y.p, D * tm, hipMemcpyDeviceToHost, s));
   DVH_HIP(h, hipMemcpyAsync(stats.data(), h->d_stats.p, D * 4 * count, hipMemcpyDeviceToHost, s));
   DVH_HIP(h, hipMemcpyAsync(ist.data(), h->d_istats.p, I * 2 * count, hipMemcpyDeviceToHost, s));
-  rc = finish_timing(h);
+  rc = finish_timing(h, s);
   if (rc != DVH_OK) return rc;
   for (int k = 0; k < count; ++k) {
     const int64_t* d = &desc[8 * (size_t)k];
@@ -480,6 +550,5 @@ extern "C" int dvh_solve_packed_device(dvh_handle* h, const dvh_packed* bt, void
   }
   int rc = solve_packed(h, bt, desc, s);
   if (rc != DVH_OK) return rc;
-  if (!stream) return finish_timing(h);
-  return DVH_OK;
+  return finish_timing(h, s);
 }

@@ -8,12 +8,12 @@ namespace dvh {
 constexpr int kWave = 64;
 constexpr int kLongRow = 32;   // CSR rows longer than this are reduced by a whole wave
 constexpr int kLMax = 64;      // long rows per matrix per window handled on chip
-constexpr int kScal = 8;       // per-window scalars written by the setup kernel
+constexpr int kScal = 16;      // per-window scalars written by the setup kernel
 
 // Kernel-side copy of dvh_options (POD, passed by value).
 struct Opts {
   double eps, step_safety, rho, b_suff, b_nec, b_art, theta;
-  int max_iters, check_every, ruiz_iters, power_iters;
+  int max_iters, check_every, kkt_every, ruiz_iters, power_iters;
 };
 
 // Inputs of one chunk of the packed batch (device pointers, global offsets from desc).
@@ -53,7 +53,8 @@ struct Work {
   double* tmpr;     // [sum m]
   int32_t* longk;   // [count * kLMax]  long rows of K
   int32_t* longt;   // [count * kLMax]  long rows of K^T (dense columns, e.g. the DCM tau)
-  double* scal;     // [count * kScal]  eta, w0, ||c||, ||q||, nlong(K), nlong(K^T), flag, ||K||
+  double* scal;     // [count * kScal]  eta, w0, ||c||, ||q||, nlong(K), nlong(K^T), flag, ||K||,
+                    //   max short row len K, K^T (<= 8), #rows > 8 in K, K^T
 };
 
 struct Chunk {
@@ -67,8 +68,13 @@ hipError_t launch_setup(const Batch& b, const Work& w, const Chunk& ch, const Op
                         hipStream_t s);
 // Solve kernel selection is made from the chunk maxima; returns hipErrorInvalidValue when no
 // instantiation covers the sizes (the caller reports DVH_ERR_UNSUPPORTED).
+// Generic (CSR) kernel; list = optional device list of window ids (nlist blocks) instead of the whole chunk.
 hipError_t launch_pdhg(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n, int max_m,
-                       int64_t max_nnz, hipStream_t s, int* variant_out);
+                       int64_t max_nnz, hipStream_t s, int* variant_out, const int32_t* list, int nlist);
+// ELL fast-path kernel over the whole chunk (wx, wy: ELL widths for K^T and K).  Windows that do not fit
+// its shape come back with istats status -1 (kNeedsGeneric) and must be re-run by launch_pdhg.
+hipError_t launch_pdhg_ell(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n, int max_m,
+                           int wx, int wy, hipStream_t s, int* variant_out);
 size_t setup_lds_bytes(int max_n);
 
 }  // namespace dvh

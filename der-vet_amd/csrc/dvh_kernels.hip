@@ -34,6 +34,45 @@ __device__ __forceinline__ double wave_max(double v) {
   return v;
 }
 
+// Wave-wide f64 sum on the VALU: DPP row rotations (16-lane rows) then the gfx950 permlane16/32 swaps.
+// Every lane ends with the wave total (lanes may differ in the last bit; callers use one lane's value).
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  v += dpp_f64<0x128>(v);  // row_ror:8
+  v += dpp_f64<0x124>(v);  // row_ror:4
+  v += dpp_f64<0x122>(v);  // row_ror:2
+  v += dpp_f64<0x121>(v);  // row_ror:1
+  {
+    const unsigned lo = __double2loint(v), hi = __double2hiint(v);
+    const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    v = __hiloint2double(b[0], a[0]) + __hiloint2double(b[1], a[1]);
+  }
+  {
+    const unsigned lo = __double2loint(v), hi = __double2hiint(v);
+    const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    v = __hiloint2double(b[0], a[0]) + __hiloint2double(b[1], a[1]);
+  }
+  return v;
+}
+
+// Makes an index opaque to the optimiser so that address arithmetic of cold (check-phase) code is not
+// hoisted out of the iteration loop into long-lived VGPRs.
+__device__ __forceinline__ int opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+__device__ __forceinline__ double opaque(double v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
 // Block reduction of NV doubles; red must hold (NW + 1) * NV doubles.  Result identical in all threads.
 template <int B, int NV>
 __device__ __forceinline__ void block_sum(double (&v)[NV], double* red) {
@@ -85,6 +124,7 @@ __device__ __forceinline__ WinOff win_offsets(const Batch& b, const Chunk& ch, i
 // setup kernel
 // ------------------------------------------------------------------------------------------------
 constexpr int kSetupB = 256;
+constexpr int kEllMax = 8;   // widest ELL slice of the fast kernel
 
 // Row reductions over a CSR matrix: short rows one per thread, long rows one per wave.
 // f(e, row) -> contribution; MAXR selects max instead of sum.  out[row] = g(row, reduced).
@@ -303,6 +343,32 @@ __global__ __launch_bounds__(kSetupB) void setup_kernel(const Batch b, const Wor
     for (int j = tid; j < n; j += kSetupB) v[j] = tmpc[j] * inv;
     __syncthreads();
   }
+  // 8. row-length statistics for the ELL fast path: max length among rows with <= kEllMax entries and
+  //    the number of longer rows, for K and K^T
+  double wst[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int i = tid; i < m; i += kSetupB) {
+    const int len = Kp[i + 1] - Kp[i];
+    if (len <= kEllMax) wst[0] = fmax(wst[0], (double)len); else wst[2] += 1.0;
+  }
+  for (int j = tid; j < n; j += kSetupB) {
+    const int len = Tp[j + 1] - Tp[j];
+    if (len <= kEllMax) wst[1] = fmax(wst[1], (double)len); else wst[3] += 1.0;
+  }
+  {
+    double mx[2] = {wave_max(wst[0]), wave_max(wst[1])};
+    double ct[2] = {wst[2], wst[3]};
+    block_sum<kSetupB, 2>(ct, red);
+    if (lane == 0) { red[wid * 2] = mx[0]; red[wid * 2 + 1] = mx[1]; }
+    __syncthreads();
+    if (tid == 0) {
+      double a = 0.0, c2 = 0.0;
+      for (int t = 0; t < kSetupB / kWave; ++t) { a = fmax(a, red[2 * t]); c2 = fmax(c2, red[2 * t + 1]); }
+      scal[8] = a;
+      scal[9] = c2;
+      scal[10] = ct[0];
+      scal[11] = ct[1];
+    }
+  }
   if (tid == 0) {
     const double ncs = sqrt(nrm[0]), nqs = sqrt(nrm[1]);
     scal[0] = sig > 0.0 ? o.step_safety / sig : 1.0;
@@ -358,11 +424,12 @@ __host__ __device__ inline size_t pdhg_lds_bytes(int n, int m, int nnz, bool mld
 }
 
 template <int B, int XS, int YS, bool MLDS>
-__global__ __launch_bounds__(B) void pdhg_kernel(const Batch b, const Work w, const Chunk ch, const Opts o) {
+__global__ __launch_bounds__(B) void pdhg_kernel(const Batch b, const Work w, const Chunk ch, const Opts o,
+                                                 const int32_t* list) {
   constexpr int NW = B / kWave;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int k = ch.first + blockIdx.x;
-  const int kl = blockIdx.x;
+  const int k = list ? list[blockIdx.x] : ch.first + blockIdx.x;
+  const int kl = k - ch.first;
   const WinOff W = win_offsets(b, ch, k);
   const int n = W.n, m = W.m, meq = W.meq, nnz = W.nnz;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -503,11 +570,14 @@ __global__ __launch_bounds__(B) void pdhg_kernel(const Batch b, const Work w, co
   double r0 = -1.0, rprev = -1.0;
   double fin[4] = {NAN, NAN, NAN, NAN};  // obj, pres, dres, gap at the last check
   const int chk = o.check_every > 0 ? o.check_every : 64;
+  const int kkt_every = o.kkt_every > 0 ? o.kkt_every : 1;
+  int ck = chk, kk = kkt_every;
 
   while (it < o.max_iters) {
     const double tau = eta / pw, sigma = eta * pw;
-    const bool check = ((it + 1) % chk) == 0;
-    const double ca = (kin + 1.0) / (kin + 2.0), cb = 1.0 / (kin + 2.0);
+    const bool check = --ck == 0;
+    if (check) ck = chk;
+    const double cb = 1.0 / (kin + 2.0), ca = 1.0 - cb;
     double acc[kNRed];
 #pragma unroll
     for (int t = 0; t < kNRed; ++t) acc[t] = 0.0;
@@ -592,7 +662,10 @@ __global__ __launch_bounds__(B) void pdhg_kernel(const Batch b, const Work w, co
     __syncthreads();
     if (!check) continue;
 
-    // ---------------- check: KKT of T(z) = (x+, y+) in the unscaled space, restart test
+    // ---------------- check: restart test; every kkt_every-th check also the KKT error of T(z) = (x+, y+)
+    const bool kkt = (--kk == 0) || (it + chk > o.max_iters);
+    if (kkt) kk = kkt_every;
+    if (kkt) {
 #pragma unroll
     for (int s = 0; s < XS; ++s)
       if (ts[s] >= 0) X[tid + s * B] = xo_g[tid + s * B];
@@ -649,21 +722,24 @@ __global__ __launch_bounds__(B) void pdhg_kernel(const Batch b, const Work w, co
       kx = wave_sum(kx);
       if (lane == 0) row_kkt(i, kx, ly[2 * kLMax + L], ly[3 * kLMax + L]);
     }
-    block_sum<B, kNRed>(acc, red);
-    const double pobj = acc[6] + c0, dobj = acc[7] + acc[8] + c0;
-    const double pres = sqrt(acc[4]) / (1.0 + qnorm), dres = sqrt(acc[5]) / (1.0 + cnorm);
-    const double gap = fabs(pobj - dobj) / (1.0 + fabs(pobj) + fabs(dobj));
-    fin[0] = pobj;
-    fin[1] = pres;
-    fin[2] = dres;
-    fin[3] = gap;
-    if (pres <= o.eps && dres <= o.eps && gap <= o.eps) {
-      status = kOptimal;
-      break;
     }
-    if (!(isfinite(pobj) && isfinite(dobj))) {
-      status = kNumerical;
-      break;
+    block_sum<B, kNRed>(acc, red);
+    if (kkt) {
+      const double pobj = acc[6] + c0, dobj = acc[7] + acc[8] + c0;
+      const double pres = sqrt(acc[4]) / (1.0 + qnorm), dres = sqrt(acc[5]) / (1.0 + cnorm);
+      const double gap = fabs(pobj - dobj) / (1.0 + fabs(pobj) + fabs(dobj));
+      fin[0] = pobj;
+      fin[1] = pres;
+      fin[2] = dres;
+      fin[3] = gap;
+      if (pres <= o.eps && dres <= o.eps && gap <= o.eps) {
+        status = kOptimal;
+        break;
+      }
+      if (!(isfinite(pobj) && isfinite(dobj))) {
+        status = kNumerical;
+        break;
+      }
     }
     const double r = sqrt(pw * acc[0] + acc[2] / pw);
     if (r0 < 0.0) r0 = r;
@@ -680,16 +756,22 @@ __global__ __launch_bounds__(B) void pdhg_kernel(const Batch b, const Work w, co
         if (ks[s] >= 0) y[s] = ya[s] = yo_g[tid + s * B];
       for (int L = tid; L < nlt; L += B) lx[L] = lx[kLMax + L] = lx[5 * kLMax + L];
       for (int L = tid; L < nlk; L += B) ly[L] = ly[kLMax + L] = ly[3 * kLMax + L];
-      // Y already holds y+ = the new iterate
+      // Y <- y+ (the new iterate)
+#pragma unroll
+      for (int s = 0; s < YS; ++s)
+        if (ks[s] >= 0) Y[tid + s * B] = y[s];
+      for (int L = tid; L < nlk; L += B) Y[lyi[L]] = ly[3 * kLMax + L];
       kin = 0;
       r0 = r;
       rprev = -1.0;
     } else {
       rprev = r;
+      if (kkt) {
 #pragma unroll
-      for (int s = 0; s < YS; ++s)
-        if (ks[s] >= 0) Y[tid + s * B] = y[s];
-      for (int L = tid; L < nlk; L += B) Y[lyi[L]] = ly[L];
+        for (int s = 0; s < YS; ++s)
+          if (ks[s] >= 0) Y[tid + s * B] = y[s];
+        for (int L = tid; L < nlk; L += B) Y[lyi[L]] = ly[L];
+      }
     }
     __syncthreads();
   }
@@ -715,12 +797,587 @@ __global__ __launch_bounds__(B) void pdhg_kernel(const Batch b, const Work w, co
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// ELL fast-path PDHG kernel
+// ------------------------------------------------------------------------------------------------
+// Lane tid owns columns j = tid + s*B (s < XS) and rows i = tid + s*B (s < YS).  Short rows (K rows with
+// <= WY entries, K^T rows with <= WX entries) are stored as column-major ELL slices in LDS
+// (value[e][slot], coalesced ds_read_b64) with their column indices held in VGPRs for the whole solve,
+// so an iteration issues every value load and gather of a lane back to back.  Long rows (the dense DCM
+// tau column of K^T, or any longer row) are never gathered in the loop: their products are accumulated
+// on the *producing* side -- each lane adds K_ij * y_i (or K_ij * xbar_j) of its short rows into a per-wave
+// partial with a segmented wave reduction -- and one lane sums the NW partials after the barrier that
+// already separates the two half-steps.  Windows that do not fit this shape are reported with
+// istats status -1 and re-run by the generic kernel.
+constexpr int kNeedsGeneric = -1;
+
+// Segmented wave reduction of (target, value) pairs into part[target] (lane 0 accumulates).
+__device__ __forceinline__ void wave_scatter(double v, int tgt, double* part) {
+  const int lane = threadIdx.x & 63;
+  unsigned long long act = __ballot(tgt >= 0);
+  while (act) {
+    const int leader = __ffsll((long long)act) - 1;
+    const int tf = __shfl(tgt, leader, kWave);
+    const bool sel = tgt == tf;
+    const double sum = wave_sum_dpp(sel ? v : 0.0);
+    if (lane == 0) part[tf] += sum;
+    act &= ~__ballot(sel);
+  }
+}
+
+__host__ __device__ inline size_t ell_lds_bytes(int n, int m, int B, int XS, int YS, int WX, int WY) {
+  const int NW = B / kWave;
+  size_t d = (size_t)n + m + (size_t)WX * XS * B + (size_t)WY * YS * B + 2 * (size_t)NW * kLMax +
+             (size_t)kNRed * (NW + 1) + 4 + 12 * kLMax;
+  return align16(sizeof(double) * d) + align16(sizeof(int32_t) * 4 * kLMax);
+}
+
+template <int B, int XS, int YS, int WX, int WY>
+__global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w, const Chunk ch, const Opts o) {
+  constexpr int NW = B / kWave;
+  constexpr int RX = XS * B, RY = YS * B;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int k = ch.first + blockIdx.x;
+  const int kl = blockIdx.x;
+  const WinOff W = win_offsets(b, ch, k);
+  const int n = W.n, m = W.m, meq = W.meq;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const double* scal = w.scal + (int64_t)kl * kScal;
+  auto bail = [&]() {
+    if (tid == 0) {
+      b.istats[2 * k] = kNeedsGeneric;
+      b.istats[2 * k + 1] = 0;
+    }
+  };
+  if (scal[6] != 0.0 || n > RX || m > RY || n < 1) {
+    bail();
+    return;
+  }
+  // ---- LDS carve
+  double* X = reinterpret_cast<double*>(smem);
+  double* Y = X + n;
+  double* TE = Y + m;              // [WX][RX]
+  double* KE = TE + WX * RX;       // [WY][RY]
+  double* partC = KE + WY * RY;    // [NW][kLMax]  partial K'y of long columns
+  double* partR = partC + NW * kLMax;  // [NW][kLMax] partial K xbar of long rows
+  double* red = partR + NW * kLMax;
+  double* lx = red + kNRed * (NW + 1) + 4;  // long columns: x, xa, c, lo, hi, xp
+  double* ly = lx + 6 * kLMax;          // long rows: y, ya, q, yp
+  double* lkt = ly + 4 * kLMax;         // long columns: K'y+ of the last check (restart)
+  int32_t* ints = reinterpret_cast<int32_t*>(
+      smem + align16(sizeof(double) * ((size_t)n + m + (size_t)WX * RX + (size_t)WY * RY + 2 * (size_t)NW * kLMax +
+                                       (size_t)kNRed * (NW + 1) + 4 + 12 * kLMax)));
+  int32_t* lxi = ints;            // long column ids
+  int32_t* lyi = ints + kLMax;    // long row ids
+  int32_t* cnt = ints + 2 * kLMax;  // [0] nlx, [1] nly, [2] bad flag
+  const int32_t* gkp = b.indptr + W.row;
+  const int32_t* gkc = b.indices + W.nz;
+  const double* gkv = w.kval + W.wz;
+  const int32_t* gtp = w.tptr + W.wtr;
+  const int32_t* gtc = w.tind + W.wz;
+  const double* gtv = w.tval + W.wz;
+  const double* cs = w.cs + W.wn;
+  const double* ls = w.ls + W.wn;
+  const double* us = w.us + W.wn;
+  const double* qs = w.qs + W.wm;
+  const double* dcv = w.dc + W.wn;
+  const double* drv = w.dr + W.wm;
+  double* xo_g = b.x + W.on;   // x+ (scaled) at check iterations, final unscaled x
+  double* yo_g = b.y + W.om;
+  double* xk_g = w.tmpc + W.wn;  // z_k (pre-step iterate) at check iterations
+  double* yk_g = w.tmpr + W.wm;
+
+  // ---- long lists (deterministic ballot compaction by wave 0)
+  if (wid == 0) {
+    int nx = 0, ny = 0;
+    for (int base = 0; base < n; base += kWave) {
+      const int j = base + lane;
+      const bool isl = j < n && (gtp[j + 1] - gtp[j]) > WX;
+      const unsigned long long bal = __ballot(isl);
+      const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+      if (isl && nx + pre < kLMax) lxi[nx + pre] = j;
+      nx += __popcll(bal);
+    }
+    for (int base = 0; base < m; base += kWave) {
+      const int i = base + lane;
+      const bool isl = i < m && (gkp[i + 1] - gkp[i]) > WY;
+      const unsigned long long bal = __ballot(isl);
+      const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+      if (isl && ny + pre < kLMax) lyi[ny + pre] = i;
+      ny += __popcll(bal);
+    }
+    if (lane == 0) {
+      cnt[0] = nx;
+      cnt[1] = ny;
+      cnt[2] = 0;
+    }
+  }
+  // slot maps (in the X / Y images, as int32 before the iteration starts)
+  int32_t* cmap = reinterpret_cast<int32_t*>(X);  // n ints fit in n doubles
+  int32_t* rmap = reinterpret_cast<int32_t*>(Y);
+  for (int j = tid; j < n; j += B) cmap[j] = -1;
+  for (int i = tid; i < m; i += B) rmap[i] = -1;
+  __syncthreads();
+  const int nlx = cnt[0], nly = cnt[1];
+  if (nlx > kLMax || nly > kLMax) {
+    bail();
+    return;
+  }
+  for (int L = tid; L < nlx; L += B) cmap[lxi[L]] = L;
+  for (int L = tid; L < nly; L += B) rmap[lyi[L]] = L;
+  __syncthreads();
+
+  // ---- lane-owned state
+  int xi[XS][WX];
+  double x[XS], xa[XS], cc[XS], lo[XS], hi[XS];
+  int xs_tgt[XS];  // long K row fed by this column (scatter target)
+  double xs_cf[XS];
+  bool xown[XS];
+#pragma unroll
+  for (int s = 0; s < XS; ++s) {
+    const int j = tid + s * B;
+    xown[s] = false;
+    xs_tgt[s] = -1;
+    xs_cf[s] = 0.0;
+    x[s] = xa[s] = cc[s] = lo[s] = 0.0;
+    hi[s] = 0.0;
+    int a0 = 0, len = 0;
+    if (j < n) {
+      a0 = gtp[j];
+      len = gtp[j + 1] - a0;
+      if (len <= WX) {
+        xown[s] = true;
+        cc[s] = cs[j];
+        lo[s] = ls[j];
+        hi[s] = us[j];
+        x[s] = xa[s] = fmin(fmax(0.0, lo[s]), hi[s]);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < WX; ++e) {
+      const bool v = xown[s] && e < len;
+      const int r = v ? gtc[a0 + e] : 0;
+      xi[s][e] = r;
+      TE[e * RX + tid + s * B] = v ? gtv[a0 + e] : 0.0;
+      if (v) {
+        const int L = rmap[r];
+        if (L >= 0) {
+          if (xs_tgt[s] >= 0) cnt[2] = 1;  // two long rows in one column: not this kernel's shape
+          xs_tgt[s] = L;
+          xs_cf[s] = gtv[a0 + e];
+        }
+      }
+    }
+  }
+  int yi[YS][WY];
+  double y[YS], ya[YS], qq[YS];
+  int ys_tgt[YS];
+  double ys_cf[YS];
+  bool yown[YS];
+#pragma unroll
+  for (int s = 0; s < YS; ++s) {
+    const int i = tid + s * B;
+    yown[s] = false;
+    ys_tgt[s] = -1;
+    ys_cf[s] = 0.0;
+    y[s] = ya[s] = qq[s] = 0.0;
+    int a0 = 0, len = 0;
+    if (i < m) {
+      a0 = gkp[i];
+      len = gkp[i + 1] - a0;
+      if (len <= WY) {
+        yown[s] = true;
+        qq[s] = qs[i];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < WY; ++e) {
+      const bool v = yown[s] && e < len;
+      const int c = v ? gkc[a0 + e] : 0;
+      yi[s][e] = c;
+      KE[e * RY + tid + s * B] = v ? gkv[a0 + e] : 0.0;
+      if (v) {
+        const int L = cmap[c];
+        if (L >= 0) {
+          if (ys_tgt[s] >= 0) cnt[2] = 1;
+          ys_tgt[s] = L;
+          ys_cf[s] = gkv[a0 + e];
+        }
+      }
+    }
+  }
+  for (int L = wid; L < nly; L += NW) {  // a long row touching a long column is not this kernel's shape
+    const int i = lyi[L];
+    for (int p = gkp[i] + lane; p < gkp[i + 1]; p += kWave)
+      if (cmap[gkc[p]] >= 0) cnt[2] = 1;
+  }
+  for (int L = tid; L < nlx; L += B) {
+    const int j = lxi[L];
+    const double l0 = ls[j], h0 = us[j], x0 = fmin(fmax(0.0, l0), h0);
+    lx[L] = x0;
+    lx[kLMax + L] = x0;
+    lx[2 * kLMax + L] = cs[j];
+    lx[3 * kLMax + L] = l0;
+    lx[4 * kLMax + L] = h0;
+    lx[5 * kLMax + L] = x0;
+  }
+  for (int L = tid; L < nly; L += B) {
+    const int i = lyi[L];
+    ly[L] = 0.0;
+    ly[kLMax + L] = 0.0;
+    ly[2 * kLMax + L] = qs[i];
+    ly[3 * kLMax + L] = 0.0;
+  }
+  for (int t = tid; t < 2 * NW * kLMax; t += B) partC[t] = 0.0;  // partC and partR are contiguous
+  // Per-wave scatter shape: when every lane of the wave feeds at most one long row (column), and all lanes
+  // feed the same one, a lane sums its slots in registers and the wave needs ONE reduction per half-step.
+  auto wave_target = [&](const int* tg, int S) {
+    int t = -1;
+    bool multi = false;
+    for (int q = 0; q < S; ++q)
+      if (tg[q] >= 0) {
+        if (t >= 0 && t != tg[q]) multi = true;
+        t = tg[q];
+      }
+    const unsigned long long has = __ballot(t >= 0);
+    const int lead = has ? __ffsll((long long)has) - 1 : 0;
+    const int tw = __shfl(t, lead, kWave);
+    const bool ok = !__any(multi || (t >= 0 && t != tw));
+    return has == 0ull ? -1 : (ok ? tw : -2);  // -1 none, -2 general, >= 0 the single target
+  };
+  const int xtw = wave_target(xs_tgt, XS);
+  const int ytw = wave_target(ys_tgt, YS);
+  __syncthreads();
+  if (cnt[2] != 0) {
+    bail();
+    return;
+  }
+  for (int i = tid; i < m; i += B) Y[i] = 0.0;
+  __syncthreads();
+
+  double eta = scal[0], pw = scal[1];
+  const double cnorm = scal[2], qnorm = scal[3], c0 = b.c0[k];
+  const double rho = o.rho;
+  int it = 0, kin = 0, status = kIterLimit;
+  double r0 = -1.0, rprev = -1.0;
+  double* fin = red + kNRed * NW;  // obj, pres, dres, gap of the last check (LDS, written by block_sum readers)
+  if (tid == 0)
+    for (int t = 0; t < 4; ++t) fin[t] = NAN;
+  const int chk = o.check_every > 0 ? o.check_every : 64;
+  double* myPC = partC + wid * kLMax;
+  double* myPR = partR + wid * kLMax;
+
+  double tau = eta / pw, sigma = eta * pw;
+  const int kkt_every = o.kkt_every > 0 ? o.kkt_every : 1;
+  int ck = chk, kk = kkt_every;
+  while (it < o.max_iters) {
+    const bool check = --ck == 0;
+    if (check) ck = chk;
+    const double cb = 1.0 / (kin + 2.0), ca = 1.0 - cb;
+    // ---------------- primal half-step
+    {
+      double kty[XS];
+#pragma unroll
+      for (int s = 0; s < XS; ++s) {
+        kty[s] = 0.0;
+#pragma unroll
+        for (int e = 0; e < WX; ++e) kty[s] += TE[e * RX + tid + s * B] * Y[xi[s][e]];
+      }
+      double xbs[XS];
+#pragma unroll
+      for (int s = 0; s < XS; ++s) {
+        double xb = 0.0;
+        if (xown[s]) {
+          const int j = tid + s * B;
+          const double p1 = fmin(fmax(x[s] - tau * (cc[s] - kty[s]), lo[s]), hi[s]);
+          xb = 2.0 * p1 - x[s];
+          X[j] = xb;
+          if (check) {
+            const int jo = opaque(j);
+            xk_g[jo] = x[s];
+            xo_g[jo] = p1;
+          }
+          x[s] = ca * ((1.0 + rho) * p1 - rho * x[s]) + cb * xa[s];
+        }
+        xbs[s] = xb;
+      }
+      if (xtw >= 0) {
+        double a = 0.0;
+#pragma unroll
+        for (int s = 0; s < XS; ++s) a += xs_cf[s] * xbs[s];
+        a = wave_sum_dpp(a);
+        if (lane == 0) myPR[xtw] = a;
+      } else if (xtw == -2) {
+#pragma unroll
+        for (int s = 0; s < XS; ++s) wave_scatter(xs_cf[s] * xbs[s], xs_tgt[s], myPR);
+      }
+      // long columns: K'y accumulated by the previous dual half-step
+      for (int L = tid; L < nlx; L += B) {
+        double kt = 0.0;
+        for (int w2 = 0; w2 < NW; ++w2) {
+          kt += partC[w2 * kLMax + L];
+          partC[w2 * kLMax + L] = 0.0;
+        }
+        const int j = lxi[L];
+        const double xo = lx[L], xan = lx[kLMax + L];
+        const double p1 = fmin(fmax(xo - tau * (lx[2 * kLMax + L] - kt), lx[3 * kLMax + L]), lx[4 * kLMax + L]);
+        X[j] = 2.0 * p1 - xo;
+        if (check) {
+          xk_g[j] = xo;
+          lx[5 * kLMax + L] = p1;
+        }
+        lx[L] = ca * ((1.0 + rho) * p1 - rho * xo) + cb * xan;
+      }
+    }
+    __syncthreads();
+    // ---------------- dual half-step
+    {
+      double kx[YS];
+#pragma unroll
+      for (int s = 0; s < YS; ++s) {
+        kx[s] = 0.0;
+#pragma unroll
+        for (int e = 0; e < WY; ++e) kx[s] += KE[e * RY + tid + s * B] * X[yi[s][e]];
+      }
+      double yns[YS];
+#pragma unroll
+      for (int s = 0; s < YS; ++s) {
+        double yn = 0.0;
+        if (yown[s]) {
+          const int i = tid + s * B;
+          double p1 = y[s] + sigma * (qq[s] - kx[s]);
+          if (i >= meq) p1 = fmax(p1, 0.0);
+          if (check) {
+            const int io = opaque(i);
+            yk_g[io] = y[s];
+            yo_g[io] = p1;
+          }
+          yn = ca * ((1.0 + rho) * p1 - rho * y[s]) + cb * ya[s];
+          y[s] = yn;
+          Y[i] = yn;
+        }
+        yns[s] = yn;
+      }
+      if (ytw >= 0) {
+        double a = 0.0;
+#pragma unroll
+        for (int s = 0; s < YS; ++s) a += ys_cf[s] * yns[s];
+        a = wave_sum_dpp(a);
+        if (lane == 0) myPC[ytw] = a;
+      } else if (ytw == -2) {
+#pragma unroll
+        for (int s = 0; s < YS; ++s) wave_scatter(ys_cf[s] * yns[s], ys_tgt[s], myPC);
+      }
+      for (int L = tid; L < nly; L += B) {
+        double kv = 0.0;
+        for (int w2 = 0; w2 < NW; ++w2) {
+          kv += partR[w2 * kLMax + L];
+          partR[w2 * kLMax + L] = 0.0;
+        }
+        const int i = lyi[L];
+        const double yo = ly[L], yan = ly[kLMax + L];
+        double p1 = yo + sigma * (ly[2 * kLMax + L] - kv);
+        if (i >= meq) p1 = fmax(p1, 0.0);
+        if (check) {
+          yk_g[i] = yo;
+          ly[3 * kLMax + L] = p1;
+        }
+        const double yn = ca * ((1.0 + rho) * p1 - rho * yo) + cb * yan;
+        ly[L] = yn;
+        Y[i] = yn;
+      }
+    }
+    ++it;
+    ++kin;
+    __syncthreads();
+    if (!check) continue;
+
+    // ---------------- check (every check_every iterations): fixed-point residual of z_k, restart test;
+    // every kkt_every-th check also the relative KKT error of T(z_k) = (x+, y+) in the unscaled space.
+    const bool kkt = (--kk == 0) || (it + chk > o.max_iters);  // the last check before the limit is a KKT one
+    if (kkt) kk = kkt_every;
+    double acc[kNRed];  // 0..3 movement norms, 4 ||r_p||^2, 5 ||r_d||^2, 6 c'x, 7 q'y, 8 bound term
+#pragma unroll
+    for (int t = 0; t < kNRed; ++t) acc[t] = 0.0;
+#pragma unroll
+    for (int s = 0; s < XS; ++s)
+      if (xown[s]) {
+        const int j = opaque(tid + s * B);
+        const double p1 = xo_g[j], d = xk_g[j] - p1, da = p1 - xa[s];
+        acc[0] += d * d;
+        acc[1] += da * da;
+        if (kkt) X[j] = p1;
+      }
+#pragma unroll
+    for (int s = 0; s < YS; ++s)
+      if (yown[s]) {
+        const int i = opaque(tid + s * B);
+        const double p1 = yo_g[i], d = yk_g[i] - p1, da = p1 - ya[s];
+        acc[2] += d * d;
+        acc[3] += da * da;
+        if (kkt) Y[i] = p1;
+      }
+    for (int L = tid; L < nlx; L += B) {
+      const double p1 = lx[5 * kLMax + L], d = xk_g[lxi[L]] - p1, da = p1 - lx[kLMax + L];
+      acc[0] += d * d;
+      acc[1] += da * da;
+      if (kkt) X[lxi[L]] = p1;
+    }
+    for (int L = tid; L < nly; L += B) {
+      const double p1 = ly[3 * kLMax + L], d = yk_g[lyi[L]] - p1, da = p1 - ly[kLMax + L];
+      acc[2] += d * d;
+      acc[3] += da * da;
+      if (kkt) Y[lyi[L]] = p1;
+    }
+    if (kkt) {
+      __syncthreads();
+      auto col_kkt = [&](int j, double kt, double cj, double loj, double hij, double xj) {
+        loj = opaque(loj);
+        hij = opaque(hij);
+        const double d = dcv[opaque(j)];
+        const double rc = (cj - kt) / d;
+        const bool fl = isfinite(loj), fh = isfinite(hij);
+        const double lam = (fl && fh) ? rc : (fl ? fmax(rc, 0.0) : (fh ? fmin(rc, 0.0) : 0.0));
+        const double rd = rc - lam;
+        acc[5] += rd * rd;
+        acc[6] += cj * xj;
+        acc[8] += (fl ? loj * d * fmax(lam, 0.0) : 0.0) + (fh ? hij * d * fmin(lam, 0.0) : 0.0);
+      };
+      auto row_kkt = [&](int i, double kv, double qi, double yi2) {
+        double r = (qi - kv) / drv[opaque(i)];
+        if (i >= meq) r = fmax(r, 0.0);
+        acc[4] += r * r;
+        acc[7] += qi * yi2;
+      };
+#pragma unroll
+      for (int s = 0; s < XS; ++s) {
+        if (xown[s]) {
+          double kt = 0.0;
+#pragma unroll
+          for (int e = 0; e < WX; ++e) kt += TE[e * RX + tid + s * B] * Y[xi[s][e]];
+          col_kkt(tid + s * B, kt, cc[s], lo[s], hi[s], X[tid + s * B]);
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < YS; ++s) {
+        if (yown[s]) {
+          double kv = 0.0;
+#pragma unroll
+          for (int e = 0; e < WY; ++e) kv += KE[e * RY + tid + s * B] * X[yi[s][e]];
+          row_kkt(tid + s * B, kv, qq[s], Y[tid + s * B]);
+        }
+      }
+      // long rows / columns: wave gathers from the workspace CSR (termination checks only)
+      for (int L = wid; L < nlx; L += NW) {
+        const int j = lxi[L];
+        double kt = 0.0;
+        for (int p = gtp[j] + lane; p < gtp[j + 1]; p += kWave) kt += gtv[p] * Y[gtc[p]];
+        kt = wave_sum(kt);
+        if (lane == 0) col_kkt(j, kt, lx[2 * kLMax + L], lx[3 * kLMax + L], lx[4 * kLMax + L], lx[5 * kLMax + L]);
+      }
+      for (int L = wid; L < nly; L += NW) {
+        const int i = lyi[L];
+        double kv = 0.0;
+        for (int p = gkp[i] + lane; p < gkp[i + 1]; p += kWave) kv += gkv[p] * X[gkc[p]];
+        kv = wave_sum(kv);
+        if (lane == 0) row_kkt(i, kv, ly[2 * kLMax + L], ly[3 * kLMax + L]);
+      }
+    }
+    block_sum<B, kNRed>(acc, red);
+    if (kkt) {
+      const double pobj = acc[6] + c0, dobj = acc[7] + acc[8] + c0;
+      const double pres = sqrt(acc[4]) / (1.0 + qnorm), dres = sqrt(acc[5]) / (1.0 + cnorm);
+      const double gap = fabs(pobj - dobj) / (1.0 + fabs(pobj) + fabs(dobj));
+      if (tid == 0) {
+        fin[0] = pobj;
+        fin[1] = pres;
+        fin[2] = dres;
+        fin[3] = gap;
+      }
+      if (pres <= o.eps && dres <= o.eps && gap <= o.eps) {
+        status = kOptimal;
+        break;
+      }
+      if (!(isfinite(pobj) && isfinite(dobj))) {
+        status = kNumerical;
+        break;
+      }
+    }
+    const double r = sqrt(pw * acc[0] + acc[2] / pw);
+    if (r0 < 0.0) r0 = r;
+    const bool restart = (r <= o.b_suff * r0) || (r <= o.b_nec * r0 && rprev >= 0.0 && r > rprev) ||
+                         ((double)kin >= o.b_art * (double)it);
+    if (restart) {
+      const double ddx = sqrt(acc[1]), ddy = sqrt(acc[3]);
+      if (ddx > 1e-10 && ddy > 1e-10) pw = exp(o.theta * log(ddy / ddx) + (1.0 - o.theta) * log(pw));
+      tau = eta / pw;
+      sigma = eta * pw;
+      double yns[YS];
+#pragma unroll
+      for (int s = 0; s < XS; ++s)
+        if (xown[s]) x[s] = xa[s] = xo_g[opaque(tid + s * B)];
+#pragma unroll
+      for (int s = 0; s < YS; ++s) {
+        yns[s] = 0.0;
+        if (yown[s]) {
+          const int i = opaque(tid + s * B);
+          y[s] = ya[s] = yns[s] = yo_g[i];
+          Y[i] = y[s];
+        }
+      }
+      for (int L = tid; L < nlx; L += B) lx[L] = lx[kLMax + L] = lx[5 * kLMax + L];
+      for (int L = tid; L < nly; L += B) {
+        ly[L] = ly[kLMax + L] = ly[3 * kLMax + L];
+        Y[lyi[L]] = ly[L];
+      }
+      // the long columns' K'y partials must now refer to y = y+: rebuild this wave's row
+      if (lane < kLMax) myPC[lane] = 0.0;
+      if (ytw >= 0) {
+        double a2 = 0.0;
+#pragma unroll
+        for (int s = 0; s < YS; ++s) a2 += ys_cf[s] * yns[s];
+        a2 = wave_sum_dpp(a2);
+        if (lane == 0) myPC[ytw] = a2;
+      } else if (ytw == -2) {
+#pragma unroll
+        for (int s = 0; s < YS; ++s) wave_scatter(ys_cf[s] * yns[s], ys_tgt[s], myPC);
+      }
+      kin = 0;
+      r0 = r;
+      rprev = -1.0;
+    } else {
+      rprev = r;
+      if (kkt) {
+#pragma unroll
+        for (int s = 0; s < YS; ++s)
+          if (yown[s]) Y[tid + s * B] = y[s];
+        for (int L = tid; L < nly; L += B) Y[lyi[L]] = ly[L];
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int s = 0; s < XS; ++s)
+    if (xown[s]) xo_g[tid + s * B] *= dcv[tid + s * B];
+  for (int L = tid; L < nlx; L += B) xo_g[lxi[L]] = lx[5 * kLMax + L] * dcv[lxi[L]];
+#pragma unroll
+  for (int s = 0; s < YS; ++s)
+    if (yown[s]) yo_g[tid + s * B] *= drv[tid + s * B];
+  for (int L = tid; L < nly; L += B) yo_g[lyi[L]] = ly[3 * kLMax + L] * drv[lyi[L]];
+  if (tid == 0) {
+    b.istats[2 * k] = status;
+    b.istats[2 * k + 1] = it;
+    for (int t = 0; t < 4; ++t) b.stats[4 * k + t] = fin[t];
+  }
+}
+
 template <int B, int XS, int YS, bool MLDS>
-hipError_t launch_one(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, size_t lds, hipStream_t s) {
+hipError_t launch_one(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, size_t lds, hipStream_t s,
+                      const int32_t* list, int nlist) {
   auto kern = pdhg_kernel<B, XS, YS, MLDS>;
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(kern, dim3(ch.count), dim3(B), lds, s, b, w, ch, o);
+  hipLaunchKernelGGL(kern, dim3(list ? nlist : ch.count), dim3(B), lds, s, b, w, ch, o, list);
   return hipGetLastError();
 }
 
@@ -728,20 +1385,42 @@ hipError_t launch_one(const Batch& b, const Work& w, const Chunk& ch, const Opts
 // so windows with n, m <= 4096 run with the whole iterate in registers.
 template <bool MLDS>
 hipError_t dispatch_xy(int xs, int ys, const Batch& b, const Work& w, const Chunk& ch, const Opts& o, size_t lds,
-                       hipStream_t s) {
+                       hipStream_t s, const int32_t* list, int nlist) {
   constexpr int B = 512;
 #define DVH_CASE(X_, Y_) \
-  if (xs <= X_ && ys <= Y_) return launch_one<B, X_, Y_, MLDS>(b, w, ch, o, lds, s);
+  if (xs <= X_ && ys <= Y_) return launch_one<B, X_, Y_, MLDS>(b, w, ch, o, lds, s, list, nlist);
+  DVH_CASE(2, 2)
+  DVH_CASE(5, 3)
+  DVH_CASE(6, 4)
+  DVH_CASE(8, 8)
+#undef DVH_CASE
+  return hipErrorInvalidValue;
+}
+
+template <int B, int XS, int YS, int WX, int WY>
+hipError_t launch_ell_one(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n, int max_m,
+                          hipStream_t s) {
+  const size_t lds = ell_lds_bytes(max_n, max_m, B, XS, YS, WX, WY);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  auto kern = pdhg_ell_kernel<B, XS, YS, WX, WY>;
+  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(kern, dim3(ch.count), dim3(B), lds, s, b, w, ch, o);
+  return hipGetLastError();
+}
+
+template <int WX, int WY>
+hipError_t ell_dispatch_xy(int xs, int ys, const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n,
+                           int max_m, hipStream_t s) {
+  constexpr int B = 512;
+#define DVH_CASE(X_, Y_) \
+  if (xs <= X_ && ys <= Y_) return launch_ell_one<B, X_, Y_, WX, WY>(b, w, ch, o, max_n, max_m, s);
   DVH_CASE(1, 1)
-  DVH_CASE(2, 1)
   DVH_CASE(2, 2)
   DVH_CASE(3, 2)
-  DVH_CASE(4, 3)
   DVH_CASE(5, 3)
-  DVH_CASE(5, 4)
   DVH_CASE(6, 4)
   DVH_CASE(8, 6)
-  DVH_CASE(8, 8)
 #undef DVH_CASE
   return hipErrorInvalidValue;
 }
@@ -759,7 +1438,7 @@ hipError_t launch_setup(const Batch& b, const Work& w, const Chunk& ch, const Op
 }
 
 hipError_t launch_pdhg(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n, int max_m,
-                       int64_t max_nnz, hipStream_t s, int* variant_out) {
+                       int64_t max_nnz, hipStream_t s, int* variant_out, const int32_t* list, int nlist) {
   constexpr int B = 512;
   constexpr size_t kLdsCap = 160 * 1024;
   const int xs = (max_n + B - 1) / B, ys = (max_m + B - 1) / B;
@@ -769,7 +1448,18 @@ hipError_t launch_pdhg(const Batch& b, const Work& w, const Chunk& ch, const Opt
   const size_t lds = mlds ? lds_m : pdhg_lds_bytes(max_n, max_m, 0, false, B / kWave);
   if (lds > kLdsCap) return hipErrorInvalidValue;
   if (variant_out) *variant_out = (mlds ? 1000 : 0) + xs * 10 + ys;
-  return mlds ? dispatch_xy<true>(xs, ys, b, w, ch, o, lds, s) : dispatch_xy<false>(xs, ys, b, w, ch, o, lds, s);
+  return mlds ? dispatch_xy<true>(xs, ys, b, w, ch, o, lds, s, list, nlist)
+              : dispatch_xy<false>(xs, ys, b, w, ch, o, lds, s, list, nlist);
+}
+
+hipError_t launch_pdhg_ell(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n, int max_m,
+                           int wx, int wy, hipStream_t s, int* variant_out) {
+  constexpr int B = 512;
+  const int xs = (max_n + B - 1) / B, ys = (max_m + B - 1) / B;
+  if (variant_out) *variant_out = 2000000 + wx * 10000 + wy * 1000 + xs * 10 + ys;
+  if (wx <= 2 && wy <= 4) return ell_dispatch_xy<2, 4>(xs, ys, b, w, ch, o, max_n, max_m, s);
+  if (wx <= 4 && wy <= 8) return ell_dispatch_xy<4, 8>(xs, ys, b, w, ch, o, max_n, max_m, s);
+  return hipErrorInvalidValue;
 }
 
 }  // namespace dvh

@@ -25,7 +25,7 @@ class Options(ctypes.Structure):
                 ("reflection", ctypes.c_double), ("restart_sufficient", ctypes.c_double),
                 ("restart_necessary", ctypes.c_double), ("restart_artificial", ctypes.c_double),
                 ("primal_weight_theta", ctypes.c_double), ("verbose", ctypes.c_int32),
-                ("reserved", ctypes.c_int32 * 7)]
+                ("kkt_every", ctypes.c_int32), ("reserved", ctypes.c_int32 * 6)]
 
 
 class LP(ctypes.Structure):
@@ -62,6 +62,8 @@ SYMBOLS = {
     "dvh_solve_packed_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Packed), ctypes.c_void_p]),
     "dvh_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
     "dvh_last_timing": (ctypes.c_int, [ctypes.c_void_p, c_double_p]),
+    "dvh_last_stats": (ctypes.c_int, [ctypes.c_void_p, c_int32_p]),
+    "dvh_set_kernel_path": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
 }
 
 _lib = None

@@ -1,0 +1,209 @@
+"""Vectorised builder of DER-VET dispatch-window LPs for many windows at once (native export path).
+
+Emits exactly the LP that storagevet's ``Scenario.set_up_optimization`` + CVXPY hand to the solver at
+``dervet/MicrogridScenario.py:319`` for the in-scope DER / value-stream set (SURVEY.md section 8a rows
+a3-a10, Appendix A), in the canonical form of include/dervet_hip.h (equalities first, then >= rows):
+
+  x = [ch(T), dis(T), ene(T), tau(J)]                              (battery: ESSSizing.py:223-278)
+  row 0            ene_0 = target                                  (target = soc_target * E)
+  rows 1..T-1      -dt eta ch_t + dt dis_t - (1 - dt sdr) ene_t + ene_{t+1} = 0
+  row T            dt eta ch_{T-1} - dt dis_{T-1} + (1 - dt sdr) ene_{T-1} = target
+  >= rows          -ch_t + dis_t + tau_j >= L_t - G_t + hp          for t in M_j   (DCM epigraph)
+  bounds           0 <= ch <= P_ch, 0 <= dis <= P_dis, max(llsoc E, a_min) <= ene <= min(ulsoc E, a_max)
+  objective keys   'retailETS', 'DCM', 'DA', '<es> fixed_om', '<es> var_om'  (golden objective_values columns)
+
+Windows that share (T, J, demand masks) share one CSR pattern; values broadcast over the G windows of a
+group, so a 10,000-scenario x 12-month sweep is built with a handful of array operations.
+"""
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from ..packed import PackedBatch
+
+
+@dataclass
+class WindowGroup:
+    """G windows with one CSR pattern."""
+    T: int
+    J: int
+    m_eq: int
+    indptr: np.ndarray      # int32 [m+1]
+    indices: np.ndarray     # int32 [nnz]
+    data: np.ndarray        # f64 [G, nnz]
+    c: np.ndarray           # f64 [G, n]
+    c0: np.ndarray          # f64 [G]
+    q: np.ndarray           # f64 [G, m]
+    l: np.ndarray           # f64 [G, n]
+    u: np.ndarray           # f64 [G, n]
+    terms: dict = field(default_factory=dict)   # key -> (coef [G, n], const [G])
+    tags: list = field(default_factory=list)    # per-window identifiers (scenario, window)
+
+    @property
+    def G(self):
+        return self.data.shape[0]
+
+    @property
+    def n(self):
+        return self.c.shape[1]
+
+    @property
+    def m(self):
+        return self.q.shape[1]
+
+
+def _col(a, G, T=None):
+    a = np.asarray(a, np.float64)
+    if T is None:
+        return np.broadcast_to(a, (G,)).astype(np.float64, copy=True) if a.ndim <= 1 else a
+    return np.broadcast_to(a, (G, T)).astype(np.float64, copy=False)
+
+
+def battery_group(T, dt, base_load, bat, retail_price=None, da_price=None, demand_masks=None, demand_prices=None,
+                  ene_min=None, ene_max=None, name="es", tags=None):
+    """Build G windows sharing T steps and the demand masks.
+
+    base_load [G, T]  : site load minus fixed generation (kW), hp is added here from ``bat``
+    bat               : dict of [G] (or scalar) arrays: E, Pch, Pdis, rte (fraction), sdr (%/h), soc_target,
+                        ulsoc, llsoc (fractions), fixedOM ($/kW-yr, charged per window), OMexpenses ($/MWh), hp (kW)
+    retail_price, da_price [G, T] ($/kWh) or None
+    demand_masks bool [J, T] ; demand_prices [G, J] ($/kW)
+    ene_min / ene_max [G, T] aggregate SOE limits (User / Reliability requirements) or None
+    """
+    base_load = np.atleast_2d(np.asarray(base_load, np.float64))
+    G = base_load.shape[0]
+    masks = np.zeros((0, T), bool) if demand_masks is None else np.asarray(demand_masks, bool)
+    masks = masks[masks.any(axis=1)] if len(masks) else masks
+    J = masks.shape[0]
+    E = _col(bat["E"], G)
+    pch, pdis = _col(bat["Pch"], G), _col(bat["Pdis"], G)
+    eta, sdr = _col(bat["rte"], G), _col(bat.get("sdr", 0.0), G) / 100.0
+    target = _col(bat.get("soc_target", 1.0), G) * E
+    hp = _col(bat.get("hp", 0.0), G)
+    base = base_load + hp[:, None]
+    n = 3 * T + J
+    ich, idis, iene, itau = 0, T, 2 * T, 3 * T
+    t = np.arange(T)
+
+    # ---- pattern: row lengths 1, 4 x (T-1), 3, then 3 per >= row
+    rows_i = [np.nonzero(mk)[0] for mk in masks]
+    mI = int(sum(len(r) for r in rows_i))
+    m = T + 1 + mI
+    lens = np.concatenate([[1], np.full(T - 1, 4), [3], np.full(mI, 3)]).astype(np.int64)
+    indptr = np.zeros(m + 1, np.int64)
+    np.cumsum(lens, out=indptr[1:])
+    nnz = int(indptr[-1])
+    indices = np.empty(nnz, np.int32)
+    data = np.empty((G, nnz))
+    indices[0] = iene
+    data[:, 0] = 1.0
+    # recurrence rows (sorted columns: ch_t, dis_t, ene_t, ene_t+1)
+    r = indptr[1:T].reshape(-1, 1) + np.arange(4)
+    tt = t[:-1]
+    indices[r] = np.stack([ich + tt, idis + tt, iene + tt, iene + tt + 1], axis=1)
+    data[:, r[:, 0]] = -dt * eta[:, None]
+    data[:, r[:, 1]] = dt
+    data[:, r[:, 2]] = -(1.0 - dt * sdr)[:, None]
+    data[:, r[:, 3]] = 1.0
+    # final row
+    p = indptr[T]
+    indices[p:p + 3] = [ich + T - 1, idis + T - 1, iene + T - 1]
+    data[:, p] = dt * eta
+    data[:, p + 1] = -dt
+    data[:, p + 2] = 1.0 - dt * sdr
+    # DCM epigraph rows
+    q = np.zeros((G, m))
+    q[:, 0] = target
+    q[:, T] = target
+    row = T + 1
+    for j, ti in enumerate(rows_i):
+        k = len(ti)
+        rr = indptr[row:row + k].reshape(-1, 1) + np.arange(3)
+        indices[rr] = np.stack([ich + ti, idis + ti, np.full(k, itau + j)], axis=1)
+        data[:, rr[:, 0]] = -1.0
+        data[:, rr[:, 1]] = 1.0
+        data[:, rr[:, 2]] = 1.0
+        q[:, row:row + k] = base[:, ti]
+        row += k
+
+    # ---- bounds
+    l = np.zeros((G, n))
+    u = np.empty((G, n))
+    u[:, ich:ich + T] = pch[:, None]
+    u[:, idis:idis + T] = pdis[:, None]
+    lo = (_col(bat.get("llsoc", 0.0), G) * E)[:, None] * np.ones((1, T))
+    hi = (_col(bat.get("ulsoc", 1.0), G) * E)[:, None] * np.ones((1, T))
+    if ene_min is not None:
+        lo = np.maximum(lo, _col(ene_min, G, T))
+    if ene_max is not None:
+        hi = np.minimum(hi, _col(ene_max, G, T))
+    l[:, iene:iene + T] = lo
+    u[:, iene:iene + T] = hi
+    l[:, itau:] = -np.inf
+    u[:, itau:] = np.inf
+
+    # ---- objective terms
+    terms = {}
+
+    def net_term(price):
+        pr = _col(price, G, T)
+        coef = np.zeros((G, n))
+        coef[:, ich:ich + T] = pr * dt
+        coef[:, idis:idis + T] = -pr * dt
+        return coef, (pr * dt * base).sum(axis=1)
+
+    if da_price is not None:
+        terms["DA"] = net_term(da_price)
+    if J:
+        coef = np.zeros((G, n))
+        coef[:, itau:itau + J] = np.asarray(demand_prices, np.float64).reshape(G, J)
+        terms["DCM"] = (coef, np.zeros(G))
+    if retail_price is not None:
+        terms["retailETS"] = net_term(retail_price)
+    terms[f"{name} fixed_om"] = (np.zeros((G, n)), _col(bat.get("fixedOM", 0.0), G) * pdis)
+    coef = np.zeros((G, n))
+    coef[:, idis:idis + T] = (_col(bat.get("OMexpenses", 0.0), G) / 1000.0 * dt)[:, None]
+    terms[f"{name} var_om"] = (coef, np.zeros(G))
+    c = np.zeros((G, n))
+    c0 = np.zeros(G)
+    for coef, const in terms.values():
+        c += coef
+        c0 += const
+    return WindowGroup(T=T, J=J, m_eq=T + 1, indptr=indptr.astype(np.int32), indices=indices, data=data, c=c, c0=c0,
+                       q=q, l=l, u=u, terms=terms, tags=list(tags) if tags is not None else [None] * G)
+
+
+def group_window_lps(g):
+    """Per-window solver.WindowLP objects of a group (small batches, tests, the drop-in)."""
+    from ..solver import WindowLP
+    return [WindowLP(g.indptr, g.indices, g.data[k], g.c[k], g.q[k], g.l[k], g.u[k], g.m_eq, float(g.c0[k]),
+                     meta={"tag": g.tags[k]}) for k in range(g.G)]
+
+
+def pack_groups(groups):
+    """Concatenate window groups into one numpy PackedBatch (group order, then window order)."""
+    count = sum(g.G for g in groups)
+    desc = np.zeros((count, 8), np.int64)
+    k = 0
+    tr = tz = tn = tm = 0
+    for g in groups:
+        G, n, m, nnz = g.G, g.n, g.m, len(g.indices)
+        kk = np.arange(G, dtype=np.int64)
+        desc[k:k + G] = np.stack([np.full(G, n), np.full(G, m), np.full(G, g.m_eq), np.full(G, nnz),
+                                  tr + kk * (m + 1), tz + kk * nnz, tn + kk * n, tm + kk * m], axis=1)
+        k += G
+        tr += G * (m + 1)
+        tz += G * nnz
+        tn += G * n
+        tm += G * m
+    cat = lambda f, t: np.concatenate([np.ascontiguousarray(getattr(g, f), t).ravel() for g in groups])
+    return PackedBatch(desc=desc,
+                       indptr=np.concatenate([np.tile(g.indptr, g.G) for g in groups]).astype(np.int32),
+                       indices=np.concatenate([np.tile(g.indices, g.G) for g in groups]).astype(np.int32),
+                       data=cat("data", np.float64), c=cat("c", np.float64), c0=cat("c0", np.float64),
+                       q=cat("q", np.float64), l=cat("l", np.float64), u=cat("u", np.float64))
+
+
+def evaluate_terms(g, x):
+    """Objective breakdown per window: {key: [G]} for solutions x [G, n] (the objective_values row)."""
+    return {k: (coef * x).sum(axis=1) + const for k, (coef, const) in g.terms.items()}

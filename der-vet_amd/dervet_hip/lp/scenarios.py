@@ -1,0 +1,153 @@
+"""Scenario / window assembly for the BASELINE.json configurations.
+
+``windows_by_period`` plays the role of storagevet ``Scenario.optimization_levels`` + the per-window
+``set_up_optimization`` of dervet/MicrogridScenario.py:322-346 for many scenarios at once: it splits each
+scenario's time series into optimization windows (n = 'month' | 'year') and builds one WindowGroup per
+window position (all scenarios together, one CSR pattern).
+
+Config 4 (the bench workload): 10,000 perturbations of the config-2 scenario x 12 monthly windows.
+Generator (numpy PCG64), per scenario s with seed 20250217 + s, draws in this order:
+  load scale ~ LogNormal(0, 0.15); AR(1) innovations e_t ~ N(0,1), t < 8760; price scale ~ U[0.7, 1.3];
+  demand charge ~ U[5, 25] $/kW; PV rated ~ U[0, 2000] kW; E ~ U[500, 10000] kWh; duration ~ U[2, 6] h
+  (P = E / duration); rte ~ U[0.80, 0.95].
+  load_t = base_t * scale * (1 + 0.05 a_t),  a_t = 0.9 a_{t-1} + sqrt(1 - 0.81) e_t,  a_0 = e_0.
+"""
+import os
+
+import numpy as np
+
+from . import tariff as _tariff
+from .builder import battery_group
+
+DATA = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data")
+SEED0 = 20250217
+
+
+def reference_inputs():
+    return dict(np.load(os.path.join(DATA, "reference_inputs.npz")))
+
+
+def tariff(name="data_tariff"):
+    return _tariff.load_tariff_json(os.path.join(DATA, f"tariff_{name}.json"))
+
+
+def windows_by_period(year, dt, load, gen, bat, tariff_def=None, da_price=None, n="month", ene_min=None,
+                      ene_max=None, demand_price_override=None, price_scale=None, tags_prefix=None):
+    """Split S scenarios' series [S, Tall] into windows; returns a list of WindowGroup (one per window id).
+
+    demand_price_override [S] replaces every demand charge's $/kW (sweep); price_scale [S] scales energy prices.
+    """
+    load = np.atleast_2d(np.asarray(load, np.float64))
+    S, Tall = load.shape
+    gen = np.zeros_like(load) if gen is None else np.broadcast_to(np.asarray(gen, np.float64), load.shape)
+    month, he, wd, yr = _tariff.calendar(year, Tall, dt)
+    price = None
+    d_ids, d_vals, d_masks = np.zeros(0), np.zeros(0), np.zeros((0, Tall), bool)
+    if tariff_def is not None:
+        price = np.broadcast_to(_tariff.energy_price(tariff_def, month, he, wd), (S, Tall))
+        if price_scale is not None:
+            price = price * np.asarray(price_scale, np.float64)[:, None]
+        d_ids, d_vals, d_masks = _tariff.demand_charges(tariff_def, month, he, wd)
+    if n == "month":
+        wid = (yr - yr[0]) * 12 + month - 1
+    elif n == "year":
+        wid = yr - yr[0]
+    else:
+        wid = np.arange(Tall) // int(n)
+    groups = []
+    for w in np.unique(wid):
+        sel = np.nonzero(wid == w)[0]
+        T = len(sel)
+        masks, prices = [], []
+        for p in range(len(d_vals)):
+            for mo in np.unique(month[sel]):
+                mk = d_masks[p, sel] & (month[sel] == mo)
+                if mk.any():
+                    masks.append(mk)
+                    dp = np.full(S, d_vals[p]) if demand_price_override is None else np.asarray(demand_price_override)
+                    prices.append(dp)
+        masks = np.array(masks, bool).reshape(-1, T)
+        prices = np.stack(prices, axis=1) if prices else np.zeros((S, 0))
+        g = battery_group(
+            T, dt, load[:, sel] - gen[:, sel], bat,
+            retail_price=None if price is None else price[:, sel],
+            da_price=None if da_price is None else np.broadcast_to(np.asarray(da_price, np.float64), (S, Tall))[:, sel],
+            demand_masks=masks, demand_prices=prices,
+            ene_min=None if ene_min is None else np.broadcast_to(ene_min, (S, Tall))[:, sel],
+            ene_max=None if ene_max is None else np.broadcast_to(ene_max, (S, Tall))[:, sel],
+            tags=[(s if tags_prefix is None else tags_prefix[s], int(w)) for s in range(S)])
+        g.index = sel
+        groups.append(g)
+    return groups
+
+
+def template_battery():
+    """Model_Parameters_Template_DER.csv battery (:50-70): 1000 kWh, 250 kW, rte 85 %, hp 100 kW."""
+    return dict(E=1000.0, Pch=250.0, Pdis=250.0, rte=0.85, sdr=0.0, soc_target=1.0, ulsoc=1.0, llsoc=0.0,
+                fixedOM=10.0, OMexpenses=0.0, hp=100.0)
+
+
+def config1(with_retail=False):
+    """Template battery, DA energy time shift on data/hourly_timeseries.csv (incl_site_load = 0), monthly."""
+    ri = reference_inputs()
+    T = len(ri["hourly_da_price"])
+    load = np.zeros((1, T))
+    if with_retail:
+        load = ri["hourly_site_load"][None, :]
+    return windows_by_period(2017, 1.0, load, None, template_battery(),
+                             tariff_def=tariff("data_tariff") if with_retail else None,
+                             da_price=ri["hourly_da_price"][None, :])
+
+
+def config2_battery():
+    return dict(E=4000.0, Pch=1000.0, Pdis=1000.0, rte=0.91, sdr=0.0, soc_target=1.0, ulsoc=1.0, llsoc=0.0,
+                fixedOM=10.0, OMexpenses=0.0, hp=0.0)
+
+
+def config2(years=(2017, 2018, 2019), pv_rated=1000.0):
+    """Battery + fixed PV + DCM + retailETS on data/multi_der_hourly_timeseries.csv, data/tariff.csv,
+    monthly windows over 3 opt years (the same 2017 profile re-used for 2018-19: growth 0)."""
+    ri = reference_inputs()
+    load = ri["multi_der_site_load"]
+    gen = pv_rated * np.nan_to_num(ri["multi_der_pv_profile"])
+    groups = []
+    for y in years:
+        groups += windows_by_period(y, 1.0, load[None, :], gen[None, :], config2_battery(), tariff_def=tariff())
+    return groups
+
+
+def sweep_parameters(scenarios):
+    """Per-scenario draws of the config-4 generator (module docstring)."""
+    scen = np.asarray(list(scenarios), np.int64)
+    S = len(scen)
+    out = dict(load_scale=np.empty(S), eps=np.empty((S, 8760)), price_scale=np.empty(S), demand=np.empty(S),
+               pv_rated=np.empty(S), E=np.empty(S), duration=np.empty(S), rte=np.empty(S))
+    for i, s in enumerate(scen):
+        rng = np.random.Generator(np.random.PCG64(SEED0 + int(s)))
+        out["load_scale"][i] = rng.lognormal(0.0, 0.15)
+        out["eps"][i] = rng.standard_normal(8760)
+        out["price_scale"][i] = rng.uniform(0.7, 1.3)
+        out["demand"][i] = rng.uniform(5.0, 25.0)
+        out["pv_rated"][i] = rng.uniform(0.0, 2000.0)
+        out["E"][i] = rng.uniform(500.0, 10000.0)
+        out["duration"][i] = rng.uniform(2.0, 6.0)
+        out["rte"][i] = rng.uniform(0.80, 0.95)
+    return out
+
+
+def config4(scenarios):
+    """Synthetic sweep windows for the given scenario ids (12 monthly windows each)."""
+    from scipy.signal import lfilter
+    ri = reference_inputs()
+    P = sweep_parameters(scenarios)
+    phi = 0.9
+    e = P["eps"].copy()
+    e[:, 1:] *= np.sqrt(1.0 - phi * phi)
+    a = lfilter([1.0], [1.0, -phi], e, axis=1)
+    load = ri["multi_der_site_load"][None, :] * P["load_scale"][:, None] * (1.0 + 0.05 * a)
+    gen = P["pv_rated"][:, None] * np.nan_to_num(ri["multi_der_pv_profile"])[None, :]
+    E = P["E"]
+    bat = dict(E=E, Pch=E / P["duration"], Pdis=E / P["duration"], rte=P["rte"], sdr=0.0, soc_target=1.0,
+               ulsoc=1.0, llsoc=0.0, fixedOM=10.0, OMexpenses=0.0, hp=0.0)
+    return windows_by_period(2017, 1.0, load, gen, bat, tariff_def=tariff(), demand_price_override=P["demand"],
+                             price_scale=P["price_scale"], tags_prefix=list(scenarios))

@@ -112,6 +112,14 @@ class BatchSolver:
         self._check(self._lib.dvh_last_timing(self._h, t), "dvh_last_timing")
         return {"total_ms": t[0], "setup_ms": t[1], "pdhg_ms": t[2]}
 
+    def kernel_stats(self):
+        v = (ctypes.c_int32 * 4)()
+        self._check(self._lib.dvh_last_stats(self._h, v), "dvh_last_stats")
+        return {"ell_windows": v[0], "generic_windows": v[1], "variant": v[2], "generic_only": bool(v[3])}
+
+    def set_kernel_path(self, generic_only):
+        self._check(self._lib.dvh_set_kernel_path(self._h, int(bool(generic_only))), "dvh_set_kernel_path")
+
     def solve(self, lps):
         """Solve a list of WindowLP on the GPU; returns a list of WindowResult (same order)."""
         count = len(lps)

@@ -53,18 +53,19 @@ extern "C" {
 
 typedef struct dvh_options {
   double eps;                 /* relative KKT tolerance (primal, dual, gap), default 1e-6          */
-  int32_t max_iters;          /* per window, default 200000                                       */
-  int32_t check_every;        /* restart / termination check period, default 64                   */
+  int32_t max_iters;          /* per window, default 100000                                       */
+  int32_t check_every;        /* restart-check period (iterations), default 16                    */
   int32_t ruiz_iters;         /* Ruiz equilibration passes, default 10                            */
   int32_t power_iters;        /* power-iteration steps for ||K||_2, default 64                    */
   double step_safety;         /* eta = step_safety / ||K||_2, default 0.998                       */
   double reflection;          /* Halpern reflection rho in [0,1], default 1                       */
   double restart_sufficient;  /* default 0.2  */
   double restart_necessary;   /* default 0.8  */
-  double restart_artificial;  /* default 0.36 */
-  double primal_weight_theta; /* default 0.5  */
+  double restart_artificial;  /* default 0.1  */
+  double primal_weight_theta; /* default 1.0  */
   int32_t verbose;            /* 0 silent                                                           */
-  int32_t reserved[7];
+  int32_t kkt_every;          /* termination (KKT) check every kkt_every restart checks, default 4 */
+  int32_t reserved[6];
 } dvh_options;
 
 typedef struct dvh_lp {
@@ -141,6 +142,12 @@ int dvh_synchronize(dvh_handle* h);
 /* Timing of the most recent solve on the handle's stream (HIP events, milliseconds):
  * [0] whole solve, [1] setup kernel (transpose + scaling + power iteration), [2] PDHG kernel. */
 int dvh_last_timing(const dvh_handle* h, double* ms3);
+
+/* Kernel-path diagnostics of the most recent solve: out4 = {windows solved by the ELL fast kernel,
+ * windows solved by the generic CSR kernel, kernel variant code, generic_only flag}. */
+int dvh_last_stats(const dvh_handle* h, int32_t* out4);
+/* 1 = force the generic CSR kernel for every window (testing / A-B timing), 0 = default dispatch. */
+int dvh_set_kernel_path(dvh_handle* h, int generic_only);
 
 #ifdef __cplusplus
 }

@@ -14,7 +14,7 @@ Algorithm (restarted reflected Halpern PDHG, PDLP-family):
   3. PDHG operator T(x, y):  x+ = proj_[lt,ut](x - tau (ct - Kt'y));  y+ = proj_Y(y + sigma (qt - Kt(2x+ - x)))
      with proj_Y clamping the >= rows' duals at 0.
   4. reflected Halpern step:  z_{k+1} = (k+1)/(k+2) ((1+rho) T(z_k) - rho z_k) + 1/(k+2) z_anchor
-  5. every ``check_every`` iterations: fixed-point residual r = ||z_k - T(z_k)||_w  with
+  5. every ``check_every`` iterations (termination every ``kkt_every`` such checks): fixed-point residual r = ||z_k - T(z_k)||_w  with
      ||(dx,dy)||_w^2 = w ||dx||^2 + ||dy||^2 / w; restart when r <= b_suff r0, or (r <= b_nec r0 and
      r > r_prev), or k >= b_art * total; on restart z_anchor = z = T(z_k) and the primal weight moves
      halfway (in log space) towards ||dy|| / ||dx|| of the anchor change.
@@ -26,8 +26,9 @@ import numpy as np
 
 OPTIMAL, PRIMAL_INFEASIBLE, DUAL_INFEASIBLE, ITER_LIMIT, NUMERICAL = 0, 1, 2, 3, 4
 
-DEFAULTS = dict(eps=1e-6, max_iters=100000, check_every=64, ruiz_iters=10, power_iters=64, step_safety=0.998,
-                rho=1.0, b_suff=0.2, b_nec=0.8, b_art=0.36, theta=0.5)
+# defaults mirror dvh_default_options (der-vet_amd/csrc/dvh_api.cpp)
+DEFAULTS = dict(eps=1e-6, max_iters=100000, check_every=16, kkt_every=4, ruiz_iters=10, power_iters=64,
+                step_safety=0.998, rho=1.0, b_suff=0.2, b_nec=0.8, b_art=0.1, theta=1.0)
 
 
 def precondition(K, ruiz_iters):
@@ -120,19 +121,22 @@ def solve(lp, opts=None, trace=None):
     it = 0
     rho = o["rho"]
     info = None
+    last = (x, y)
     while it < o["max_iters"]:
         xp, yp = T(x, y)
         it += 1
         if it % o["check_every"] == 0:
             dx, dy = x - xp, y - yp
             r = np.sqrt(w * (dx @ dx) + (dy @ dy) / w)
-            info = kkt(xp, yp)
-            if trace is not None:
-                trace.append((it, k, w, r, info["pres_rel"], info["dres_rel"], info["gap_rel"]))
-            if info["pres_rel"] <= o["eps"] and info["dres_rel"] <= o["eps"] and info["gap_rel"] <= o["eps"]:
-                x, y = xp, yp
-                status = OPTIMAL
-                break
+            if it % (o["check_every"] * o["kkt_every"]) == 0 or it + o["check_every"] > o["max_iters"]:
+                info = kkt(xp, yp)
+                last = (xp, yp)
+                if trace is not None:
+                    trace.append((it, k, w, r, info["pres_rel"], info["dres_rel"], info["gap_rel"]))
+                if info["pres_rel"] <= o["eps"] and info["dres_rel"] <= o["eps"] and info["gap_rel"] <= o["eps"]:
+                    x, y = xp, yp
+                    status = OPTIMAL
+                    break
             if r0 is None:
                 r0 = r
             restart = (r <= o["b_suff"] * r0) or (r <= o["b_nec"] * r0 and r_prev is not None and r > r_prev) \
@@ -151,7 +155,7 @@ def solve(lp, opts=None, trace=None):
         x = (k + 1) / (k + 2) * ((1 + rho) * xp - rho * x) + xa / (k + 2)
         y = (k + 1) / (k + 2) * ((1 + rho) * yp - rho * y) + ya / (k + 2)
         k += 1
-    xs, ys = x, y
+    xs, ys = (x, y) if status == OPTIMAL else last
     info = kkt(xs, ys)
     xo = Dc * xs
     return dict(x=xo, y=Dr * ys, obj=float(c @ xo + c0), status=status, iters=it, kkt=info)
