@@ -1,0 +1,189 @@
+#!/usr/bin/env python3
+"""Bench: dispatch-LP windows/s of the batched HIP PDHG solver (BASELINE.json metric, config 4).
+
+Workload (N=1): BASELINE.json configs[3] -- the synthetic scenario sweep, 10,000 perturbations of the
+config-2 battery + PV + demand-charge + retail scenario (data/multi_der_hourly_timeseries.csv,
+data/tariff.csv) x 12 monthly windows (T = 672..744 hourly steps) = 120,000 window LPs per GPU.
+Multi-GPU (one process per GPU, torchrun): every rank solves its own 10,000-scenario shard (global
+scenario ids rank*S .. rank*S+S-1, weak scaling); no traffic during the solve, then ONE RCCL all-gather
+returns every window's {objective, residuals, status, iterations} to all ranks.
+
+A step = one solve of the rank's whole batch, already resident in HBM (setup kernel: transpose +
+scaling + ||K|| estimate; PDHG kernel: the iterations), plus the result all-gather when N > 1.
+The CPU baseline (rank 0, N=1 only) solves a bounded sample of the same windows with HiGHS on a process
+pool (oracle/cpu_baseline.py) and is also the parity check of the GPU objectives on that sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "der-vet_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "dispatch LP windows/sec (whole node, 8760h monthly windows); % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def alg_bytes_per_iter(desc):
+    """B_iter = 24 nnz + 4 (n + m) + 72 n + 48 m bytes per PDHG iteration per window."""
+    n, m, nnz = desc[:, 0].astype(np.float64), desc[:, 1].astype(np.float64), desc[:, 3].astype(np.float64)
+    return 24 * nnz + 4 * (n + m) + 72 * n + 48 * m
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scenarios", type=int, default=10000, help="scenarios per GPU (x 12 monthly windows)")
+    ap.add_argument("--cpu-sample", type=int, default=960, help="windows in the HiGHS CPU-baseline sample")
+    ap.add_argument("--cpu-procs", type=int, default=0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a GPU (the solver has no CPU fallback)")
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from dervet_hip import BatchSolver
+    from dervet_hip.lp import builder, scenarios
+
+    S = args.scenarios
+    scen = range(rank * S, (rank + 1) * S)
+    t0 = time.time()
+    groups = scenarios.config4(scen)
+    pb = builder.pack_groups(groups)
+    del groups
+    dev = pb.to_torch(f"cuda:{local}").alloc_outputs()
+    build_s = time.time() - t0
+    count = pb.count
+    solver = BatchSolver(local)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    gathered = None
+
+    def step():
+        nonlocal gathered
+        solver.solve_packed(dev)
+        if dist is not None:
+            # the single RCCL all-gather of the results (objective, residuals, status, iterations)
+            pay = torch.cat([dev.stats, dev.istats.to(torch.float64)], dim=1).contiguous()
+            out = [torch.empty_like(pay) for _ in range(world)]
+            dist.all_gather(out, pay)
+            gathered = out
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    t = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    el = time.perf_counter() - t
+    if dist is not None:
+        tt = torch.tensor([el], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    ms_per_step = 1e3 * el / args.steps
+    windows_total = count * world
+    value = windows_total / (el / args.steps)
+
+    # ---- per-window results of the last step (this rank), roofline of the PDHG kernel
+    ist = dev.istats.cpu().numpy()
+    st = dev.stats.cpu().numpy()
+    tm = solver.timing()
+    ks = solver.kernel_stats()
+    iters = ist[:, 1].astype(np.float64)
+    alg = float((alg_bytes_per_iter(pb.desc) * iters).sum())
+    pdhg_s = tm["pdhg_ms"] * 1e-3
+    achieved = alg / pdhg_s / 1e9 if pdhg_s > 0 else None
+    status_counts = np.bincount(ist[:, 0] + 1, minlength=6)[1:].tolist()  # OPTIMAL..NUMERICAL
+    optimal_frac = float(np.mean(ist[:, 0] == 0))
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "pdhg_traffic.json")
+    if os.path.exists(tf):
+        with open(tf) as f:
+            tj = json.load(f)
+        if tj.get("windows") == count:
+            traffic = tj.get("hbm_bytes_per_launch")
+
+    cpu = None
+    parity = None
+    if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0:
+        from oracle import cpu_baseline, window_lp
+        idx = np.linspace(0, count - 1, min(args.cpu_sample, count)).astype(np.int64)
+        lps = [window_lp.from_packed_window(pb.window(int(k))) for k in idx]
+        objs, sts, wall, procs = cpu_baseline.highs_batch(lps, args.cpu_procs or None)
+        cpu = {"value": round(len(idx) / wall, 2), "unit": "windows/s", "cores": procs, "kind": "port",
+               "sample": f"{len(idx)} of the {count} config-4 windows (evenly spaced), restated LP + HiGHS "
+                         f"(scipy {__import__('scipy').__version__}), one LP per process, {procs} processes, "
+                         f"{wall:.1f} s wall"}
+        g = st[idx, 0]
+        ok = sts == 0
+        rel = np.abs(g[ok] - objs[ok]) / np.maximum(np.abs(objs[ok]), 1e-12)
+        parity = {"sample_windows": int(len(idx)), "highs_optimal": int(ok.sum()),
+                  "max_obj_rel_err_vs_highs": float(rel.max()) if ok.any() else None,
+                  "frac_obj_rel_err_le_1e-5": float(np.mean(rel <= 1e-5)) if ok.any() else None}
+
+    line = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "windows/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 2),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: config-4 generator (PCG64 seeds 20250217+s) over data/multi_der_hourly_timeseries.csv "
+                "and data/tariff.csv",
+        "config": {"workload": "config4 sweep: 10,000 scenarios x 12 monthly windows per GPU (battery + PV + "
+                               "DCM + retailETS, T=672-744 h)",
+                   "scenarios_per_gpu": S, "windows_per_gpu": count, "eps_rel_kkt": 1e-6,
+                   "parallelism": f"dp{world} (independent windows, 1 RCCL all-gather of results)"},
+        "scenario_years_per_s": round(value / 12.0, 2),
+        "iters_mean": round(float(iters.mean()), 1),
+        "iters_max": int(iters.max()),
+        "optimal_frac": optimal_frac,
+        "status_counts": status_counts,
+        "max_primal_res_rel": float(np.nanmax(st[:, 1])),
+        "kernel_ms": {"setup": round(tm["setup_ms"], 2), "pdhg": round(tm["pdhg_ms"], 2),
+                      "solve_total": round(tm["total_ms"], 2)},
+        "kernel_path": ks,
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 3) if achieved else None,
+                     "traffic": traffic,
+                     "kernel": "pdhg_ell_kernel (1 launch per step); achieved = sum_w B_iter(w) * iters(w) / "
+                               "kernel time (HIP events on the solver stream)",
+                     "note": "iterate and scaled K are LDS/VGPR-resident, so algorithmic bytes exceed what HBM "
+                             "moves; frac > 1 means the on-chip design beats the HBM roofline"},
+        "cpu_baseline": cpu,
+        "parity": parity,
+        "build_s": round(build_s, 1),
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

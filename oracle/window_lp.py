@@ -177,11 +177,20 @@ def solve_highs(lp, tol=1e-9):
         x = res.x
         out["x"] = x
         out["obj"] = float(lp["c"] @ x + lp["c0"])
-        out["terms"] = {k: float(coef @ x + const) for k, (coef, const) in lp["funcs"].items()}
+        out["terms"] = {k: float(coef @ x + const) for k, (coef, const) in lp.get("funcs", {}).items()}
         # duals (scipy sign convention: eqlin.marginals = d obj / d b_eq; ineqlin for A_ub x <= b_ub)
         y = np.concatenate([res.eqlin.marginals, -res.ineqlin.marginals if A_ub.shape[0] else np.zeros(0)])
         out["y"] = y
     return out
+
+
+def from_packed_window(w):
+    """LP dict (the form build() returns, without objective terms) from a packed-batch window view."""
+    import scipy.sparse as sp
+    K = sp.csr_matrix((np.asarray(w["data"]), np.asarray(w["indices"]), np.asarray(w["indptr"])),
+                      shape=(w["m"], w["n"]))
+    return dict(K=K, q=np.asarray(w["q"]), c=np.asarray(w["c"]), c0=float(w["c0"]), l=np.asarray(w["l"]),
+                u=np.asarray(w["u"]), m_eq=int(w["m_eq"]), funcs={})
 
 
 def evaluate_terms(lp, x):
