@@ -60,8 +60,10 @@ def main():
     from dervet_hip import BatchSolver
     from dervet_hip.lp import builder, scenarios
 
+    from dervet_hip import parallel
+
     S = args.scenarios
-    scen = range(rank * S, (rank + 1) * S)
+    scen = range(*parallel.weak_shard(S, rank))
     t0 = time.time()
     groups = scenarios.config4(scen)
     pb = builder.pack_groups(groups)
@@ -83,10 +85,7 @@ def main():
         solver.solve_packed(dev)
         if dist is not None:
             # the single RCCL all-gather of the results (objective, residuals, status, iterations)
-            pay = torch.cat([dev.stats, dev.istats.to(torch.float64)], dim=1).contiguous()
-            out = [torch.empty_like(pay) for _ in range(world)]
-            dist.all_gather(out, pay)
-            gathered = out
+            gathered = parallel.gather_rows(parallel.result_rows(dev.stats, dev.istats))
 
     for _ in range(args.warmup):
         step()
