@@ -323,6 +323,7 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
     }
     if (!generic.empty()) {
       DVH_HIP(h, hipMemcpyAsync(h->d_list.p, generic.data(), I * generic.size(), hipMemcpyHostToDevice, s));
+      DVH_HIP(h, dvh::launch_power(b, w, c.ch, o, h->d_list.as<int32_t>(), (int)generic.size(), s));
       int gv = -1;
       e = dvh::launch_pdhg(b, w, c.ch, o, c.mn, c.mm, c.mnz, s, &gv, h->d_list.as<int32_t>(), (int)generic.size());
       if (e == hipErrorInvalidValue)

@@ -14,6 +14,7 @@ constexpr int kScal = 16;      // per-window scalars written by the setup kernel
 struct Opts {
   double eps, step_safety, rho, b_suff, b_nec, b_art, theta;
   int max_iters, check_every, kkt_every, ruiz_iters, power_iters;
+  int setup_segments;  // set by launch_setup
 };
 
 // Inputs of one chunk of the packed batch (device pointers, global offsets from desc).
@@ -76,5 +77,8 @@ hipError_t launch_pdhg(const Batch& b, const Work& w, const Chunk& ch, const Opt
 hipError_t launch_pdhg_ell(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n, int max_m,
                            int wx, int wy, hipStream_t s, int* variant_out);
 size_t setup_lds_bytes(int max_n);
+// Power iteration for ||Kt||_2 of the listed windows (generic path; the ELL kernel does its own on chip).
+hipError_t launch_power(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, const int32_t* list, int nlist,
+                        hipStream_t s);
 
 }  // namespace dvh

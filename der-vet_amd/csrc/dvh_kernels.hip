@@ -146,11 +146,20 @@ __device__ __forceinline__ void rows_reduce(const int32_t* ptr, int rows, const 
   for (int L = wid; L < nlong; L += NW) {
     const int i = longl[L];
     const int s = ptr[i], e = ptr[i + 1];
-    double acc = 0.0;
-    for (int p = s + lane; p < e; p += kWave) {
-      const double v = f(p, i);
-      acc = MAXR ? fmax(acc, v) : acc + v;
+    double a4[4] = {0.0, 0.0, 0.0, 0.0};  // 4 independent chains: 4 global loads in flight per lane
+    int p = s + lane;
+    for (; p + 3 * kWave < e; p += 4 * kWave) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const double v = f(p + u * kWave, i);
+        a4[u] = MAXR ? fmax(a4[u], v) : a4[u] + v;
+      }
     }
+    for (; p < e; p += kWave) {
+      const double v = f(p, i);
+      a4[0] = MAXR ? fmax(a4[0], v) : a4[0] + v;
+    }
+    double acc = MAXR ? fmax(fmax(a4[0], a4[1]), fmax(a4[2], a4[3])) : (a4[0] + a4[1]) + (a4[2] + a4[3]);
     acc = MAXR ? wave_max(acc) : wave_sum(acc);
     if (lane == 0) g(i, acc);
   }
@@ -185,19 +194,26 @@ __global__ __launch_bounds__(kSetupB) void setup_kernel(const Batch b, const Wor
   int32_t* longt = w.longt + (int64_t)kl * kLMax;
   double* scal = w.scal + (int64_t)kl * kScal;
 
-  // 1. column counts, entry -> row map
-  for (int j = tid; j <= n; j += kSetupB) cursor[j] = 0;
+  // 1. entry -> row map; per-segment column counts (the nnz are split into nseg contiguous segments, one
+  //    wave each; counts are order-independent, so the layout below is deterministic)
+  const int nseg = o.setup_segments;
+  for (int j = tid; j < nseg * (n + 1); j += kSetupB) cursor[j] = 0;
   __syncthreads();
   for (int i = tid; i < m; i += kSetupB)
     for (int p = Kp[i]; p < Kp[i + 1]; ++p) rowof[p] = i;
-  for (int p = tid; p < nnz; p += kSetupB) atomicAdd(&cursor[Kc[p]], 1);
+  auto seg_lo = [&](int sg) { return (int)(((long long)nnz * sg) / nseg); };
+  for (int sg = 0; sg < nseg; ++sg) {
+    const int a = seg_lo(sg), e = seg_lo(sg + 1);
+    for (int p = a + tid; p < e; p += kSetupB) atomicAdd(&cursor[sg * (n + 1) + Kc[p]], 1);
+  }
   __syncthreads();
-  // 2. exclusive scan of the n counts -> Tp (chunked per thread, partials scanned by thread 0)
+  // 2. column totals, exclusive scan -> Tp; per-segment cursors = Tp + counts of earlier segments
   {
     const int per = (n + kSetupB - 1) / kSetupB;
-    const int s = tid * per, e = min(n, s + per);
+    const int s0 = tid * per, e0 = min(n, s0 + per);
     int acc = 0;
-    for (int j = s; j < e; ++j) acc += cursor[j];
+    for (int j = s0; j < e0; ++j)
+      for (int sg = 0; sg < nseg; ++sg) acc += cursor[sg * (n + 1) + j];
     sh_part[tid] = acc;
     __syncthreads();
     if (tid == 0) {
@@ -210,20 +226,25 @@ __global__ __launch_bounds__(kSetupB) void setup_kernel(const Batch b, const Wor
     }
     __syncthreads();
     int run = sh_part[tid];
-    for (int j = s; j < e; ++j) {
-      const int v = cursor[j];
+    for (int j = s0; j < e0; ++j) {
       Tp[j] = run;
-      cursor[j] = run;
-      run += v;
+      for (int sg = 0; sg < nseg; ++sg) {
+        const int v = cursor[sg * (n + 1) + j];
+        cursor[sg * (n + 1) + j] = run;
+        run += v;
+      }
     }
     if (tid == 0) Tp[n] = nnz;
   }
   __syncthreads();
-  // 3. stable fill of K^T by wave 0 (entries visited in row-major order; ties ranked by lane).
-  if (wid == 0) {
-    for (int base = 0; base < nnz; base += kWave) {
+  // 3. stable fill of K^T, wave sg walks segment sg in row-major order; ties inside a 64-entry chunk are
+  //    ranked by lane
+  if (wid < nseg) {
+    int32_t* cur = cursor + wid * (n + 1);
+    const int a = seg_lo(wid), e = seg_lo(wid + 1);
+    for (int base = a; base < e; base += kWave) {
       const int p = base + lane;
-      const bool v = p < nnz;
+      const bool v = p < e;
       const int j = v ? Kc[p] : -1 - lane;
       int rank = 0, cnt = 0;
       for (int l = 0; l < kWave; ++l) {
@@ -234,16 +255,19 @@ __global__ __launch_bounds__(kSetupB) void setup_kernel(const Batch b, const Wor
         }
       }
       int pos = 0;
-      if (v) pos = cursor[j] + rank;
+      if (v) pos = cur[j] + rank;
       __builtin_amdgcn_wave_barrier();
       if (v) {
         Ti[pos] = rowof[p];
         Tv[pos] = Kv[p];
         perm[p] = pos;
-        if (rank == cnt - 1) cursor[j] = pos + 1;
+        if (rank == cnt - 1) cur[j] = pos + 1;
       }
       __builtin_amdgcn_wave_barrier();
     }
+  }
+  __syncthreads();
+  if (wid == 0) {
     // 4. long-row lists (deterministic ballot compaction)
     int nk = 0, nt = 0;
     for (int base = 0; base < m; base += kWave) {
@@ -320,29 +344,6 @@ __global__ __launch_bounds__(kSetupB) void setup_kernel(const Batch b, const Wor
     nrm[3] += qi * qi;
   }
   block_sum<kSetupB, 4>(nrm, red);
-  // 7. power iteration on Kt'Kt
-  double* v = w.vbuf + W.wn;
-  double* wv = w.wbuf + W.wm;
-  const double v0 = 1.0 / sqrt((double)(n > 0 ? n : 1));
-  for (int j = tid; j < n; j += kSetupB) v[j] = v0;
-  __syncthreads();
-  double sig = 0.0;
-  for (int it = 0; it < o.power_iters; ++it) {
-    rows_reduce<false>(Kp, m, longk, nlk, [&](int p, int) { return KV[p] * v[Kc[p]]; },
-                       [&](int i, double a) { wv[i] = a; });
-    __syncthreads();
-    double s2[1] = {0.0};
-    rows_reduce<false>(Tp, n, longt, nlt, [&](int p, int) { return Tv[p] * wv[Ti[p]]; },
-                       [&](int j, double a) { tmpc[j] = a; });
-    __syncthreads();
-    for (int j = tid; j < n; j += kSetupB) s2[0] += tmpc[j] * tmpc[j];
-    block_sum<kSetupB, 1>(s2, red);
-    const double nv = sqrt(s2[0]);
-    sig = sqrt(nv);
-    const double inv = nv > 0.0 ? 1.0 / nv : 0.0;
-    for (int j = tid; j < n; j += kSetupB) v[j] = tmpc[j] * inv;
-    __syncthreads();
-  }
   // 8. row-length statistics for the ELL fast path: max length among rows with <= kEllMax entries and
   //    the number of longer rows, for K and K^T
   double wst[4] = {0.0, 0.0, 0.0, 0.0};
@@ -371,13 +372,62 @@ __global__ __launch_bounds__(kSetupB) void setup_kernel(const Batch b, const Wor
   }
   if (tid == 0) {
     const double ncs = sqrt(nrm[0]), nqs = sqrt(nrm[1]);
-    scal[0] = sig > 0.0 ? o.step_safety / sig : 1.0;
+    scal[0] = o.step_safety;  // Pock-Chambolle bound ||Kt|| <= 1; the PDHG kernels refine it (power iteration)
     scal[1] = (ncs > 1e-10 && nqs > 1e-10) ? ncs / nqs : 1.0;
     scal[2] = sqrt(nrm[2]);
     scal[3] = sqrt(nrm[3]);
     scal[4] = (double)nlk;
     scal[5] = (double)nlt;
     scal[6] = 0.0;
+    scal[7] = 1.0;
+  }
+}
+
+// Power iteration on Kt'Kt for the windows of the generic path (the ELL kernel runs its own on chip).
+__global__ __launch_bounds__(kSetupB) void power_kernel(const Batch b, const Work w, const Chunk ch, const Opts o,
+                                                        const int32_t* list) {
+  __shared__ double red[(kSetupB / kWave + 1) * 4];
+  const int k = list[blockIdx.x];
+  const int kl = k - ch.first;
+  const WinOff W = win_offsets(b, ch, k);
+  const int n = W.n, m = W.m;
+  const int tid = threadIdx.x;
+  const int32_t* Kp = b.indptr + W.row;
+  const int32_t* Kc = b.indices + W.nz;
+  const int32_t* Tp = w.tptr + W.wtr;
+  const int32_t* Ti = w.tind + W.wz;
+  const double* Tv = w.tval + W.wz;
+  const double* KV = w.kval + W.wz;
+  double* tmpc = w.tmpc + W.wn;
+  const int32_t* longk = w.longk + (int64_t)kl * kLMax;
+  const int32_t* longt = w.longt + (int64_t)kl * kLMax;
+  double* scal = w.scal + (int64_t)kl * kScal;
+  if (scal[6] != 0.0 || o.power_iters <= 0) return;
+  const int nlk = (int)scal[4], nlt = (int)scal[5];
+  double* v = w.vbuf + W.wn;
+  double* wv = w.wbuf + W.wm;
+  const double v0 = 1.0 / sqrt((double)(n > 0 ? n : 1));
+  for (int j = tid; j < n; j += kSetupB) v[j] = v0;
+  __syncthreads();
+  double sig = 0.0;
+  for (int it = 0; it < o.power_iters; ++it) {
+    rows_reduce<false>(Kp, m, longk, nlk, [&](int p, int) { return KV[p] * v[Kc[p]]; },
+                       [&](int i, double a) { wv[i] = a; });
+    __syncthreads();
+    double s2[1] = {0.0};
+    rows_reduce<false>(Tp, n, longt, nlt, [&](int p, int) { return Tv[p] * wv[Ti[p]]; },
+                       [&](int j, double a) { tmpc[j] = a; });
+    __syncthreads();
+    for (int j = tid; j < n; j += kSetupB) s2[0] += tmpc[j] * tmpc[j];
+    block_sum<kSetupB, 1>(s2, red);
+    const double nv = sqrt(s2[0]);
+    sig = sqrt(nv);
+    const double inv = nv > 0.0 ? 1.0 / nv : 0.0;
+    for (int j = tid; j < n; j += kSetupB) v[j] = tmpc[j] * inv;
+    __syncthreads();
+  }
+  if (tid == 0 && sig > 0.0) {
+    scal[0] = o.step_safety / sig;
     scal[7] = sig;
   }
 }
@@ -1055,7 +1105,102 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
   for (int i = tid; i < m; i += B) Y[i] = 0.0;
   __syncthreads();
 
-  double eta = scal[0], pw = scal[1];
+  double* myPC = partC + wid * kLMax;
+  double* myPR = partR + wid * kLMax;
+  // ---- ||Kt||_2 by power iteration, v <- Kt'(Kt v) for o.power_iters steps, on chip with the same ELL
+  //      slices and dense-row scatter as the half-steps; sigma^2 = |v_P| / |v_{P-1}| (no per-step
+  //      normalisation: |Kt| <= 1 after Pock-Chambolle scaling, so v only shrinks by sigma^2 per step)
+  double eta = scal[0];
+  if (o.power_iters > 0) {
+    const int P = o.power_iters;
+    const double v0 = 1.0 / sqrt((double)n);
+    double vc[XS];
+#pragma unroll
+    for (int s = 0; s < XS; ++s) vc[s] = xown[s] ? v0 : 0.0;
+    double nv[2] = {0.0, 0.0};  // |v_{P-1}|^2, |v_P|^2
+    for (int pi = 0; pi <= P; ++pi) {
+      if (pi > 0) {  // v_pi = Kt' w (gathers of the Y image; dense columns from the row-side partials)
+#pragma unroll
+        for (int s = 0; s < XS; ++s) {
+          double a = 0.0;
+#pragma unroll
+          for (int e = 0; e < WX; ++e) a += TE[e * RX + tid + s * B] * Y[xi[s][e]];
+          vc[s] = xown[s] ? a : 0.0;
+        }
+      }
+      double lv = 0.0;
+      for (int L = tid; L < nlx; L += B) {
+        if (pi == 0) {
+          lv = v0;
+        } else {
+          lv = 0.0;
+          for (int w2 = 0; w2 < NW; ++w2) {
+            lv += partC[w2 * kLMax + L];
+            partC[w2 * kLMax + L] = 0.0;
+          }
+        }
+        X[lxi[L]] = lv;
+      }
+      if (pi >= P - 1) {
+        double a = 0.0;
+#pragma unroll
+        for (int s = 0; s < XS; ++s) a += vc[s] * vc[s];
+        if (tid < nlx) a += lv * lv;  // nlx <= kLMax <= B: one long column per thread at most
+        nv[pi - (P - 1)] = a;
+      }
+      if (pi == P) break;
+#pragma unroll
+      for (int s = 0; s < XS; ++s)
+        if (xown[s]) X[tid + s * B] = vc[s];
+      if (xtw >= 0) {
+        double a = 0.0;
+#pragma unroll
+        for (int s = 0; s < XS; ++s) a += xs_cf[s] * vc[s];
+        a = wave_sum_dpp(a);
+        if (lane == 0) myPR[xtw] = a;
+      } else if (xtw == -2) {
+#pragma unroll
+        for (int s = 0; s < XS; ++s) wave_scatter(xs_cf[s] * vc[s], xs_tgt[s], myPR);
+      }
+      __syncthreads();
+      // w = Kt v (gathers of the X image; dense rows from the column-side partials)
+      double wr[YS];
+#pragma unroll
+      for (int s = 0; s < YS; ++s) {
+        double a = 0.0;
+#pragma unroll
+        for (int e = 0; e < WY; ++e) a += KE[e * RY + tid + s * B] * X[yi[s][e]];
+        wr[s] = yown[s] ? a : 0.0;
+        if (yown[s]) Y[tid + s * B] = wr[s];
+      }
+      for (int L = tid; L < nly; L += B) {
+        double a = 0.0;
+        for (int w2 = 0; w2 < NW; ++w2) {
+          a += partR[w2 * kLMax + L];
+          partR[w2 * kLMax + L] = 0.0;
+        }
+        Y[lyi[L]] = a;
+      }
+      if (ytw >= 0) {
+        double a = 0.0;
+#pragma unroll
+        for (int s = 0; s < YS; ++s) a += ys_cf[s] * wr[s];
+        a = wave_sum_dpp(a);
+        if (lane == 0) myPC[ytw] = a;
+      } else if (ytw == -2) {
+#pragma unroll
+        for (int s = 0; s < YS; ++s) wave_scatter(ys_cf[s] * wr[s], ys_tgt[s], myPC);
+      }
+      __syncthreads();
+    }
+    block_sum<B, 2>(nv, red);
+    if (nv[0] > 0.0 && nv[1] > 0.0) eta = o.step_safety / sqrt(sqrt(nv[1] / nv[0]));
+    // back to the PDHG starting state: y = 0, empty partials
+    for (int i = tid; i < m; i += B) Y[i] = 0.0;
+    for (int t = tid; t < 2 * NW * kLMax; t += B) partC[t] = 0.0;
+    __syncthreads();
+  }
+  double pw = scal[1];
   const double cnorm = scal[2], qnorm = scal[3], c0 = b.c0[k];
   const double rho = o.rho;
   int it = 0, kin = 0, status = kIterLimit;
@@ -1064,8 +1209,6 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
   if (tid == 0)
     for (int t = 0; t < 4; ++t) fin[t] = NAN;
   const int chk = o.check_every > 0 ? o.check_every : 64;
-  double* myPC = partC + wid * kLMax;
-  double* myPR = partR + wid * kLMax;
 
   double tau = eta / pw, sigma = eta * pw;
   const int kkt_every = o.kkt_every > 0 ? o.kkt_every : 1;
@@ -1427,13 +1570,24 @@ hipError_t ell_dispatch_xy(int xs, int ys, const Batch& b, const Work& w, const 
 
 }  // namespace
 
-size_t setup_lds_bytes(int max_n) { return align16(sizeof(int32_t) * ((size_t)max_n + 1)); }
+int setup_segments(int max_n) { return max_n <= 8000 ? 4 : 1; }
+size_t setup_lds_bytes(int max_n) {
+  return align16(sizeof(int32_t) * (size_t)setup_segments(max_n) * ((size_t)max_n + 1));
+}
 
 hipError_t launch_setup(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n, hipStream_t s) {
   const size_t lds = setup_lds_bytes(max_n);
+  Opts o2 = o;
+  o2.setup_segments = setup_segments(max_n);
   hipError_t e = hipFuncSetAttribute((const void*)setup_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(setup_kernel, dim3(ch.count), dim3(kSetupB), lds, s, b, w, ch, o);
+  hipLaunchKernelGGL(setup_kernel, dim3(ch.count), dim3(kSetupB), lds, s, b, w, ch, o2);
+  return hipGetLastError();
+}
+
+hipError_t launch_power(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, const int32_t* list, int nlist,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(power_kernel, dim3(nlist), dim3(kSetupB), 0, s, b, w, ch, o, list);
   return hipGetLastError();
 }
 

@@ -54,17 +54,16 @@ def precondition(K, ruiz_iters):
 
 
 def power_norm(Kt, iters):
+    """sigma_max(Kt) from `iters` steps of v <- Kt'(Kt v) from v0 = 1/sqrt(n) (no per-step normalisation,
+    as the ELL kernel does it): sigma^2 = |v_iters| / |v_iters-1|."""
     n = Kt.shape[1]
     v = np.ones(n) / np.sqrt(n)
-    s = 0.0
+    prev = v
     for _ in range(iters):
-        w = Kt.T @ (Kt @ v)
-        s = np.sqrt(np.linalg.norm(w))
-        nv = np.linalg.norm(w)
-        if nv == 0:
-            return 1.0
-        v = w / nv
-    return s
+        prev = v
+        v = Kt.T @ (Kt @ v)
+    a, b = np.linalg.norm(prev), np.linalg.norm(v)
+    return np.sqrt(b / a) if a > 0 and b > 0 else 1.0
 
 
 def solve(lp, opts=None, trace=None):
@@ -82,7 +81,8 @@ def solve(lp, opts=None, trace=None):
     KtT = Kt.T.tocsr()
     ct, qt = Dc * c, Dr * q
     lt, ut = l / Dc, u / Dc
-    eta = o["step_safety"] / power_norm(Kt, o["power_iters"])
+    # power_iters = 0: use the Pock-Chambolle bound ||Kt||_2 <= 1 instead of an estimate
+    eta = o["step_safety"] / (power_norm(Kt, o["power_iters"]) if o["power_iters"] > 0 else 1.0)
     nc, nq = np.linalg.norm(ct), np.linalg.norm(qt)
     w = nc / nq if (nc > 1e-10 and nq > 1e-10) else 1.0
     q_norm, c_norm = np.linalg.norm(q), np.linalg.norm(c)
