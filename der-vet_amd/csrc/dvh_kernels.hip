@@ -62,6 +62,18 @@ __device__ __forceinline__ double wave_sum_dpp(double v) {
   return v;
 }
 
+// Primal-weight update w <- exp(theta log(ratio) + (1 - theta) log(w)) (PDLP smoothing).  theta = 1 and
+// theta = 0.5 have closed forms; the general case is a separate (non-inlined) function so that the
+// exp / log polynomial constants are not hoisted into the iteration loop's registers.
+__device__ __noinline__ double pw_update_general(double ratio, double w, double theta) {
+  return exp(theta * log(ratio) + (1.0 - theta) * log(w));
+}
+__device__ __forceinline__ double pw_update(double ratio, double w, double theta) {
+  if (theta == 1.0) return ratio;
+  if (theta == 0.5) return sqrt(ratio * w);
+  return pw_update_general(ratio, w, theta);
+}
+
 // Makes an index opaque to the optimiser so that address arithmetic of cold (check-phase) code is not
 // hoisted out of the iteration loop into long-lived VGPRs.
 __device__ __forceinline__ int opaque(int v) {
@@ -797,7 +809,7 @@ __global__ __launch_bounds__(B) void pdhg_kernel(const Batch b, const Work w, co
                          ((double)kin >= o.b_art * (double)it);
     if (restart) {
       const double ddx = sqrt(acc[1]), ddy = sqrt(acc[3]);
-      if (ddx > 1e-10 && ddy > 1e-10) pw = exp(o.theta * log(ddy / ddx) + (1.0 - o.theta) * log(pw));
+      if (ddx > 1e-10 && ddy > 1e-10) pw = pw_update(ddy / ddx, pw, o.theta);
 #pragma unroll
       for (int s = 0; s < XS; ++s)
         if (ts[s] >= 0) x[s] = xa[s] = xo_g[tid + s * B];
@@ -877,7 +889,7 @@ __device__ __forceinline__ void wave_scatter(double v, int tgt, double* part) {
 
 __host__ __device__ inline size_t ell_lds_bytes(int n, int m, int B, int XS, int YS, int WX, int WY) {
   const int NW = B / kWave;
-  size_t d = (size_t)n + m + (size_t)WX * XS * B + (size_t)WY * YS * B + 2 * (size_t)NW * kLMax +
+  size_t d = (size_t)n + m + 2 * (size_t)B + (size_t)WX * XS * B + (size_t)WY * YS * B + 2 * (size_t)NW * kLMax +
              (size_t)kNRed * (NW + 1) + 4 + 12 * kLMax;
   return align16(sizeof(double) * d) + align16(sizeof(int32_t) * 4 * kLMax);
 }
@@ -905,8 +917,8 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
   }
   // ---- LDS carve
   double* X = reinterpret_cast<double*>(smem);
-  double* Y = X + n;
-  double* TE = Y + m;              // [WX][RX]
+  double* Y = X + n + B;           // X has B dummy slots [n, n+B) for stores of non-owning lanes
+  double* TE = Y + m + B;          // [WX][RX]   (Y likewise)
   double* KE = TE + WX * RX;       // [WY][RY]
   double* partC = KE + WY * RY;    // [NW][kLMax]  partial K'y of long columns
   double* partR = partC + NW * kLMax;  // [NW][kLMax] partial K xbar of long rows
@@ -915,8 +927,8 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
   double* ly = lx + 6 * kLMax;          // long rows: y, ya, q, yp
   double* lkt = ly + 4 * kLMax;         // long columns: K'y+ of the last check (restart)
   int32_t* ints = reinterpret_cast<int32_t*>(
-      smem + align16(sizeof(double) * ((size_t)n + m + (size_t)WX * RX + (size_t)WY * RY + 2 * (size_t)NW * kLMax +
-                                       (size_t)kNRed * (NW + 1) + 4 + 12 * kLMax)));
+      smem + align16(sizeof(double) * ((size_t)n + m + 2 * B + (size_t)WX * RX + (size_t)WY * RY +
+                                       2 * (size_t)NW * kLMax + (size_t)kNRed * (NW + 1) + 4 + 12 * kLMax)));
   int32_t* lxi = ints;            // long column ids
   int32_t* lyi = ints + kLMax;    // long row ids
   int32_t* cnt = ints + 2 * kLMax;  // [0] nlx, [1] nly, [2] bad flag
@@ -979,6 +991,7 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
 
   // ---- lane-owned state
   int xi[XS][WX];
+  int xst[XS];  // LDS store slot of the X image (own column or this lane's dummy slot)
   double x[XS], xa[XS], cc[XS], lo[XS], hi[XS];
   int xs_tgt[XS];  // long K row fed by this column (scatter target)
   double xs_cf[XS];
@@ -991,15 +1004,17 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
     xs_cf[s] = 0.0;
     x[s] = xa[s] = cc[s] = lo[s] = 0.0;
     hi[s] = 0.0;
+    xst[s] = n + tid;
     int a0 = 0, len = 0;
     if (j < n) {
       a0 = gtp[j];
       len = gtp[j + 1] - a0;
       if (len <= WX) {
         xown[s] = true;
+        xst[s] = j;
         cc[s] = cs[j];
-        lo[s] = ls[j];
-        hi[s] = us[j];
+        lo[s] = __builtin_canonicalize(ls[j]);  // lets the clamps below skip per-use canonicalisation
+        hi[s] = __builtin_canonicalize(us[j]);
         x[s] = xa[s] = fmin(fmax(0.0, lo[s]), hi[s]);
       }
     }
@@ -1020,6 +1035,7 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
     }
   }
   int yi[YS][WY];
+  int yst[YS];
   double y[YS], ya[YS], qq[YS];
   int ys_tgt[YS];
   double ys_cf[YS];
@@ -1031,12 +1047,14 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
     ys_tgt[s] = -1;
     ys_cf[s] = 0.0;
     y[s] = ya[s] = qq[s] = 0.0;
+    yst[s] = m + tid;
     int a0 = 0, len = 0;
     if (i < m) {
       a0 = gkp[i];
       len = gkp[i + 1] - a0;
       if (len <= WY) {
         yown[s] = true;
+        yst[s] = i;
         qq[s] = qs[i];
       }
     }
@@ -1228,20 +1246,16 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
       }
       double xbs[XS];
 #pragma unroll
-      for (int s = 0; s < XS; ++s) {
-        double xb = 0.0;
-        if (xown[s]) {
-          const int j = tid + s * B;
-          const double p1 = fmin(fmax(x[s] - tau * (cc[s] - kty[s]), lo[s]), hi[s]);
-          xb = 2.0 * p1 - x[s];
-          X[j] = xb;
-          if (check) {
-            const int jo = opaque(j);
-            xk_g[jo] = x[s];
-            xo_g[jo] = p1;
-          }
-          x[s] = ca * ((1.0 + rho) * p1 - rho * x[s]) + cb * xa[s];
+      for (int s = 0; s < XS; ++s) {  // branch-free: a non-owning slot has c = lo = hi = 0 and stays at 0
+        const double p1 = fmin(fmax(x[s] - tau * (cc[s] - kty[s]), lo[s]), hi[s]);
+        const double xb = 2.0 * p1 - x[s];
+        X[xst[s]] = xb;
+        if (check && xown[s]) {
+          const int jo = opaque(tid + s * B);
+          xk_g[jo] = x[s];
+          xo_g[jo] = p1;
         }
+        x[s] = ca * ((1.0 + rho) * p1 - rho * x[s]) + cb * xa[s];
         xbs[s] = xb;
       }
       if (xtw >= 0) {
@@ -1284,21 +1298,17 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
       }
       double yns[YS];
 #pragma unroll
-      for (int s = 0; s < YS; ++s) {
-        double yn = 0.0;
-        if (yown[s]) {
-          const int i = tid + s * B;
-          double p1 = y[s] + sigma * (qq[s] - kx[s]);
-          if (i >= meq) p1 = fmax(p1, 0.0);
-          if (check) {
-            const int io = opaque(i);
-            yk_g[io] = y[s];
-            yo_g[io] = p1;
-          }
-          yn = ca * ((1.0 + rho) * p1 - rho * y[s]) + cb * ya[s];
-          y[s] = yn;
-          Y[i] = yn;
+      for (int s = 0; s < YS; ++s) {  // branch-free: a non-owning slot has q = 0 and stays at 0
+        double p1 = y[s] + sigma * (qq[s] - kx[s]);
+        if (tid + s * B >= meq) p1 = fmax(p1, 0.0);  // duals of >= rows stay non-negative
+        if (check && yown[s]) {
+          const int io = opaque(tid + s * B);
+          yk_g[io] = y[s];
+          yo_g[io] = p1;
         }
+        const double yn = ca * ((1.0 + rho) * p1 - rho * y[s]) + cb * ya[s];
+        y[s] = yn;
+        Y[yst[s]] = yn;
         yns[s] = yn;
       }
       if (ytw >= 0) {
@@ -1452,7 +1462,7 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
                          ((double)kin >= o.b_art * (double)it);
     if (restart) {
       const double ddx = sqrt(acc[1]), ddy = sqrt(acc[3]);
-      if (ddx > 1e-10 && ddy > 1e-10) pw = exp(o.theta * log(ddy / ddx) + (1.0 - o.theta) * log(pw));
+      if (ddx > 1e-10 && ddy > 1e-10) pw = pw_update(ddy / ddx, pw, o.theta);
       tau = eta / pw;
       sigma = eta * pw;
       double yns[YS];
