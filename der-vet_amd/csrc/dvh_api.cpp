@@ -303,7 +303,8 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
       wx = std::max(wx, (int)sc[9]);
     }
     int variant = -1;
-    hipError_t e = h->disable_ell ? hipErrorInvalidValue
+    // the ELL kernel is specialised to reflection rho = 1 (the default); other values use the generic kernel
+    hipError_t e = (h->disable_ell || o.rho != 1.0) ? hipErrorInvalidValue
                                   : dvh::launch_pdhg_ell(b, w, c.ch, o, c.mn, c.mm, wx, wy, s, &variant);
     std::vector<int32_t> generic;
     if (e == hipSuccess) {

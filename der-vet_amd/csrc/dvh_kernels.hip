@@ -108,6 +108,33 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double* red) {
   __syncthreads();
 }
 
+// One-barrier variant: per-wave partials in red[wave*NV + k], one __syncthreads, then every lane adds the
+// NW partials in wave order (identical, deterministic result in all lanes).  The caller must not reuse
+// `red` before another barrier has passed (in the PDHG loop the next use is >= 2 barriers later).
+template <int B, int NV>
+__device__ __forceinline__ void block_sum1(double (&v)[NV], double* red) {
+  static_assert(NV <= kWave, "one lane per reduced value");
+  constexpr int NW = B / kWave;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = wave_sum_dpp(v[k]);
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) red[wid * NV + k] = v[k];
+  }
+  __syncthreads();
+  // lane k adds value k over the waves (fixed order), then every value is broadcast from its lane
+  double t = 0.0;
+  if (lane < NV) {
+#pragma unroll
+    for (int w = 0; w < NW; ++w) t += red[w * NV + lane];
+  }
+  const int lo = __double2loint(t), hi = __double2hiint(t);
+#pragma unroll
+  for (int k = 0; k < NV; ++k)
+    v[k] = __hiloint2double(__builtin_amdgcn_readlane(hi, k), __builtin_amdgcn_readlane(lo, k));
+}
+
 struct WinOff {
   int n, m, meq, nnz;
   int64_t row, nz, on, om;     // global offsets (inputs / outputs)
@@ -946,8 +973,6 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
   const double* drv = w.dr + W.wm;
   double* xo_g = b.x + W.on;   // x+ (scaled) at check iterations, final unscaled x
   double* yo_g = b.y + W.om;
-  double* xk_g = w.tmpc + W.wn;  // z_k (pre-step iterate) at check iterations
-  double* yk_g = w.tmpr + W.wm;
 
   // ---- long lists (deterministic ballot compaction by wave 0)
   if (wid == 0) {
@@ -1220,7 +1245,6 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
   }
   double pw = scal[1];
   const double cnorm = scal[2], qnorm = scal[3], c0 = b.c0[k];
-  const double rho = o.rho;
   int it = 0, kin = 0, status = kIterLimit;
   double r0 = -1.0, rprev = -1.0;
   double* fin = red + kNRed * NW;  // obj, pres, dres, gap of the last check (LDS, written by block_sum readers)
@@ -1235,7 +1259,9 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
     const bool check = --ck == 0;
     if (check) ck = chk;
     const double cb = 1.0 / (kin + 2.0), ca = 1.0 - cb;
-    // ---------------- primal half-step
+    // movement norms of this check iteration: |z_k - T(z_k)|^2 and |T(z_k) - z_anchor|^2, primal / dual
+    double mv0 = 0.0, mv1 = 0.0, mv2 = 0.0, mv3 = 0.0;
+    // ---------------- primal half-step (reflection rho = 1: z_{k+1} = ca (2 T(z_k) - z_k) + cb z_anchor)
     {
       double kty[XS];
 #pragma unroll
@@ -1251,11 +1277,12 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
         const double xb = 2.0 * p1 - x[s];
         X[xst[s]] = xb;
         if (check && xown[s]) {
-          const int jo = opaque(tid + s * B);
-          xk_g[jo] = x[s];
-          xo_g[jo] = p1;
+          const double d = x[s] - p1, da = p1 - xa[s];
+          mv0 += d * d;
+          mv1 += da * da;
+          xo_g[opaque(tid + s * B)] = p1;
         }
-        x[s] = ca * ((1.0 + rho) * p1 - rho * x[s]) + cb * xa[s];
+        x[s] = ca * xb + cb * xa[s];
         xbs[s] = xb;
       }
       if (xtw >= 0) {
@@ -1278,12 +1305,15 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
         const int j = lxi[L];
         const double xo = lx[L], xan = lx[kLMax + L];
         const double p1 = fmin(fmax(xo - tau * (lx[2 * kLMax + L] - kt), lx[3 * kLMax + L]), lx[4 * kLMax + L]);
-        X[j] = 2.0 * p1 - xo;
+        const double xb = 2.0 * p1 - xo;
+        X[j] = xb;
         if (check) {
-          xk_g[j] = xo;
+          const double d = xo - p1, da = p1 - xan;
+          mv0 += d * d;
+          mv1 += da * da;
           lx[5 * kLMax + L] = p1;
         }
-        lx[L] = ca * ((1.0 + rho) * p1 - rho * xo) + cb * xan;
+        lx[L] = ca * xb + cb * xan;
       }
     }
     __syncthreads();
@@ -1302,11 +1332,12 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
         double p1 = y[s] + sigma * (qq[s] - kx[s]);
         if (tid + s * B >= meq) p1 = fmax(p1, 0.0);  // duals of >= rows stay non-negative
         if (check && yown[s]) {
-          const int io = opaque(tid + s * B);
-          yk_g[io] = y[s];
-          yo_g[io] = p1;
+          const double d = y[s] - p1, da = p1 - ya[s];
+          mv2 += d * d;
+          mv3 += da * da;
+          yo_g[opaque(tid + s * B)] = p1;
         }
-        const double yn = ca * ((1.0 + rho) * p1 - rho * y[s]) + cb * ya[s];
+        const double yn = ca * (2.0 * p1 - y[s]) + cb * ya[s];
         y[s] = yn;
         Y[yst[s]] = yn;
         yns[s] = yn;
@@ -1332,10 +1363,12 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
         double p1 = yo + sigma * (ly[2 * kLMax + L] - kv);
         if (i >= meq) p1 = fmax(p1, 0.0);
         if (check) {
-          yk_g[i] = yo;
+          const double d = yo - p1, da = p1 - yan;
+          mv2 += d * d;
+          mv3 += da * da;
           ly[3 * kLMax + L] = p1;
         }
-        const double yn = ca * ((1.0 + rho) * p1 - rho * yo) + cb * yan;
+        const double yn = ca * (2.0 * p1 - yo) + cb * yan;
         ly[L] = yn;
         Y[i] = yn;
       }
@@ -1350,37 +1383,27 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
     const bool kkt = (--kk == 0) || (it + chk > o.max_iters);  // the last check before the limit is a KKT one
     if (kkt) kk = kkt_every;
     double acc[kNRed];  // 0..3 movement norms, 4 ||r_p||^2, 5 ||r_d||^2, 6 c'x, 7 q'y, 8 bound term
+    acc[0] = mv0;
+    acc[1] = mv1;
+    acc[2] = mv2;
+    acc[3] = mv3;
 #pragma unroll
-    for (int t = 0; t < kNRed; ++t) acc[t] = 0.0;
+    for (int t = 4; t < kNRed; ++t) acc[t] = 0.0;
+    if (kkt) {  // images of T(z_k) for the KKT products
 #pragma unroll
-    for (int s = 0; s < XS; ++s)
-      if (xown[s]) {
-        const int j = opaque(tid + s * B);
-        const double p1 = xo_g[j], d = xk_g[j] - p1, da = p1 - xa[s];
-        acc[0] += d * d;
-        acc[1] += da * da;
-        if (kkt) X[j] = p1;
-      }
+      for (int s = 0; s < XS; ++s)
+        if (xown[s]) {
+          const int j = opaque(tid + s * B);
+          X[j] = xo_g[j];
+        }
 #pragma unroll
-    for (int s = 0; s < YS; ++s)
-      if (yown[s]) {
-        const int i = opaque(tid + s * B);
-        const double p1 = yo_g[i], d = yk_g[i] - p1, da = p1 - ya[s];
-        acc[2] += d * d;
-        acc[3] += da * da;
-        if (kkt) Y[i] = p1;
-      }
-    for (int L = tid; L < nlx; L += B) {
-      const double p1 = lx[5 * kLMax + L], d = xk_g[lxi[L]] - p1, da = p1 - lx[kLMax + L];
-      acc[0] += d * d;
-      acc[1] += da * da;
-      if (kkt) X[lxi[L]] = p1;
-    }
-    for (int L = tid; L < nly; L += B) {
-      const double p1 = ly[3 * kLMax + L], d = yk_g[lyi[L]] - p1, da = p1 - ly[kLMax + L];
-      acc[2] += d * d;
-      acc[3] += da * da;
-      if (kkt) Y[lyi[L]] = p1;
+      for (int s = 0; s < YS; ++s)
+        if (yown[s]) {
+          const int i = opaque(tid + s * B);
+          Y[i] = yo_g[i];
+        }
+      for (int L = tid; L < nlx; L += B) X[lxi[L]] = lx[5 * kLMax + L];
+      for (int L = tid; L < nly; L += B) Y[lyi[L]] = ly[3 * kLMax + L];
     }
     if (kkt) {
       __syncthreads();
@@ -1436,7 +1459,7 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
         if (lane == 0) row_kkt(i, kv, ly[2 * kLMax + L], ly[3 * kLMax + L]);
       }
     }
-    block_sum<B, kNRed>(acc, red);
+    block_sum1<B, kNRed>(acc, red);
     if (kkt) {
       const double pobj = acc[6] + c0, dobj = acc[7] + acc[8] + c0;
       const double pres = sqrt(acc[4]) / (1.0 + qnorm), dres = sqrt(acc[5]) / (1.0 + cnorm);
