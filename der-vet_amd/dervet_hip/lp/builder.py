@@ -60,7 +60,7 @@ def _col(a, G, T=None):
 
 
 def battery_group(T, dt, base_load, bat, retail_price=None, da_price=None, demand_masks=None, demand_prices=None,
-                  ene_min=None, ene_max=None, name="es", tags=None):
+                  ene_min=None, ene_max=None, name="es", tags=None, pv_curtail_max=None, ice=None):
     """Build G windows sharing T steps and the demand masks.
 
     base_load [G, T]  : site load minus fixed generation (kW), hp is added here from ``bat``
@@ -69,6 +69,13 @@ def battery_group(T, dt, base_load, bat, retail_price=None, da_price=None, deman
     retail_price, da_price [G, T] ($/kWh) or None
     demand_masks bool [J, T] ; demand_prices [G, J] ($/kW)
     ene_min / ene_max [G, T] aggregate SOE limits (User / Reliability requirements) or None
+    pv_curtail_max [G, T]: curtailable PV (IntermittentResourceSizing.py:79-91, curtail = 1): variable
+                      0 <= pv_t <= max_t subtracted from the net load (UNPINNED)
+    ice               : dict of [G] arrays rated_power, n, min_power, efficiency (gal/kWh), fuel_cost ($/gal),
+                      variable_om_cost ($/kWh): storagevet RotatingGenerator rows
+                      min_power n on_t <= elec_t <= rated n on_t with on_t in [0, 1] (the opt-in LP relaxation
+                      of the binary commitment, RotatingGeneratorSizing.py:110-136; UNPINNED)
+    Variable order [ch, dis, ene, tau, pv?, elec?, on?]; >= rows: DCM epigraph, then per step the two ICE rows.
     """
     base_load = np.atleast_2d(np.asarray(base_load, np.float64))
     G = base_load.shape[0]
@@ -83,13 +90,23 @@ def battery_group(T, dt, base_load, bat, retail_price=None, da_price=None, deman
     base = base_load + hp[:, None]
     n = 3 * T + J
     ich, idis, iene, itau = 0, T, 2 * T, 3 * T
+    ipv = ielec = ion = -1
+    if pv_curtail_max is not None:
+        ipv = n
+        n += T
+    if ice is not None:
+        ielec, ion = n, n + T
+        n += 2 * T
+    net_extra = [c for c in (ipv, ielec) if c >= 0]  # columns that reduce the net load (-1 coefficient)
     t = np.arange(T)
 
     # ---- pattern: row lengths 1, 4 x (T-1), 3, then 3 per >= row
     rows_i = [np.nonzero(mk)[0] for mk in masks]
     mI = int(sum(len(r) for r in rows_i))
-    m = T + 1 + mI
-    lens = np.concatenate([[1], np.full(T - 1, 4), [3], np.full(mI, 3)]).astype(np.int64)
+    w_dcm = 3 + len(net_extra)
+    m = T + 1 + mI + (2 * T if ice is not None else 0)
+    lens = np.concatenate([[1], np.full(T - 1, 4), [3], np.full(mI, w_dcm),
+                           np.full(2 * T if ice is not None else 0, 2)]).astype(np.int64)
     indptr = np.zeros(m + 1, np.int64)
     np.cumsum(lens, out=indptr[1:])
     nnz = int(indptr[-1])
@@ -118,13 +135,27 @@ def battery_group(T, dt, base_load, bat, retail_price=None, da_price=None, deman
     row = T + 1
     for j, ti in enumerate(rows_i):
         k = len(ti)
-        rr = indptr[row:row + k].reshape(-1, 1) + np.arange(3)
-        indices[rr] = np.stack([ich + ti, idis + ti, np.full(k, itau + j)], axis=1)
+        rr = indptr[row:row + k].reshape(-1, 1) + np.arange(w_dcm)
+        indices[rr] = np.stack([ich + ti, idis + ti, np.full(k, itau + j)] + [c0_ + ti for c0_ in net_extra], axis=1)
         data[:, rr[:, 0]] = -1.0
         data[:, rr[:, 1]] = 1.0
         data[:, rr[:, 2]] = 1.0
+        for e in range(3, w_dcm):
+            data[:, rr[:, e]] = 1.0
         q[:, row:row + k] = base[:, ti]
         row += k
+    if ice is not None:
+        cap = _col(ice["rated_power"], G) * _col(ice.get("n", 1.0), G)
+        pmin = _col(ice.get("min_power", 0.0), G) * _col(ice.get("n", 1.0), G)
+        r1 = indptr[row + 2 * t]        # cap on_t - elec_t >= 0
+        r2 = indptr[row + 2 * t + 1]    # elec_t - pmin on_t >= 0
+        indices[r1], indices[r1 + 1] = ielec + t, ion + t
+        indices[r2], indices[r2 + 1] = ielec + t, ion + t
+        data[:, r1] = -1.0
+        data[:, r1 + 1] = cap[:, None]
+        data[:, r2] = 1.0
+        data[:, r2 + 1] = -pmin[:, None]
+        row += 2 * T
 
     # ---- bounds
     l = np.zeros((G, n))
@@ -139,8 +170,13 @@ def battery_group(T, dt, base_load, bat, retail_price=None, da_price=None, deman
         hi = np.minimum(hi, _col(ene_max, G, T))
     l[:, iene:iene + T] = lo
     u[:, iene:iene + T] = hi
-    l[:, itau:] = -np.inf
-    u[:, itau:] = np.inf
+    l[:, itau:itau + J] = -np.inf
+    u[:, itau:itau + J] = np.inf
+    if ipv >= 0:
+        u[:, ipv:ipv + T] = _col(pv_curtail_max, G, T)
+    if ice is not None:
+        u[:, ielec:ielec + T] = np.inf
+        u[:, ion:ion + T] = 1.0
 
     # ---- objective terms
     terms = {}
@@ -150,6 +186,8 @@ def battery_group(T, dt, base_load, bat, retail_price=None, da_price=None, deman
         coef = np.zeros((G, n))
         coef[:, ich:ich + T] = pr * dt
         coef[:, idis:idis + T] = -pr * dt
+        for c0_ in net_extra:
+            coef[:, c0_:c0_ + T] = -pr * dt
         return coef, (pr * dt * base).sum(axis=1)
 
     if da_price is not None:
@@ -164,6 +202,11 @@ def battery_group(T, dt, base_load, bat, retail_price=None, da_price=None, deman
     coef = np.zeros((G, n))
     coef[:, idis:idis + T] = (_col(bat.get("OMexpenses", 0.0), G) / 1000.0 * dt)[:, None]
     terms[f"{name} var_om"] = (coef, np.zeros(G))
+    if ice is not None:
+        coef = np.zeros((G, n))
+        coef[:, ielec:ielec + T] = ((_col(ice["efficiency"], G) * _col(ice["fuel_cost"], G)
+                                     + _col(ice.get("variable_om_cost", 0.0), G)) * dt)[:, None]
+        terms["ice fuel_cost"] = (coef, np.zeros(G))
     c = np.zeros((G, n))
     c0 = np.zeros(G)
     for coef, const in terms.values():

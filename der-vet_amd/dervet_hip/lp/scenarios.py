@@ -32,7 +32,8 @@ def tariff(name="data_tariff"):
 
 
 def windows_by_period(year, dt, load, gen, bat, tariff_def=None, da_price=None, n="month", ene_min=None,
-                      ene_max=None, demand_price_override=None, price_scale=None, tags_prefix=None):
+                      ene_max=None, demand_price_override=None, price_scale=None, tags_prefix=None,
+                      pv_curtail_max=None, ice=None):
     """Split S scenarios' series [S, Tall] into windows; returns a list of WindowGroup (one per window id).
 
     demand_price_override [S] replaces every demand charge's $/kW (sweep); price_scale [S] scales energy prices.
@@ -75,7 +76,9 @@ def windows_by_period(year, dt, load, gen, bat, tariff_def=None, da_price=None, 
             demand_masks=masks, demand_prices=prices,
             ene_min=None if ene_min is None else np.broadcast_to(ene_min, (S, Tall))[:, sel],
             ene_max=None if ene_max is None else np.broadcast_to(ene_max, (S, Tall))[:, sel],
-            tags=[(s if tags_prefix is None else tags_prefix[s], int(w)) for s in range(S)])
+            tags=[(s if tags_prefix is None else tags_prefix[s], int(w)) for s in range(S)],
+            pv_curtail_max=None if pv_curtail_max is None else np.broadcast_to(pv_curtail_max, (S, Tall))[:, sel],
+            ice=ice)
         g.index = sel
         groups.append(g)
     return groups
@@ -151,3 +154,48 @@ def config4(scenarios):
                ulsoc=1.0, llsoc=0.0, fixedOM=10.0, OMexpenses=0.0, hp=0.0)
     return windows_by_period(2017, 1.0, load, gen, bat, tariff_def=tariff(), demand_price_override=P["demand"],
                              price_scale=P["price_scale"], tags_prefix=list(scenarios))
+
+
+def reliability_min_soe(critical_load, hours=4.0, dt=1.0, cap=None):
+    """Synthetic reliability requirement (BASELINE config 5): energy to carry the critical load for the next
+    `hours` hours from every step, min_soe_t = sum_{k=t}^{t+h-1} critical_k dt (the shape of
+    Reliability.min_soe_iterative, Reliability.py:685-733, without the outage simulation; UNPINNED)."""
+    c = np.atleast_2d(np.asarray(critical_load, np.float64))
+    h = int(round(hours / dt))
+    cs = np.concatenate([np.zeros((c.shape[0], 1)), np.cumsum(c, axis=1)], axis=1)
+    T = c.shape[1]
+    idx = np.minimum(np.arange(T) + h, T)
+    out = (cs[:, idx] - cs[:, :T]) * dt
+    if cap is not None:
+        out = np.minimum(out, np.asarray(cap, np.float64).reshape(-1, 1))
+    return out
+
+
+def config5(scenarios, years=20, start_year=2017):
+    """Battery + fixed PV + LP-relaxed ICE + 4-h reliability min-SOE, retail + DCM, monthly windows over
+    `years` opt years (the 2017 profile re-used each year).  Perturbations as config 4 (same seeds) plus
+    ICE fuel cost; ICE parameters from the Usecase3 ES+PV+DG model parameters (750 kW x 7 units,
+    0.0866 gal/kWh) with a 250 kW minimum stable output per unit so the relaxation binds."""
+    from scipy.signal import lfilter
+    ri = reference_inputs()
+    scen = list(scenarios)
+    P = sweep_parameters(scen)
+    e = P["eps"].copy()
+    e[:, 1:] *= np.sqrt(1.0 - 0.81)
+    a = lfilter([1.0], [1.0, -0.9], e, axis=1)
+    load = ri["multi_der_site_load"][None, :] * P["load_scale"][:, None] * (1.0 + 0.05 * a)
+    gen = P["pv_rated"][:, None] * np.nan_to_num(ri["multi_der_pv_profile"])[None, :]
+    E = P["E"]
+    bat = dict(E=E, Pch=E / P["duration"], Pdis=E / P["duration"], rte=P["rte"], sdr=0.0, soc_target=1.0,
+               ulsoc=1.0, llsoc=0.0, fixedOM=10.0, OMexpenses=0.0, hp=0.0)
+    fuel = 2.5 + P["price_scale"]  # U[3.2, 3.8] $/gal, deterministic from the same draws
+    ice = dict(rated_power=750.0, n=7.0, min_power=250.0, efficiency=0.086618705, fuel_cost=fuel,
+               variable_om_cost=0.0)
+    crit = ri["multi_der_critical_load"][None, :] * P["load_scale"][:, None]
+    emin = reliability_min_soe(crit, 4.0, 1.0, cap=E)
+    groups = []
+    for y in range(years):
+        groups += windows_by_period(start_year + y, 1.0, load, gen, bat, tariff_def=tariff(),
+                                    demand_price_override=P["demand"], price_scale=P["price_scale"],
+                                    ene_min=emin, ice=ice, tags_prefix=scen)
+    return groups

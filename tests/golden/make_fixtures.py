@@ -132,6 +132,7 @@ def make_bench_data():
         # config 2 / config 4 base scenario (data/multi_der_hourly_timeseries.csv, 2017 hourly)
         multi_der_site_load=fcol(md, "Site Load (kW)"),
         multi_der_pv_profile=fcol(md, "PV Gen (kW/rated kW)/1"),
+        multi_der_critical_load=fcol(md, "Critical Load (kW)"),
         # config 1 (data/hourly_timeseries.csv)
         hourly_da_price=fcol(hd, "DA Price ($/kWh)"),
         hourly_site_load=fcol(hd, "Site Load (kW)"),
