@@ -56,7 +56,7 @@ struct dvh_handle {
   // workspace
   DevBuf w_tptr, w_tind, w_tval, w_kval, w_rowof, w_perm, w_dr, w_dc, w_cs, w_ls, w_us, w_qs, w_vbuf, w_wbuf,
       w_tmpc, w_tmpr, w_longk, w_longt, w_scal;
-  DevBuf d_list;
+  DevBuf d_list, d_hinv;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<std::array<hipEvent_t, 3>> chunk_events;
   double timing[3] = {0, 0, 0};
@@ -139,6 +139,15 @@ int dvh_create(int device_mask, const dvh_options* opts, dvh_handle** out) {
     return DVH_ERR_HIP;
   }
   for (auto& e : h->ev) hipEventCreate(&e);
+  {  // Halpern weight table 1/(k+2): exact IEEE quotients, identical to the host restatement
+    std::vector<double> tab(dvh::kHalpernTab);
+    for (int k = 0; k < dvh::kHalpernTab; ++k) tab[k] = 1.0 / (k + 2.0);
+    if (h->d_hinv.ensure(sizeof(double) * tab.size()) != hipSuccess ||
+        hipMemcpy(h->d_hinv.p, tab.data(), sizeof(double) * tab.size(), hipMemcpyHostToDevice) != hipSuccess) {
+      dvh_destroy(h);
+      return DVH_ERR_HIP;
+    }
+  }
   *out = h;
   return DVH_OK;
 }
@@ -156,7 +165,7 @@ int dvh_destroy(dvh_handle* h) {
   hipSetDevice(h->device);
   if (h->stream) hipStreamSynchronize(h->stream);
   DevBuf* bufs[] = {&h->d_desc, &h->d_indptr, &h->d_indices, &h->d_data, &h->d_c, &h->d_c0, &h->d_q, &h->d_l,
-                    &h->d_u, &h->d_list, &h->d_x, &h->d_y, &h->d_stats, &h->d_istats, &h->w_tptr, &h->w_tind, &h->w_tval,
+                    &h->d_u, &h->d_list, &h->d_hinv, &h->d_x, &h->d_y, &h->d_stats, &h->d_istats, &h->w_tptr, &h->w_tind, &h->w_tval,
                     &h->w_kval, &h->w_rowof, &h->w_perm, &h->w_dr, &h->w_dc, &h->w_cs, &h->w_ls, &h->w_us,
                     &h->w_qs, &h->w_vbuf, &h->w_wbuf, &h->w_tmpc, &h->w_tmpr, &h->w_longk, &h->w_longt, &h->w_scal};
   for (DevBuf* b : bufs) b->release();
@@ -273,7 +282,7 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
               h->w_rowof.as<int32_t>(), h->w_perm.as<int32_t>(), h->w_dr.as<double>(), h->w_dc.as<double>(),
               h->w_cs.as<double>(), h->w_ls.as<double>(), h->w_us.as<double>(), h->w_qs.as<double>(),
               h->w_vbuf.as<double>(), h->w_wbuf.as<double>(), h->w_tmpc.as<double>(), h->w_tmpr.as<double>(),
-              h->w_longk.as<int32_t>(), h->w_longt.as<int32_t>(), h->w_scal.as<double>()};
+              h->w_longk.as<int32_t>(), h->w_longt.as<int32_t>(), h->d_hinv.as<double>(), h->w_scal.as<double>()};
   DVH_HIP(h, h->d_list.ensure(I * (size_t)wc));
   h->n_ell = h->n_generic = 0;
   h->chunk_events.clear();

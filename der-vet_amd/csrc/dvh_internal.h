@@ -9,6 +9,7 @@ constexpr int kWave = 64;
 constexpr int kLongRow = 32;   // CSR rows longer than this are reduced by a whole wave
 constexpr int kLMax = 64;      // long rows per matrix per window handled on chip
 constexpr int kScal = 16;      // per-window scalars written by the setup kernel
+constexpr int kHalpernTab = 65536;  // table of Halpern weights 1/(k+2)
 
 // Kernel-side copy of dvh_options (POD, passed by value).
 struct Opts {
@@ -54,6 +55,7 @@ struct Work {
   double* tmpr;     // [sum m]
   int32_t* longk;   // [count * kLMax]  long rows of K
   int32_t* longt;   // [count * kLMax]  long rows of K^T (dense columns, e.g. the DCM tau)
+  const double* hinv;  // [kHalpernTab] 1 / (k + 2), k = 0.. (Halpern anchor weights, exact IEEE quotients)
   double* scal;     // [count * kScal]  eta, w0, ||c||, ||q||, nlong(K), nlong(K^T), flag, ||K||,
                     //   max short row len K, K^T (<= 8), #rows > 8 in K, K^T
 };

@@ -666,7 +666,8 @@ __global__ __launch_bounds__(B) void pdhg_kernel(const Batch b, const Work w, co
     const double tau = eta / pw, sigma = eta * pw;
     const bool check = --ck == 0;
     if (check) ck = chk;
-    const double cb = 1.0 / (kin + 2.0), ca = 1.0 - cb;
+    // Halpern weights: 1/(k+2) from the host table (uniform index -> scalar load), exact quotient beyond it
+    const double cb = kin < kHalpernTab ? w.hinv[kin] : 1.0 / (kin + 2.0), ca = 1.0 - cb;
     double acc[kNRed];
 #pragma unroll
     for (int t = 0; t < kNRed; ++t) acc[t] = 0.0;
@@ -1258,11 +1259,18 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
   while (it < o.max_iters) {
     const bool check = --ck == 0;
     if (check) ck = chk;
-    const double cb = 1.0 / (kin + 2.0), ca = 1.0 - cb;
+    // Halpern weights: 1/(k+2) from the host table (uniform index -> scalar load), exact quotient beyond it
+    const double cb = kin < kHalpernTab ? w.hinv[kin] : 1.0 / (kin + 2.0), ca = 1.0 - cb;
     // movement norms of this check iteration: |z_k - T(z_k)|^2 and |T(z_k) - z_anchor|^2, primal / dual
     double mv0 = 0.0, mv1 = 0.0, mv2 = 0.0, mv3 = 0.0;
     // ---------------- primal half-step (reflection rho = 1: z_{k+1} = ca (2 T(z_k) - z_k) + cb z_anchor)
     {
+      // dense columns' K'y partials (from the previous dual half-step): loads issued before the ELL work
+      double ktl = 0.0;
+      if (tid < nlx) {
+#pragma unroll
+        for (int w2 = 0; w2 < NW; ++w2) ktl += partC[w2 * kLMax + tid];
+      }
       double kty[XS];
 #pragma unroll
       for (int s = 0; s < XS; ++s) {
@@ -1295,13 +1303,12 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
 #pragma unroll
         for (int s = 0; s < XS; ++s) wave_scatter(xs_cf[s] * xbs[s], xs_tgt[s], myPR);
       }
-      // long columns: K'y accumulated by the previous dual half-step
-      for (int L = tid; L < nlx; L += B) {
-        double kt = 0.0;
-        for (int w2 = 0; w2 < NW; ++w2) {
-          kt += partC[w2 * kLMax + L];
-          partC[w2 * kLMax + L] = 0.0;
-        }
+      // long columns: K'y accumulated by the previous dual half-step (one per thread: nlx <= kLMax <= B)
+      if (tid < nlx) {
+        const int L = tid;
+        const double kt = ktl;
+#pragma unroll
+        for (int w2 = 0; w2 < NW; ++w2) partC[w2 * kLMax + L] = 0.0;
         const int j = lxi[L];
         const double xo = lx[L], xan = lx[kLMax + L];
         const double p1 = fmin(fmax(xo - tau * (lx[2 * kLMax + L] - kt), lx[3 * kLMax + L]), lx[4 * kLMax + L]);

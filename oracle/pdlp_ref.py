@@ -152,8 +152,10 @@ def solve(lp, opts=None, trace=None):
                 r_prev = None
                 continue
             r_prev = r
-        x = (k + 1) / (k + 2) * ((1 + rho) * xp - rho * x) + xa / (k + 2)
-        y = (k + 1) / (k + 2) * ((1 + rho) * yp - rho * y) + ya / (k + 2)
+        cb = 1.0 / (k + 2)
+        ca = 1.0 - cb
+        x = ca * ((1 + rho) * xp - rho * x) + cb * xa
+        y = ca * ((1 + rho) * yp - rho * y) + cb * ya
         k += 1
     xs, ys = (x, y) if status == OPTIMAL else last
     info = kkt(xs, ys)

@@ -92,3 +92,46 @@ def test_evaluate_terms_matches_objective():
     terms = builder.evaluate_terms(g, x)
     tot = sum(terms.values())
     assert np.allclose(tot, (g.c * x).sum(axis=1) + g.c0, rtol=1e-12)
+
+
+def test_builder_curtailable_pv_ice_and_soc_limits_match_oracle():
+    """Unpinned features (curtailable PV, LP-relaxed ICE, sdr, soc_target, ulsoc/llsoc, hp, two demand
+    periods, DA + retail): the product builder emits the oracle's LP bit for bit."""
+    rng = np.random.default_rng(1)
+    T, G = 48, 2
+    load = rng.random((G, T)) * 500
+    pvmax = rng.random((G, T)) * 300
+    masks = np.zeros((2, T), bool)
+    masks[0, :24] = True
+    masks[1, 24:] = True
+    dprice = np.array([[5.0, 7.0], [6.0, 8.0]])
+    bat = dict(E=1000.0, Pch=250.0, Pdis=250.0, rte=0.9, sdr=0.5, soc_target=0.6, ulsoc=0.95, llsoc=0.1,
+               fixedOM=10.0, OMexpenses=2.0, hp=5.0)
+    ice = dict(rated_power=100.0, n=3.0, min_power=20.0, efficiency=0.08, fuel_cost=3.0, variable_om_cost=0.01)
+    price = rng.random((G, T)) * 0.1
+    g = builder.battery_group(T, 1.0, load, bat, retail_price=price, da_price=2 * price, demand_masks=masks,
+                              demand_prices=dprice, ene_min=np.full((G, T), 150.0), pv_curtail_max=pvmax, ice=ice)
+    for k in range(G):
+        w = dict(T=T, dt=1.0, load=load[k], gen=np.zeros(T), retail_price=price[k], da_price=2 * price[k],
+                 demand=list(zip(dprice[k], masks)), ene_min=np.full(T, 150.0), ene_max=None,
+                 bat=dict(bat, name="es"), pv_curtail_max=pvmax[k], ice=dict(ice))
+        lp = window_lp.build(w)
+        assert np.array_equal(lp["K"].indptr, g.indptr) and np.array_equal(lp["K"].indices, g.indices)
+        assert np.allclose(lp["K"].data, g.data[k], rtol=1e-15, atol=0)
+        assert np.array_equal(lp["q"], g.q[k]) and np.array_equal(lp["l"], g.l[k]) and np.array_equal(lp["u"], g.u[k])
+        assert np.allclose(lp["c"], g.c[k], atol=1e-15) and lp["c0"] == pytest.approx(g.c0[k], rel=1e-12)
+        assert sorted(lp["funcs"]) == sorted(g.terms)
+
+
+def test_config5_windows_solve_with_highs():
+    g = scenarios.config5([0], years=1)
+    assert len(g) == 12 and g[0].n == 5 * 744 + 1 and g[0].m == 4 * 744 + 1
+    gg = g[3]
+    K = sp.csr_matrix((gg.data[0], gg.indices, gg.indptr), shape=(gg.m, gg.n))
+    r = window_lp.solve_highs(dict(K=K, q=gg.q[0], c=gg.c[0], c0=gg.c0[0], l=gg.l[0], u=gg.u[0], m_eq=gg.m_eq))
+    assert r["status"] == 0
+    T = gg.T
+    # reliability min-SOE respected, ICE output within the relaxed commitment bounds
+    assert (r["x"][2 * T:3 * T] >= gg.l[0, 2 * T:3 * T] - 1e-6).all()
+    elec, on = r["x"][3 * T + 1:4 * T + 1], r["x"][4 * T + 1:5 * T + 1]
+    assert (elec <= 750.0 * 7 * on + 1e-6).all() and (elec >= 250.0 * 7 * on - 1e-6).all()
