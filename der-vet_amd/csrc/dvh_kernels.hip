@@ -1265,12 +1265,6 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
     double mv0 = 0.0, mv1 = 0.0, mv2 = 0.0, mv3 = 0.0;
     // ---------------- primal half-step (reflection rho = 1: z_{k+1} = ca (2 T(z_k) - z_k) + cb z_anchor)
     {
-      // dense columns' K'y partials (from the previous dual half-step): loads issued before the ELL work
-      double ktl = 0.0;
-      if (tid < nlx) {
-#pragma unroll
-        for (int w2 = 0; w2 < NW; ++w2) ktl += partC[w2 * kLMax + tid];
-      }
       double kty[XS];
 #pragma unroll
       for (int s = 0; s < XS; ++s) {
@@ -1306,7 +1300,9 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
       // long columns: K'y accumulated by the previous dual half-step (one per thread: nlx <= kLMax <= B)
       if (tid < nlx) {
         const int L = tid;
-        const double kt = ktl;
+        double kt = 0.0;
+#pragma unroll
+        for (int w2 = 0; w2 < NW; ++w2) kt += partC[w2 * kLMax + L];
 #pragma unroll
         for (int w2 = 0; w2 < NW; ++w2) partC[w2 * kLMax + L] = 0.0;
         const int j = lxi[L];

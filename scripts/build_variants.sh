@@ -1,0 +1,12 @@
+#!/bin/bash
+# Build A/B variants of libdervet_hip.so into scripts/_variants/ (dev helper; see scripts/probe_iter.py).
+set -e
+cd "$(dirname "$0")/.."
+mkdir -p scripts/_variants
+C=der-vet_amd/csrc
+for v in "$@"; do
+  name=${v%%:*}; defs=${v#*:}
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wno-unused-result -Wno-unused-value \
+    $defs -o scripts/_variants/lib_$name.so $C/dvh_api.cpp $C/dvh_kernels.hip &
+done
+wait
