@@ -61,8 +61,10 @@ struct dvh_handle {
   std::vector<std::array<hipEvent_t, 3>> chunk_events;
   double timing[3] = {0, 0, 0};
   int last_variant = -1;
-  int n_ell = 0, n_generic = 0;
+  int n_ell = 0, n_generic = 0, n_large = 0;
   bool disable_ell = false;
+  dvh::LargeSolver* large = nullptr;  // grid-wide path for windows above dvh::kSmallMax (created on first use)
+  float large_ms[2] = {0, 0};         // setup, PDHG time of the large windows of the last solve
 };
 
 static int fail(dvh_handle* h, int code, const std::string& msg) {
@@ -171,6 +173,7 @@ int dvh_destroy(dvh_handle* h) {
   for (DevBuf* b : bufs) b->release();
   for (auto& e : h->ev)
     if (e) hipEventDestroy(e);
+  if (h->large) dvh::large_destroy(h->large);
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;
   return DVH_OK;
@@ -190,6 +193,14 @@ int dvh_last_stats(const dvh_handle* h, int32_t* out4) {
   out4[1] = h->n_generic;
   out4[2] = h->last_variant;
   out4[3] = h->disable_ell ? 1 : 0;
+  return DVH_OK;
+}
+
+int dvh_last_path_counts(const dvh_handle* h, int32_t* out3) {
+  if (!h || !out3) return DVH_ERR_ARG;
+  out3[0] = h->n_ell;
+  out3[1] = h->n_generic;
+  out3[2] = h->n_large;
   return DVH_OK;
 }
 
@@ -223,15 +234,22 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
   o.kkt_every = h->opts.kkt_every;
   o.ruiz_iters = h->opts.ruiz_iters;
   o.power_iters = h->opts.power_iters;
+  o.small_max = dvh::kSmallMax;
   dvh::Batch b{bt->desc, bt->indptr, bt->indices, bt->data, bt->c, bt->c0, bt->q, bt->l, bt->u,
                bt->x, bt->y, bt->stats, bt->istats};
   // chunking + workspace sizing
   struct C {
     dvh::Chunk ch;
     int64_t sn, sm, snz;
-    int mn, mm;
+    int mn, mm;      // maxima over the chunk's small windows (the on-chip kernels' LDS sizing)
     int64_t mnz;
+    int nsmall;
   };
+  auto is_large = [&](int k) {
+    const int64_t* d = &desc[8 * (size_t)k];
+    return d[0] > dvh::kSmallMax || d[1] > dvh::kSmallMax;
+  };
+  std::vector<int> large;
   std::vector<C> chunks;
   int64_t wn = 0, wm = 0, wnz = 0;
   int wc = 0;
@@ -248,6 +266,11 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
       c.sn = std::max(c.sn, d[6] + d[0] - c.ch.base_n);
       c.sm = std::max(c.sm, d[7] + d[1] - c.ch.base_m);
       c.snz = std::max(c.snz, d[5] + d[3] - c.ch.base_nz);
+      if (is_large(k)) {
+        large.push_back(k);
+        continue;
+      }
+      ++c.nsmall;
       c.mn = std::max<int>(c.mn, (int)d[0]);
       c.mm = std::max<int>(c.mm, (int)d[1]);
       c.mnz = std::max(c.mnz, d[3]);
@@ -284,14 +307,14 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
               h->w_vbuf.as<double>(), h->w_wbuf.as<double>(), h->w_tmpc.as<double>(), h->w_tmpr.as<double>(),
               h->w_longk.as<int32_t>(), h->w_longt.as<int32_t>(), h->d_hinv.as<double>(), h->w_scal.as<double>()};
   DVH_HIP(h, h->d_list.ensure(I * (size_t)wc));
-  h->n_ell = h->n_generic = 0;
+  h->n_ell = h->n_generic = h->n_large = 0;
+  h->large_ms[0] = h->large_ms[1] = 0.0f;
   h->chunk_events.clear();
   DVH_HIP(h, hipEventRecord(h->ev[0], s));
   std::vector<double> scal;
   std::vector<int32_t> ist;
   for (const C& c : chunks) {
-    if (c.mn + 1 > 40000)
-      return fail(h, DVH_ERR_UNSUPPORTED, "window with more than 40000 variables (large-LP path not built yet)");
+    if (c.nsmall == 0) continue;
     hipEvent_t e0, e1, e2;
     DVH_HIP(h, hipEventCreate(&e0));
     DVH_HIP(h, hipEventCreate(&e1));
@@ -322,12 +345,19 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
       DVH_HIP(h, hipMemcpyAsync(ist.data(), bt->istats + 2 * (size_t)c.ch.first, I * ist.size(),
                                 hipMemcpyDeviceToHost, s));
       DVH_HIP(h, hipStreamSynchronize(s));
-      for (int k = 0; k < c.ch.count; ++k)
+      int nl = 0;
+      for (int k = 0; k < c.ch.count; ++k) {
+        if (is_large(c.ch.first + k)) {
+          ++nl;
+          continue;
+        }
         if (ist[2 * (size_t)k] < 0) generic.push_back(c.ch.first + k);
-      h->n_ell -= (int)generic.size();
+      }
+      h->n_ell -= (int)generic.size() + nl;
     } else if (e == hipErrorInvalidValue) {
       (void)hipGetLastError();
-      for (int k = 0; k < c.ch.count; ++k) generic.push_back(c.ch.first + k);
+      for (int k = 0; k < c.ch.count; ++k)
+        if (!is_large(c.ch.first + k)) generic.push_back(c.ch.first + k);
     } else {
       return hip_fail(h, e, "launch_pdhg_ell");
     }
@@ -346,6 +376,15 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
     DVH_HIP(h, hipEventRecord(e2, s));
     h->last_variant = variant;
   }
+  // windows above the on-chip limits: one at a time, the whole GPU each
+  for (int k : large) {
+    if (!h->large) h->large = dvh::large_create();
+    std::string msg;
+    hipError_t e = dvh::large_solve(h->large, b, k, &desc[8 * (size_t)k], o, h->d_hinv.as<double>(), s, &msg,
+                                    &h->large_ms[0], &h->large_ms[1]);
+    if (e != hipSuccess) return fail(h, DVH_ERR_HIP, "window " + std::to_string(k) + ": " + msg);
+    ++h->n_large;
+  }
   DVH_HIP(h, hipEventRecord(h->ev[3], s));
   return DVH_OK;
 }
@@ -361,6 +400,8 @@ static int finish_timing(dvh_handle* h, hipStream_t s) {
     for (hipEvent_t e : ce) hipEventDestroy(e);
   }
   h->chunk_events.clear();
+  h->timing[1] += h->large_ms[0];
+  h->timing[2] += h->large_ms[1];
   return DVH_OK;
 }
 

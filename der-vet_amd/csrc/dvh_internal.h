@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 namespace dvh {
 
 constexpr int kWave = 64;
@@ -10,12 +12,14 @@ constexpr int kLongRow = 32;   // CSR rows longer than this are reduced by a who
 constexpr int kLMax = 64;      // long rows per matrix per window handled on chip
 constexpr int kScal = 16;      // per-window scalars written by the setup kernel
 constexpr int kHalpernTab = 65536;  // table of Halpern weights 1/(k+2)
+constexpr int kSmallMax = 4096;     // windows with n or m above this go to the grid-wide large-LP path
 
 // Kernel-side copy of dvh_options (POD, passed by value).
 struct Opts {
   double eps, step_safety, rho, b_suff, b_nec, b_art, theta;
   int max_iters, check_every, kkt_every, ruiz_iters, power_iters;
   int setup_segments;  // set by launch_setup
+  int small_max;       // setup skips (scal[6] = 2) windows with n or m above this
 };
 
 // Inputs of one chunk of the packed batch (device pointers, global offsets from desc).
@@ -82,5 +86,13 @@ size_t setup_lds_bytes(int max_n);
 // Power iteration for ||Kt||_2 of the listed windows (generic path; the ELL kernel does its own on chip).
 hipError_t launch_power(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, const int32_t* list, int nlist,
                         hipStream_t s);
+
+// Grid-wide PDHG for one window too large for the workgroup-per-window kernels (dvh_large.hip).
+struct LargeSolver;
+LargeSolver* large_create();
+void large_destroy(LargeSolver* ls);
+// Solves window k (desc row d) of the batch on stream s; writes b.x / b.y / b.stats / b.istats of window k.
+hipError_t large_solve(LargeSolver* ls, const Batch& b, int k, const int64_t* d, const Opts& o, const double* hinv,
+                       hipStream_t s, std::string* err, float* setup_ms, float* pdhg_ms);
 
 }  // namespace dvh

@@ -215,6 +215,13 @@ __global__ __launch_bounds__(kSetupB) void setup_kernel(const Batch b, const Wor
   const int n = W.n, m = W.m, nnz = W.nnz;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   int32_t* cursor = reinterpret_cast<int32_t*>(smem);  // [n + 1]
+  if (n > o.small_max || m > o.small_max) {  // solved by the grid-wide large-LP path (dvh_large.hip)
+    if (tid == 0) {
+      w.scal[(int64_t)kl * kScal] = 0.0;
+      w.scal[(int64_t)kl * kScal + 6] = 2.0;
+    }
+    return;
+  }
 
   const int32_t* Kp = b.indptr + W.row;
   const int32_t* Kc = b.indices + W.nz;

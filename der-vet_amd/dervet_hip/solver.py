@@ -115,7 +115,10 @@ class BatchSolver:
     def kernel_stats(self):
         v = (ctypes.c_int32 * 4)()
         self._check(self._lib.dvh_last_stats(self._h, v), "dvh_last_stats")
-        return {"ell_windows": v[0], "generic_windows": v[1], "variant": v[2], "generic_only": bool(v[3])}
+        c = (ctypes.c_int32 * 3)()
+        self._check(self._lib.dvh_last_path_counts(self._h, c), "dvh_last_path_counts")
+        return {"ell_windows": v[0], "generic_windows": v[1], "variant": v[2], "generic_only": bool(v[3]),
+                "large_windows": c[2]}
 
     def set_kernel_path(self, generic_only):
         self._check(self._lib.dvh_set_kernel_path(self._h, int(bool(generic_only))), "dvh_set_kernel_path")

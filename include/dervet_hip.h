@@ -146,6 +146,9 @@ int dvh_last_timing(const dvh_handle* h, double* ms3);
 /* Kernel-path diagnostics of the most recent solve: out4 = {windows solved by the ELL fast kernel,
  * windows solved by the generic CSR kernel, kernel variant code, generic_only flag}. */
 int dvh_last_stats(const dvh_handle* h, int32_t* out4);
+/* Windows per solver path in the most recent solve: out3 = {ELL kernel, generic CSR kernel, grid-wide
+ * large-LP path (n or m > 4096: one window at a time over the whole GPU, e.g. BASELINE config 3)}. */
+int dvh_last_path_counts(const dvh_handle* h, int32_t* out3);
 /* 1 = force the generic CSR kernel for every window (testing / A-B timing), 0 = default dispatch. */
 int dvh_set_kernel_path(dvh_handle* h, int generic_only);
 

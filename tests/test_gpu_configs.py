@@ -2,8 +2,8 @@
 
 Each test builds windows with the product builder, solves them on cuda:0 with libdervet_hip and checks
 against the oracle (restated LP + HiGHS, oracle/window_lp.py): objective within 1e-5 relative, primal
-residual <= 1e-6 (recomputed here from the returned x).  Config 3 (one 105,120-step window) is not
-supported yet and is checked to fail loudly.
+residual <= 1e-6 (recomputed here from the returned x).  Config 3 (one 105,120-step window) runs on the
+grid-wide large-LP path (der-vet_amd/csrc/dvh_large.hip).
 """
 import numpy as np
 import pytest
@@ -161,13 +161,34 @@ def test_invalid_inputs_raise_with_message(gpu_solver):
         gpu_solver.solve([nanlp])
 
 
-def test_config3_large_window_fails_loudly(gpu_solver):
+def _config3_da():
     ri = scenarios.reference_inputs()
     T = len(ri["fivemin_da_price"])
     assert T == 105120
-    g = scenarios.windows_by_period(2019, 1.0 / 12, np.zeros((1, T)), None, scenarios.template_battery(),
-                                    da_price=ri["fivemin_da_price"][None, :], n="year")
-    lps = _lps(g)
-    assert lps[0].n == 3 * T
-    with pytest.raises(SolverError, match="UNSUPPORTED|40000"):
-        gpu_solver.solve(lps)
+    return scenarios.windows_by_period(2019, 1.0 / 12, np.zeros((1, T)), None, scenarios.template_battery(),
+                                       da_price=ri["fivemin_da_price"][None, :], n="year")
+
+
+def test_config3_annual_5min_window_large_path(gpu_solver):
+    """BASELINE config 3: one 105,120-step annual window (n = 315,360) on the grid-wide large-LP path."""
+    lps = _lps(_config3_da())
+    assert lps[0].n == 3 * 105120
+    res = gpu_solver.solve(lps)
+    assert gpu_solver.kernel_stats()["large_windows"] == 1
+    _check(lps, res, "config3")
+
+
+def test_large_path_with_dcm_columns_in_mixed_batch(gpu_solver):
+    """An annual hourly window with 12 monthly DCM tau columns (long columns -> own workgroups) batched
+    together with monthly windows: each goes to its path, all match HiGHS."""
+    ri = scenarios.reference_inputs()
+    load = ri["multi_der_site_load"][None, :]
+    gen = 1000.0 * np.nan_to_num(ri["multi_der_pv_profile"])[None, :]
+    annual = scenarios.windows_by_period(2017, 1.0, load, gen, scenarios.config2_battery(), tariff_def=scenarios.tariff(),
+                                         n="year")
+    lps = _lps(scenarios.config4([3])[:2]) + _lps(annual) + _lps(scenarios.config4([4])[:1])
+    assert lps[2].n == 3 * 8760 + 12
+    res = gpu_solver.solve(lps)
+    ks = gpu_solver.kernel_stats()
+    assert ks["large_windows"] == 1 and ks["ell_windows"] == 3
+    _check(lps, res, "mixed")
