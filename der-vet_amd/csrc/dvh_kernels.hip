@@ -17,6 +17,8 @@
 
 #include <math.h>
 
+#include <type_traits>
+
 namespace dvh {
 
 namespace {
@@ -38,8 +40,9 @@ __device__ __forceinline__ double wave_max(double v) {
 // Every lane ends with the wave total (lanes may differ in the last bit; callers use one lane's value).
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, false);
+  // row rotations read every lane of the row, so the DPP "old" operand is dead: mov_dpp needs no zeroed copy
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xf, 0xf, false);
   return __hiloint2double(hi, lo);
 }
 __device__ __forceinline__ double wave_sum_dpp(double v) {
@@ -59,6 +62,15 @@ __device__ __forceinline__ double wave_sum_dpp(double v) {
     const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
     v = __hiloint2double(b[0], a[0]) + __hiloint2double(b[1], a[1]);
   }
+  return v;
+}
+
+// Sum over each 16-lane row (every lane of the row gets its row's total; fixed order).
+__device__ __forceinline__ double row_sum16(double v) {
+  v += dpp_f64<0x128>(v);  // row_ror:8
+  v += dpp_f64<0x124>(v);  // row_ror:4
+  v += dpp_f64<0x122>(v);  // row_ror:2
+  v += dpp_f64<0x121>(v);  // row_ror:1
   return v;
 }
 
@@ -83,6 +95,13 @@ __device__ __forceinline__ int opaque(int v) {
 __device__ __forceinline__ double opaque(double v) {
   asm volatile("" : "+v"(v));
   return v;
+}
+
+// Workgroup barrier that orders LDS only.  __syncthreads() is a workgroup release/acquire fence, which also
+// waits for every outstanding global store of the wave to be acknowledged (s_waitcnt vmcnt(0)); in the PDHG
+// loops global memory is only read back by the lane that wrote it, so that wait is pure latency.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 // Block reduction of NV doubles; red must hold (NW + 1) * NV doubles.  Result identical in all threads.
@@ -111,7 +130,7 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double* red) {
 // One-barrier variant: per-wave partials in red[wave*NV + k], one __syncthreads, then every lane adds the
 // NW partials in wave order (identical, deterministic result in all lanes).  The caller must not reuse
 // `red` before another barrier has passed (in the PDHG loop the next use is >= 2 barriers later).
-template <int B, int NV>
+template <int B, int NV, bool LDSB = false>
 __device__ __forceinline__ void block_sum1(double (&v)[NV], double* red) {
   static_assert(NV <= kWave, "one lane per reduced value");
   constexpr int NW = B / kWave;
@@ -122,7 +141,10 @@ __device__ __forceinline__ void block_sum1(double (&v)[NV], double* red) {
 #pragma unroll
     for (int k = 0; k < NV; ++k) red[wid * NV + k] = v[k];
   }
-  __syncthreads();
+  if constexpr (LDSB)
+    lds_barrier();
+  else
+    __syncthreads();
   // lane k adds value k over the waves (fixed order), then every value is broadcast from its lane
   double t = 0.0;
   if (lane < NV) {
@@ -922,14 +944,51 @@ __device__ __forceinline__ void wave_scatter(double v, int tgt, double* part) {
   }
 }
 
-__host__ __device__ inline size_t ell_lds_bytes(int n, int m, int B, int XS, int YS, int WX, int WY) {
+// KR bit 0: the ELL values of K^T live in VGPRs (else in LDS, [WX][RX] column-major slices); bit 1: those of K
+// (else [WY][RY] in LDS).  KR != 0 variants also keep T(z_k) = (x+, y+) of the last check in LDS images
+// (else in the x / y output arrays in HBM).
+__host__ __device__ inline size_t ell_lds_doubles(int n, int m, int B, int XS, int YS, int WX, int WY, int KR) {
   const int NW = B / kWave;
-  size_t d = (size_t)n + m + 2 * (size_t)B + (size_t)WX * XS * B + (size_t)WY * YS * B + 2 * (size_t)NW * kLMax +
-             (size_t)kNRed * (NW + 1) + 4 + 12 * kLMax;
+  const size_t img = (size_t)n + m + 2 * (size_t)B;
+  return img + (KR ? img : 0) + ((KR & 1) ? 0 : (size_t)WX * XS * B) + ((KR & 2) ? 0 : (size_t)WY * YS * B) +
+         2 * (size_t)NW * kLMax + (size_t)kNRed * (NW + 1) + 4 + 12 * kLMax;
+}
+__host__ __device__ inline size_t ell_lds_bytes(int n, int m, int B, int XS, int YS, int WX, int WY, int KR) {
+  const size_t d = ell_lds_doubles(n, m, B, XS, YS, WX, WY, KR);
   return align16(sizeof(double) * d) + align16(sizeof(int32_t) * 4 * kLMax);
 }
 
-template <int B, int XS, int YS, int WX, int WY>
+// LDS f64 load / store at an absolute LDS byte address (precomputed once in a VGPR, so a gather is a single
+// ds_read_b64 with no address arithmetic in the loop).
+typedef __attribute__((address_space(3))) double lds_f64;
+typedef __attribute__((address_space(3))) unsigned char lds_u8;
+__device__ __forceinline__ int lds_addr(const void* p) {
+  return (int)(size_t)(lds_u8*)(p);
+}
+__device__ __forceinline__ double lds_ld(int a) { return *(lds_f64*)(size_t)(unsigned)a; }
+__device__ __forceinline__ void lds_st(int a, double v) { *(lds_f64*)(size_t)(unsigned)a = v; }
+// Plain v_max_f64 / v_min_f64: the operands are finite or +-inf by construction (no NaN inputs), so the
+// IEEE-mode canonicalisation the compiler would insert before every use of a loop-invariant bound is dead.
+__device__ __forceinline__ double vmax(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double vmin(double a, double b) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double uniform(double v) {
+  return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
+                          __builtin_amdgcn_readfirstlane(__double2loint(v)));
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                          __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+
+template <int B, int XS, int YS, int WX, int WY, int KR>
 __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w, const Chunk ch, const Opts o) {
   constexpr int NW = B / kWave;
   constexpr int RX = XS * B, RY = YS * B;
@@ -938,7 +997,7 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
   const int kl = blockIdx.x;
   const WinOff W = win_offsets(b, ch, k);
   const int n = W.n, m = W.m, meq = W.meq;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const double* scal = w.scal + (int64_t)kl * kScal;
   auto bail = [&]() {
     if (tid == 0) {
@@ -950,23 +1009,26 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
     bail();
     return;
   }
-  // ---- LDS carve
+  // ---- LDS carve: the x-bar and y images (+ B dummy slots each for stores of non-owning lanes), the
+  //      per-wave partials of the long rows / columns, reduction slots and the long-row state.
+  constexpr bool PL = KR != 0;  // T(z_k) images in LDS
   double* X = reinterpret_cast<double*>(smem);
-  double* Y = X + n + B;           // X has B dummy slots [n, n+B) for stores of non-owning lanes
-  double* TE = Y + m + B;          // [WX][RX]   (Y likewise)
-  double* KE = TE + WX * RX;       // [WY][RY]
-  double* partC = KE + WY * RY;    // [NW][kLMax]  partial K'y of long columns
-  double* partR = partC + NW * kLMax;  // [NW][kLMax] partial K xbar of long rows
+  double* Y = X + n + B;
+  double* XP = Y + m + B;  // PL: x+ / y+ images of the last check, at the same byte distance D from X / Y
+  double* YP = XP + n + B;
+  double* TE = PL ? YP + m + B : XP;           // [WX][RX] K^T values (LDS variant)
+  double* KE = TE + ((KR & 1) ? 0 : WX * RX);  // [WY][RY] K values (LDS variant)
+  double* partC = KE + ((KR & 2) ? 0 : WY * RY);  // [NW][kLMax]  partial K'y of long columns
+  double* partR = partC + NW * kLMax;  // [NW][kLMax]  partial K xbar of long rows
   double* red = partR + NW * kLMax;
   double* lx = red + kNRed * (NW + 1) + 4;  // long columns: x, xa, c, lo, hi, xp
-  double* ly = lx + 6 * kLMax;          // long rows: y, ya, q, yp
-  double* lkt = ly + 4 * kLMax;         // long columns: K'y+ of the last check (restart)
-  int32_t* ints = reinterpret_cast<int32_t*>(
-      smem + align16(sizeof(double) * ((size_t)n + m + 2 * B + (size_t)WX * RX + (size_t)WY * RY +
-                                       2 * (size_t)NW * kLMax + (size_t)kNRed * (NW + 1) + 4 + 12 * kLMax)));
-  int32_t* lxi = ints;            // long column ids
-  int32_t* lyi = ints + kLMax;    // long row ids
-  int32_t* cnt = ints + 2 * kLMax;  // [0] nlx, [1] nly, [2] bad flag
+  double* ly = lx + 6 * kLMax;              // long rows: y, ya, q, yp
+  int32_t* ints = reinterpret_cast<int32_t*>(smem + align16(sizeof(double) * ell_lds_doubles(n, m, B, XS, YS, WX, WY, KR)));
+  int32_t* lxi = ints;              // long column ids
+  int32_t* lyi = ints + kLMax;      // long row ids
+  int32_t* cnt = ints + 2 * kLMax;  // [0] nlx, [1] nly, [2] bad flag, [3] some wave scatters to several targets
+  const int Xa = lds_addr(X), Ya = lds_addr(Y);  // absolute LDS byte addresses of the two images
+  const int D = 8 * (n + m + 2 * B);              // X -> XP and Y -> YP byte distance (PL)
   const int32_t* gkp = b.indptr + W.row;
   const int32_t* gkc = b.indices + W.nz;
   const double* gkv = w.kval + W.wz;
@@ -979,7 +1041,7 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
   const double* qs = w.qs + W.wm;
   const double* dcv = w.dc + W.wn;
   const double* drv = w.dr + W.wm;
-  double* xo_g = b.x + W.on;   // x+ (scaled) at check iterations, final unscaled x
+  double* xo_g = b.x + W.on;  // x+ (scaled) at check iterations, final unscaled x
   double* yo_g = b.y + W.om;
 
   // ---- long lists (deterministic ballot compaction by wave 0)
@@ -1005,6 +1067,7 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
       cnt[0] = nx;
       cnt[1] = ny;
       cnt[2] = 0;
+      cnt[3] = 0;
     }
   }
   // slot maps (in the X / Y images, as int32 before the iteration starts)
@@ -1022,9 +1085,12 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
   for (int L = tid; L < nly; L += B) rmap[lyi[L]] = L;
   __syncthreads();
 
-  // ---- lane-owned state
-  int xi[XS][WX];
-  int xst[XS];  // LDS store slot of the X image (own column or this lane's dummy slot)
+  // ---- lane-owned state: iterate, anchor, objective, bounds, and the ELL slices of K^T (columns) and K
+  //      (rows) -- values and gather offsets -- all in VGPRs for the whole solve.
+  int xi[XS][WX];     // LDS byte addresses in the Y image
+  constexpr bool KRX = (KR & 1) != 0, KRY = (KR & 2) != 0;
+  double tk[KRX ? XS : 1][KRX ? WX : 1];  // scaled K^T values (register variant)
+  int xst[XS];        // byte offset of this slot's X-image store (own column or this lane's dummy slot)
   double x[XS], xa[XS], cc[XS], lo[XS], hi[XS];
   int xs_tgt[XS];  // long K row fed by this column (scatter target)
   double xs_cf[XS];
@@ -1035,19 +1101,18 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
     xown[s] = false;
     xs_tgt[s] = -1;
     xs_cf[s] = 0.0;
-    x[s] = xa[s] = cc[s] = lo[s] = 0.0;
-    hi[s] = 0.0;
-    xst[s] = n + tid;
+    x[s] = xa[s] = cc[s] = lo[s] = hi[s] = 0.0;
+    xst[s] = Xa + 8 * (n + tid);
     int a0 = 0, len = 0;
     if (j < n) {
       a0 = gtp[j];
       len = gtp[j + 1] - a0;
       if (len <= WX) {
         xown[s] = true;
-        xst[s] = j;
+        xst[s] = Xa + 8 * j;
         cc[s] = cs[j];
-        lo[s] = __builtin_canonicalize(ls[j]);  // lets the clamps below skip per-use canonicalisation
-        hi[s] = __builtin_canonicalize(us[j]);
+        lo[s] = ls[j];
+        hi[s] = us[j];
         x[s] = xa[s] = fmin(fmax(0.0, lo[s]), hi[s]);
       }
     }
@@ -1055,8 +1120,11 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
     for (int e = 0; e < WX; ++e) {
       const bool v = xown[s] && e < len;
       const int r = v ? gtc[a0 + e] : 0;
-      xi[s][e] = r;
-      TE[e * RX + tid + s * B] = v ? gtv[a0 + e] : 0.0;
+      xi[s][e] = Ya + 8 * r;
+      if constexpr (KRX)
+        tk[s][e] = v ? gtv[a0 + e] : 0.0;
+      else
+        TE[e * RX + tid + s * B] = v ? gtv[a0 + e] : 0.0;
       if (v) {
         const int L = rmap[r];
         if (L >= 0) {
@@ -1067,9 +1135,11 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
       }
     }
   }
-  int yi[YS][WY];
+  int yi[YS][WY];     // LDS byte addresses in the X image
+  double kk[KRY ? YS : 1][KRY ? WY : 1];  // scaled K values (register variant)
   int yst[YS];
   double y[YS], ya[YS], qq[YS];
+  int ylo_hi[YS];  // high word of the dual lower bound: 0.0 for >= rows (i >= meq), -inf for equality rows
   int ys_tgt[YS];
   double ys_cf[YS];
   bool yown[YS];
@@ -1080,14 +1150,15 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
     ys_tgt[s] = -1;
     ys_cf[s] = 0.0;
     y[s] = ya[s] = qq[s] = 0.0;
-    yst[s] = m + tid;
+    ylo_hi[s] = i >= meq ? 0 : (int)0xFFF00000;
+    yst[s] = Ya + 8 * (m + tid);
     int a0 = 0, len = 0;
     if (i < m) {
       a0 = gkp[i];
       len = gkp[i + 1] - a0;
       if (len <= WY) {
         yown[s] = true;
-        yst[s] = i;
+        yst[s] = Ya + 8 * i;
         qq[s] = qs[i];
       }
     }
@@ -1095,8 +1166,11 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
     for (int e = 0; e < WY; ++e) {
       const bool v = yown[s] && e < len;
       const int c = v ? gkc[a0 + e] : 0;
-      yi[s][e] = c;
-      KE[e * RY + tid + s * B] = v ? gkv[a0 + e] : 0.0;
+      yi[s][e] = Xa + 8 * c;
+      if constexpr (KRY)
+        kk[s][e] = v ? gkv[a0 + e] : 0.0;
+      else
+        KE[e * RY + tid + s * B] = v ? gkv[a0 + e] : 0.0;
       if (v) {
         const int L = cmap[c];
         if (L >= 0) {
@@ -1112,6 +1186,9 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
     for (int p = gkp[i] + lane; p < gkp[i + 1]; p += kWave)
       if (cmap[gkc[p]] >= 0) cnt[2] = 1;
   }
+  for (int t = tid; t < 6 * kLMax; t += B) lx[t] = 0.0;
+  if (tid == 0) ly[4 * kLMax] = 0.0;  // zero slot read by the long-column fast path
+  __syncthreads();
   for (int L = tid; L < nlx; L += B) {
     const int j = lxi[L];
     const double l0 = ls[j], h0 = us[j], x0 = fmin(fmax(0.0, l0), h0);
@@ -1146,18 +1223,93 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
     const bool ok = !__any(multi || (t >= 0 && t != tw));
     return has == 0ull ? -1 : (ok ? tw : -2);  // -1 none, -2 general, >= 0 the single target
   };
-  const int xtw = wave_target(xs_tgt, XS);
-  const int ytw = wave_target(ys_tgt, YS);
+  const int xtw = __builtin_amdgcn_readfirstlane(wave_target(xs_tgt, XS));
+  const int ytw = __builtin_amdgcn_readfirstlane(wave_target(ys_tgt, YS));
+  if (lane == 0 && (xtw == -2 || ytw == -2)) cnt[3] = 1;
+  if (KR && lane == 0 && (xtw == -2 || ytw == -2)) cnt[2] = 1;  // KR variants: single-target waves only
   __syncthreads();
   if (cnt[2] != 0) {
     bail();
     return;
   }
+  // Partials are overwritten (single-target waves) unless some wave accumulates into several targets; then
+  // every consumer must zero what it read.
+  const bool zero_parts = __builtin_amdgcn_readfirstlane(cnt[3]) != 0;
   for (int i = tid; i < m; i += B) Y[i] = 0.0;
+  if constexpr (PL) {  // T(z_0) = z_0 until the first check
+#pragma unroll
+    for (int s = 0; s < XS; ++s) lds_st(xst[s] + D, x[s]);
+#pragma unroll
+    for (int s = 0; s < YS; ++s) lds_st(yst[s] + D, 0.0);
+    for (int L = tid; L < nlx; L += B) XP[lxi[L]] = lx[L];
+    for (int L = tid; L < nly; L += B) YP[lyi[L]] = 0.0;
+  }
   __syncthreads();
 
   double* myPC = partC + wid * kLMax;
   double* myPR = partR + wid * kLMax;
+  // The dense-row contributions of this wave's slots: one DPP reduction when the wave has a single target.
+  auto scatter_rows = [&](const double (&v)[XS]) {  // K xbar of long rows, from the column slots
+    if (xtw >= 0) {
+      double a = 0.0;
+#pragma unroll
+      for (int s = 0; s < XS; ++s) a += xs_cf[s] * v[s];
+      a = wave_sum_dpp(a);
+      if (lane == 0) myPR[xtw] = a;
+    } else if (!KR && xtw == -2) {
+#pragma unroll
+      for (int s = 0; s < XS; ++s) wave_scatter(xs_cf[s] * v[s], xs_tgt[s], myPR);
+    }
+  };
+  auto scatter_cols = [&](const double (&v)[YS]) {  // K'y of long columns, from the row slots
+    if (ytw >= 0) {
+      double a = 0.0;
+#pragma unroll
+      for (int s = 0; s < YS; ++s) a += ys_cf[s] * v[s];
+      a = wave_sum_dpp(a);
+      if (lane == 0) myPC[ytw] = a;
+    } else if (!KR && ytw == -2) {
+#pragma unroll
+      for (int s = 0; s < YS; ++s) wave_scatter(ys_cf[s] * v[s], ys_tgt[s], myPC);
+    }
+  };
+  auto sum_parts = [&](double* part, int L) {
+    double a = 0.0;
+#pragma unroll
+    for (int w2 = 0; w2 < NW; ++w2) a += part[w2 * kLMax + L];
+    if (zero_parts) {
+#pragma unroll
+      for (int w2 = 0; w2 < NW; ++w2) part[w2 * kLMax + L] = 0.0;
+    }
+    return a;
+  };
+  auto ktrans_y = [&](int s, int off = 0) {  // (K^T y)_j of column slot s from the Y image (off = D: YP)
+    double a = 0.0;
+#pragma unroll
+    for (int e = 0; e < WX; ++e) {
+      double v;
+      if constexpr (KRX)
+        v = tk[s][e];
+      else
+        v = TE[e * RX + tid + s * B];
+      a = fma(v, lds_ld(xi[s][e] + off), a);
+    }
+    return a;
+  };
+  auto k_xbar = [&](int s, int off = 0) {  // (K xbar)_i of row slot s from the X image (off = D: XP)
+    double a = 0.0;
+#pragma unroll
+    for (int e = 0; e < WY; ++e) {
+      double v;
+      if constexpr (KRY)
+        v = kk[s][e];
+      else
+        v = KE[e * RY + tid + s * B];
+      a = fma(v, lds_ld(yi[s][e] + off), a);
+    }
+    return a;
+  };
+
   // ---- ||Kt||_2 by power iteration, v <- Kt'(Kt v) for o.power_iters steps, on chip with the same ELL
   //      slices and dense-row scatter as the half-steps; sigma^2 = |v_P| / |v_{P-1}| (no per-step
   //      normalisation: |Kt| <= 1 after Pock-Chambolle scaling, so v only shrinks by sigma^2 per step)
@@ -1172,12 +1324,7 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
     for (int pi = 0; pi <= P; ++pi) {
       if (pi > 0) {  // v_pi = Kt' w (gathers of the Y image; dense columns from the row-side partials)
 #pragma unroll
-        for (int s = 0; s < XS; ++s) {
-          double a = 0.0;
-#pragma unroll
-          for (int e = 0; e < WX; ++e) a += TE[e * RX + tid + s * B] * Y[xi[s][e]];
-          vc[s] = xown[s] ? a : 0.0;
-        }
+        for (int s = 0; s < XS; ++s) vc[s] = xown[s] ? ktrans_y(s) : 0.0;
       }
       double lv = 0.0;
       for (int L = tid; L < nlx; L += B) {
@@ -1203,25 +1350,13 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
 #pragma unroll
       for (int s = 0; s < XS; ++s)
         if (xown[s]) X[tid + s * B] = vc[s];
-      if (xtw >= 0) {
-        double a = 0.0;
-#pragma unroll
-        for (int s = 0; s < XS; ++s) a += xs_cf[s] * vc[s];
-        a = wave_sum_dpp(a);
-        if (lane == 0) myPR[xtw] = a;
-      } else if (xtw == -2) {
-#pragma unroll
-        for (int s = 0; s < XS; ++s) wave_scatter(xs_cf[s] * vc[s], xs_tgt[s], myPR);
-      }
+      scatter_rows(vc);
       __syncthreads();
       // w = Kt v (gathers of the X image; dense rows from the column-side partials)
       double wr[YS];
 #pragma unroll
       for (int s = 0; s < YS; ++s) {
-        double a = 0.0;
-#pragma unroll
-        for (int e = 0; e < WY; ++e) a += KE[e * RY + tid + s * B] * X[yi[s][e]];
-        wr[s] = yown[s] ? a : 0.0;
+        wr[s] = yown[s] ? k_xbar(s) : 0.0;
         if (yown[s]) Y[tid + s * B] = wr[s];
       }
       for (int L = tid; L < nly; L += B) {
@@ -1232,16 +1367,7 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
         }
         Y[lyi[L]] = a;
       }
-      if (ytw >= 0) {
-        double a = 0.0;
-#pragma unroll
-        for (int s = 0; s < YS; ++s) a += ys_cf[s] * wr[s];
-        a = wave_sum_dpp(a);
-        if (lane == 0) myPC[ytw] = a;
-      } else if (ytw == -2) {
-#pragma unroll
-        for (int s = 0; s < YS; ++s) wave_scatter(ys_cf[s] * wr[s], ys_tgt[s], myPC);
-      }
+      scatter_cols(wr);
       __syncthreads();
     }
     block_sum<B, 2>(nv, red);
@@ -1251,8 +1377,9 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
     for (int t = tid; t < 2 * NW * kLMax; t += B) partC[t] = 0.0;
     __syncthreads();
   }
-  double pw = scal[1];
-  const double cnorm = scal[2], qnorm = scal[3], c0 = b.c0[k];
+  eta = uniform(eta);
+  double pw = uniform(scal[1]);
+  const double cnorm = uniform(scal[2]), qnorm = uniform(scal[3]), c0 = uniform(b.c0[k]);
   int it = 0, kin = 0, status = kIterLimit;
   double r0 = -1.0, rprev = -1.0;
   double* fin = red + kNRed * NW;  // obj, pres, dres, gap of the last check (LDS, written by block_sum readers)
@@ -1260,119 +1387,116 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
     for (int t = 0; t < 4; ++t) fin[t] = NAN;
   const int chk = o.check_every > 0 ? o.check_every : 64;
 
-  double tau = eta / pw, sigma = eta * pw;
+  double tau = uniform(eta / pw), sigma = uniform(eta * pw);
   const int kkt_every = o.kkt_every > 0 ? o.kkt_every : 1;
-  int ck = chk, kk = kkt_every;
-  while (it < o.max_iters) {
-    const bool check = --ck == 0;
-    if (check) ck = chk;
-    // Halpern weights: 1/(k+2) from the host table (uniform index -> scalar load), exact quotient beyond it
-    const double cb = kin < kHalpernTab ? w.hinv[kin] : 1.0 / (kin + 2.0), ca = 1.0 - cb;
-    // movement norms of this check iteration: |z_k - T(z_k)|^2 and |T(z_k) - z_anchor|^2, primal / dual
-    double mv0 = 0.0, mv1 = 0.0, mv2 = 0.0, mv3 = 0.0;
-    // ---------------- primal half-step (reflection rho = 1: z_{k+1} = ca (2 T(z_k) - z_k) + cb z_anchor)
+  int ck = chk, kk_ = kkt_every;
+  // Halpern weights 1/(k+2): lane l holds the weight of k = kbase + l; an iteration reads its weight with
+  // v_readlane (uniform lane index -> SGPRs), the slice is reloaded every 64 iterations.
+  int kbase = 0;
+  auto hload = [&](int k0) {
+    const int kq = k0 + lane;
+    return kq < kHalpernTab ? w.hinv[kq] : 1.0 / (kq + 2.0);
+  };
+  double hw = hload(0);
+
+  // long-column fast path (see the primal half-step): wave 0, row r = lane / 16 <-> long column r
+  const bool lc_fast = nlx <= 4 && NW <= 16 && !zero_parts;
+  const bool lc_wave = lc_fast && wid == 0 && nlx > 0;
+  const int lc_r = lane >> 4, lc_p = lane & 15;
+  const int lc_pa = (lc_p < NW && lc_r < nlx) ? lds_addr(partC + lc_p * kLMax + lc_r) : lds_addr(ly + 4 * kLMax);
+  const int lc_la = lds_addr(lx + lc_r);  // x, xa, c, lo, hi, xp at + 8 k kLMax (zeroed for r >= nlx)
+  const int lc_xs = (lc_p == 0 && lc_r < nlx) ? lds_addr(X + lxi[lc_r]) : lds_addr(X + n + tid);
+
+  // One PDHG iteration (reflected Halpern, rho = 1): z_{k+1} = ca (2 T(z_k) - z_k) + cb z_anchor.
+  // CHECK iterations also accumulate the movement norms |z_k - T(z_k)|^2, |T(z_k) - z_anchor|^2 and store
+  // T(z_k) for the restart / KKT checks.
+  double mv0, mv1, mv2, mv3;
+  auto iterate = [&](auto chk_tag, auto longc_tag) __attribute__((always_inline)) {
+    constexpr bool CHECK = decltype(chk_tag)::value;
+    constexpr bool LONGC = decltype(longc_tag)::value;
+    if (kin - kbase >= kWave) {
+      kbase = kin;
+      hw = hload(kin);
+    }
+    const double cb = readlane_f64(hw, kin - kbase), ca = 1.0 - cb;
+    mv0 = mv1 = mv2 = mv3 = 0.0;
+    // ---------------- primal half-step
     {
-      double kty[XS];
-#pragma unroll
-      for (int s = 0; s < XS; ++s) {
-        kty[s] = 0.0;
-#pragma unroll
-        for (int e = 0; e < WX; ++e) kty[s] += TE[e * RX + tid + s * B] * Y[xi[s][e]];
+      // Long columns (the dense DCM tau columns).  Fast path (nlx <= 4, single-target waves): wave 0 does
+      // them branch-free, so it interleaves them with its own slot work: lane 16 r + p reads partial p of
+      // long column r (zero slot when p >= NW or r >= nlx), a DPP row sum gives every lane of row r the
+      // column's K'y (fixed order, deterministic), the row's lanes redo the same projection, and lane 16 r
+      // stores it.  Otherwise one lane per long column sums the partials serially.
+      double lc_kt = 0.0, lc_xo = 0.0, lc_xan = 0.0, lc_c = 0.0, lc_lo = 0.0, lc_hi = 0.0;
+      if constexpr (LONGC) {
+        lc_kt = row_sum16(lds_ld(lc_pa));
+        lc_xo = lds_ld(lc_la);
+        lc_xan = lds_ld(lc_la + 8 * kLMax);
+        lc_c = lds_ld(lc_la + 16 * kLMax);
+        lc_lo = lds_ld(lc_la + 24 * kLMax);
+        lc_hi = lds_ld(lc_la + 32 * kLMax);
       }
-      double xbs[XS];
-#pragma unroll
-      for (int s = 0; s < XS; ++s) {  // branch-free: a non-owning slot has c = lo = hi = 0 and stays at 0
-        const double p1 = fmin(fmax(x[s] - tau * (cc[s] - kty[s]), lo[s]), hi[s]);
-        const double xb = 2.0 * p1 - x[s];
-        X[xst[s]] = xb;
-        if (check && xown[s]) {
-          const double d = x[s] - p1, da = p1 - xa[s];
-          mv0 += d * d;
-          mv1 += da * da;
-          xo_g[opaque(tid + s * B)] = p1;
-        }
-        x[s] = ca * xb + cb * xa[s];
-        xbs[s] = xb;
-      }
-      if (xtw >= 0) {
-        double a = 0.0;
-#pragma unroll
-        for (int s = 0; s < XS; ++s) a += xs_cf[s] * xbs[s];
-        a = wave_sum_dpp(a);
-        if (lane == 0) myPR[xtw] = a;
-      } else if (xtw == -2) {
-#pragma unroll
-        for (int s = 0; s < XS; ++s) wave_scatter(xs_cf[s] * xbs[s], xs_tgt[s], myPR);
-      }
-      // long columns: K'y accumulated by the previous dual half-step (one per thread: nlx <= kLMax <= B)
-      if (tid < nlx) {
+      if (!lc_fast && tid < nlx) {
         const int L = tid;
-        double kt = 0.0;
-#pragma unroll
-        for (int w2 = 0; w2 < NW; ++w2) kt += partC[w2 * kLMax + L];
-#pragma unroll
-        for (int w2 = 0; w2 < NW; ++w2) partC[w2 * kLMax + L] = 0.0;
+        const double kt = sum_parts(partC, L);
         const int j = lxi[L];
         const double xo = lx[L], xan = lx[kLMax + L];
-        const double p1 = fmin(fmax(xo - tau * (lx[2 * kLMax + L] - kt), lx[3 * kLMax + L]), lx[4 * kLMax + L]);
-        const double xb = 2.0 * p1 - xo;
+        const double p1 = vmin(vmax(fma(-tau, lx[2 * kLMax + L] - kt, xo), lx[3 * kLMax + L]), lx[4 * kLMax + L]);
+        const double xb = fma(2.0, p1, -xo);
         X[j] = xb;
-        if (check) {
+        if (CHECK) {
           const double d = xo - p1, da = p1 - xan;
           mv0 += d * d;
           mv1 += da * da;
           lx[5 * kLMax + L] = p1;
         }
-        lx[L] = ca * xb + cb * xan;
+        lx[L] = fma(ca, xb, cb * xan);
       }
+      double kty[XS];
+#pragma unroll
+      for (int s = 0; s < XS; ++s) kty[s] = ktrans_y(s);
+      double xbs[XS];
+#pragma unroll
+      for (int s = 0; s < XS; ++s) {  // branch-free: a non-owning slot has c = lo = hi = 0 and stays at 0
+        const double p1 = vmin(vmax(fma(-tau, cc[s] - kty[s], x[s]), lo[s]), hi[s]);
+        const double xb = fma(2.0, p1, -x[s]);
+        lds_st(xst[s], xb);
+        if (CHECK && xown[s]) {
+          const double d = x[s] - p1, da = p1 - xa[s];
+          mv0 += d * d;
+          mv1 += da * da;
+          if constexpr (PL)
+            lds_st(xst[s] + D, p1);
+          else
+            xo_g[(opaque(tid) + s * B)] = p1;
+        }
+        x[s] = fma(ca, xb, cb * xa[s]);
+        xbs[s] = xb;
+      }
+      if constexpr (LONGC) {
+        const double p1 = vmin(vmax(fma(-tau, lc_c - lc_kt, lc_xo), lc_lo), lc_hi);
+        const double xb = fma(2.0, p1, -lc_xo);
+        lds_st(lc_xs, xb);  // row leaders: X[j]; other lanes: their dummy slot
+        if ((lane & 15) == 0) lds_st(lc_la, fma(ca, xb, cb * lc_xan));
+        if (CHECK && (lane & 15) == 0) {
+          const double d = lc_xo - p1, da = p1 - lc_xan;  // zero in rows >= nlx
+          mv0 += d * d;
+          mv1 += da * da;
+          lds_st(lc_la + 40 * kLMax, p1);
+        }
+      }
+      scatter_rows(xbs);
     }
-    __syncthreads();
+    lds_barrier();
     // ---------------- dual half-step
     {
-      double kx[YS];
-#pragma unroll
-      for (int s = 0; s < YS; ++s) {
-        kx[s] = 0.0;
-#pragma unroll
-        for (int e = 0; e < WY; ++e) kx[s] += KE[e * RY + tid + s * B] * X[yi[s][e]];
-      }
-      double yns[YS];
-#pragma unroll
-      for (int s = 0; s < YS; ++s) {  // branch-free: a non-owning slot has q = 0 and stays at 0
-        double p1 = y[s] + sigma * (qq[s] - kx[s]);
-        if (tid + s * B >= meq) p1 = fmax(p1, 0.0);  // duals of >= rows stay non-negative
-        if (check && yown[s]) {
-          const double d = y[s] - p1, da = p1 - ya[s];
-          mv2 += d * d;
-          mv3 += da * da;
-          yo_g[opaque(tid + s * B)] = p1;
-        }
-        const double yn = ca * (2.0 * p1 - y[s]) + cb * ya[s];
-        y[s] = yn;
-        Y[yst[s]] = yn;
-        yns[s] = yn;
-      }
-      if (ytw >= 0) {
-        double a = 0.0;
-#pragma unroll
-        for (int s = 0; s < YS; ++s) a += ys_cf[s] * yns[s];
-        a = wave_sum_dpp(a);
-        if (lane == 0) myPC[ytw] = a;
-      } else if (ytw == -2) {
-#pragma unroll
-        for (int s = 0; s < YS; ++s) wave_scatter(ys_cf[s] * yns[s], ys_tgt[s], myPC);
-      }
       for (int L = tid; L < nly; L += B) {
-        double kv = 0.0;
-        for (int w2 = 0; w2 < NW; ++w2) {
-          kv += partR[w2 * kLMax + L];
-          partR[w2 * kLMax + L] = 0.0;
-        }
+        const double kv = sum_parts(partR, L);
         const int i = lyi[L];
         const double yo = ly[L], yan = ly[kLMax + L];
         double p1 = yo + sigma * (ly[2 * kLMax + L] - kv);
         if (i >= meq) p1 = fmax(p1, 0.0);
-        if (check) {
+        if (CHECK) {
           const double d = yo - p1, da = p1 - yan;
           mv2 += d * d;
           mv3 += da * da;
@@ -1382,16 +1506,56 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
         ly[L] = yn;
         Y[i] = yn;
       }
+      double kx[YS];
+#pragma unroll
+      for (int s = 0; s < YS; ++s) kx[s] = k_xbar(s);
+      double yns[YS];
+#pragma unroll
+      for (int s = 0; s < YS; ++s) {  // branch-free: a non-owning slot has q = 0 and stays at 0
+        // duals of >= rows stay >= 0 (branch-free: max with 0 or -inf)
+        const double p1 = vmax(fma(sigma, qq[s] - kx[s], y[s]), __hiloint2double(ylo_hi[s], 0));
+        if (CHECK && yown[s]) {
+          const double d = y[s] - p1, da = p1 - ya[s];
+          mv2 += d * d;
+          mv3 += da * da;
+          if constexpr (PL)
+            lds_st(yst[s] + D, p1);
+          else
+            yo_g[(opaque(tid) + s * B)] = p1;
+        }
+        const double yn = fma(ca, fma(2.0, p1, -y[s]), cb * ya[s]);
+        y[s] = yn;
+        lds_st(yst[s], yn);
+        yns[s] = yn;
+      }
+      scatter_cols(yns);
     }
     ++it;
     ++kin;
-    __syncthreads();
-    if (!check) continue;
+    lds_barrier();
+  };
+
+  while (it < o.max_iters) {
+    const bool check = --ck == 0;
+    using F = std::integral_constant<bool, false>;
+    using T = std::integral_constant<bool, true>;
+    if (!check) {
+      if (lc_wave)
+        iterate(F(), T());
+      else
+        iterate(F(), F());
+      continue;
+    }
+    ck = chk;
+    if (lc_wave)
+      iterate(T(), T());
+    else
+      iterate(T(), F());
 
     // ---------------- check (every check_every iterations): fixed-point residual of z_k, restart test;
     // every kkt_every-th check also the relative KKT error of T(z_k) = (x+, y+) in the unscaled space.
-    const bool kkt = (--kk == 0) || (it + chk > o.max_iters);  // the last check before the limit is a KKT one
-    if (kkt) kk = kkt_every;
+    const bool kkt = (--kk_ == 0) || (it + chk > o.max_iters);  // the last check before the limit is a KKT one
+    if (kkt) kk_ = kkt_every;
     double acc[kNRed];  // 0..3 movement norms, 4 ||r_p||^2, 5 ||r_d||^2, 6 c'x, 7 q'y, 8 bound term
     acc[0] = mv0;
     acc[1] = mv1;
@@ -1399,24 +1563,29 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
     acc[3] = mv3;
 #pragma unroll
     for (int t = 4; t < kNRed; ++t) acc[t] = 0.0;
-    if (kkt) {  // images of T(z_k) for the KKT products
-#pragma unroll
-      for (int s = 0; s < XS; ++s)
-        if (xown[s]) {
-          const int j = opaque(tid + s * B);
-          X[j] = xo_g[j];
-        }
-#pragma unroll
-      for (int s = 0; s < YS; ++s)
-        if (yown[s]) {
-          const int i = opaque(tid + s * B);
-          Y[i] = yo_g[i];
-        }
-      for (int L = tid; L < nlx; L += B) X[lxi[L]] = lx[5 * kLMax + L];
-      for (int L = tid; L < nly; L += B) Y[lyi[L]] = ly[3 * kLMax + L];
-    }
+    // The KKT products gather from images of T(z_k): XP / YP (PL; the long slots are copied in here), or
+    // X / Y refilled from the HBM copies (restored after the check unless a restart rewrites them).
+    double* const XK = PL ? XP : X;
+    double* const YK = PL ? YP : Y;
+    const int KO = PL ? D : 0;
     if (kkt) {
-      __syncthreads();
+      if constexpr (!PL) {
+#pragma unroll
+        for (int s = 0; s < XS; ++s)
+          if (xown[s]) {
+            const int j = (opaque(tid) + s * B);
+            X[j] = xo_g[j];
+          }
+#pragma unroll
+        for (int s = 0; s < YS; ++s)
+          if (yown[s]) {
+            const int i = (opaque(tid) + s * B);
+            Y[i] = yo_g[i];
+          }
+      }
+      for (int L = tid; L < nlx; L += B) XK[lxi[L]] = lx[5 * kLMax + L];
+      for (int L = tid; L < nly; L += B) YK[lyi[L]] = ly[3 * kLMax + L];
+      lds_barrier();
       auto col_kkt = [&](int j, double kt, double cj, double loj, double hij, double xj) {
         loj = opaque(loj);
         hij = opaque(hij);
@@ -1436,40 +1605,37 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
         acc[7] += qi * yi2;
       };
 #pragma unroll
-      for (int s = 0; s < XS; ++s) {
-        if (xown[s]) {
-          double kt = 0.0;
+      for (int s = 0; s < XS; ++s)
+        if (xown[s]) col_kkt(tid + s * B, ktrans_y(s, KO), cc[s], lo[s], hi[s], XK[tid + s * B]);
 #pragma unroll
-          for (int e = 0; e < WX; ++e) kt += TE[e * RX + tid + s * B] * Y[xi[s][e]];
-          col_kkt(tid + s * B, kt, cc[s], lo[s], hi[s], X[tid + s * B]);
-        }
-      }
-#pragma unroll
-      for (int s = 0; s < YS; ++s) {
-        if (yown[s]) {
-          double kv = 0.0;
-#pragma unroll
-          for (int e = 0; e < WY; ++e) kv += KE[e * RY + tid + s * B] * X[yi[s][e]];
-          row_kkt(tid + s * B, kv, qq[s], Y[tid + s * B]);
-        }
-      }
+      for (int s = 0; s < YS; ++s)
+        if (yown[s]) row_kkt(tid + s * B, k_xbar(s, KO), qq[s], YK[tid + s * B]);
       // long rows / columns: wave gathers from the workspace CSR (termination checks only)
       for (int L = wid; L < nlx; L += NW) {
         const int j = lxi[L];
         double kt = 0.0;
-        for (int p = gtp[j] + lane; p < gtp[j + 1]; p += kWave) kt += gtv[p] * Y[gtc[p]];
-        kt = wave_sum(kt);
+        for (int p = gtp[j] + lane; p < gtp[j + 1]; p += kWave) kt += gtv[p] * YK[gtc[p]];
+        kt = wave_sum_dpp(kt);
         if (lane == 0) col_kkt(j, kt, lx[2 * kLMax + L], lx[3 * kLMax + L], lx[4 * kLMax + L], lx[5 * kLMax + L]);
       }
       for (int L = wid; L < nly; L += NW) {
         const int i = lyi[L];
         double kv = 0.0;
-        for (int p = gkp[i] + lane; p < gkp[i + 1]; p += kWave) kv += gkv[p] * X[gkc[p]];
-        kv = wave_sum(kv);
+        for (int p = gkp[i] + lane; p < gkp[i + 1]; p += kWave) kv += gkv[p] * XK[gkc[p]];
+        kv = wave_sum_dpp(kv);
         if (lane == 0) row_kkt(i, kv, ly[2 * kLMax + L], ly[3 * kLMax + L]);
       }
     }
-    block_sum1<B, kNRed>(acc, red);
+    // readlane broadcast: the sums (and all decisions below) are uniform.  A restart-only check needs the
+    // four movement norms alone (each wave-wide sum is ~25 VALU ops).
+    if (kkt) {
+      block_sum1<B, kNRed, true>(acc, red);
+    } else {
+      double acc4[4] = {acc[0], acc[1], acc[2], acc[3]};
+      block_sum1<B, 4, true>(acc4, red);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = acc4[t];
+    }
     if (kkt) {
       const double pobj = acc[6] + c0, dobj = acc[7] + acc[8] + c0;
       const double pres = sqrt(acc[4]) / (1.0 + qnorm), dres = sqrt(acc[5]) / (1.0 + cnorm);
@@ -1495,19 +1661,19 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
                          ((double)kin >= o.b_art * (double)it);
     if (restart) {
       const double ddx = sqrt(acc[1]), ddy = sqrt(acc[3]);
-      if (ddx > 1e-10 && ddy > 1e-10) pw = pw_update(ddy / ddx, pw, o.theta);
-      tau = eta / pw;
-      sigma = eta * pw;
+      if (ddx > 1e-10 && ddy > 1e-10) pw = uniform(pw_update(ddy / ddx, pw, o.theta));
+      tau = uniform(eta / pw);
+      sigma = uniform(eta * pw);
       double yns[YS];
 #pragma unroll
       for (int s = 0; s < XS; ++s)
-        if (xown[s]) x[s] = xa[s] = xo_g[opaque(tid + s * B)];
+        if (xown[s]) x[s] = xa[s] = PL ? lds_ld(xst[s] + D) : xo_g[(opaque(tid) + s * B)];
 #pragma unroll
       for (int s = 0; s < YS; ++s) {
         yns[s] = 0.0;
         if (yown[s]) {
-          const int i = opaque(tid + s * B);
-          y[s] = ya[s] = yns[s] = yo_g[i];
+          const int i = (opaque(tid) + s * B);
+          y[s] = ya[s] = yns[s] = PL ? lds_ld(yst[s] + D) : yo_g[i];
           Y[i] = y[s];
         }
       }
@@ -1518,37 +1684,31 @@ __global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w
       }
       // the long columns' K'y partials must now refer to y = y+: rebuild this wave's row
       if (lane < kLMax) myPC[lane] = 0.0;
-      if (ytw >= 0) {
-        double a2 = 0.0;
-#pragma unroll
-        for (int s = 0; s < YS; ++s) a2 += ys_cf[s] * yns[s];
-        a2 = wave_sum_dpp(a2);
-        if (lane == 0) myPC[ytw] = a2;
-      } else if (ytw == -2) {
-#pragma unroll
-        for (int s = 0; s < YS; ++s) wave_scatter(ys_cf[s] * yns[s], ys_tgt[s], myPC);
-      }
+      scatter_cols(yns);
       kin = 0;
+      kbase = 0;
+      hw = hload(0);
       r0 = r;
       rprev = -1.0;
     } else {
       rprev = r;
-      if (kkt) {
+      if (kkt && !PL) {
 #pragma unroll
         for (int s = 0; s < YS; ++s)
           if (yown[s]) Y[tid + s * B] = y[s];
         for (int L = tid; L < nly; L += B) Y[lyi[L]] = ly[L];
       }
     }
-    __syncthreads();
+    lds_barrier();
   }
+  // outputs: the last check's T(z_k), unscaled
 #pragma unroll
   for (int s = 0; s < XS; ++s)
-    if (xown[s]) xo_g[tid + s * B] *= dcv[tid + s * B];
+    if (xown[s]) xo_g[tid + s * B] = (PL ? lds_ld(xst[s] + D) : xo_g[tid + s * B]) * dcv[tid + s * B];
   for (int L = tid; L < nlx; L += B) xo_g[lxi[L]] = lx[5 * kLMax + L] * dcv[lxi[L]];
 #pragma unroll
   for (int s = 0; s < YS; ++s)
-    if (yown[s]) yo_g[tid + s * B] *= drv[tid + s * B];
+    if (yown[s]) yo_g[tid + s * B] = (PL ? lds_ld(yst[s] + D) : yo_g[tid + s * B]) * drv[tid + s * B];
   for (int L = tid; L < nly; L += B) yo_g[lyi[L]] = ly[3 * kLMax + L] * drv[lyi[L]];
   if (tid == 0) {
     b.istats[2 * k] = status;
@@ -1583,30 +1743,46 @@ hipError_t dispatch_xy(int xs, int ys, const Batch& b, const Work& w, const Chun
   return hipErrorInvalidValue;
 }
 
-template <int B, int XS, int YS, int WX, int WY>
+template <int B, int XS, int YS, int WX, int WY, int KR>
 hipError_t launch_ell_one(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n, int max_m,
                           hipStream_t s) {
-  const size_t lds = ell_lds_bytes(max_n, max_m, B, XS, YS, WX, WY);
+  const size_t lds = ell_lds_bytes(max_n, max_m, B, XS, YS, WX, WY, KR);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  auto kern = pdhg_ell_kernel<B, XS, YS, WX, WY>;
+  auto kern = pdhg_ell_kernel<B, XS, YS, WX, WY, KR>;
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3(ch.count), dim3(B), lds, s, b, w, ch, o);
   return hipGetLastError();
 }
 
+// Instantiations, tried in order; the first whose slots cover (n, m) and whose LDS fits is launched.
+// KR variants keep K / K^T in VGPRs: 768-thread workgroups (12 waves, <= 168 VGPRs) cover the monthly
+// battery + DCM window (n <= 2304, m <= 1536) with three waves per SIMD; larger windows keep the values in
+// LDS with 512 threads.
+#ifndef DVH_KR768
+#define DVH_KR768 -1
+#endif
+// K and K^T in VGPRs for the narrow <2,4> slices (the monthly battery + DCM window: measured 1.40 vs 1.59
+// us per window-iteration per CU against K^T in LDS); only K for the <4,8> slices, whose K^T registers
+// would spill.
 template <int WX, int WY>
-hipError_t ell_dispatch_xy(int xs, int ys, const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n,
-                           int max_m, hipStream_t s) {
-  constexpr int B = 512;
-#define DVH_CASE(X_, Y_) \
-  if (xs <= X_ && ys <= Y_) return launch_ell_one<B, X_, Y_, WX, WY>(b, w, ch, o, max_n, max_m, s);
-  DVH_CASE(1, 1)
-  DVH_CASE(2, 2)
-  DVH_CASE(3, 2)
-  DVH_CASE(5, 3)
-  DVH_CASE(6, 4)
-  DVH_CASE(8, 6)
+constexpr int kr768() { return DVH_KR768 >= 0 ? DVH_KR768 : (WX <= 2 && WY <= 4 ? 3 : 2); }
+template <int WX, int WY>
+hipError_t ell_dispatch_xy(int max_n, int max_m, const Batch& b, const Work& w, const Chunk& ch, const Opts& o,
+                           hipStream_t s, int* variant_out) {
+#define DVH_CASE(B_, X_, Y_, KR_)                                                                          \
+  if (max_n <= X_ * B_ && max_m <= Y_ * B_ && ell_lds_bytes(max_n, max_m, B_, X_, Y_, WX, WY, KR_) <= 160 * 1024) { \
+    if (variant_out) *variant_out = (2000000 + 1000000 * KR_) + WX * 100000 + WY * 10000 + (B_ / 64) * 100 + X_ * 10 + Y_; \
+    return launch_ell_one<B_, X_, Y_, WX, WY, KR_>(b, w, ch, o, max_n, max_m, s);                          \
+  }
+  DVH_CASE(512, 1, 1, 3)
+  DVH_CASE(512, 2, 2, 3)
+#ifndef DVH_NO768
+  DVH_CASE(768, 3, 2, (kr768<WX, WY>()))
+#endif
+  DVH_CASE(512, 5, 3, 0)
+  DVH_CASE(512, 6, 4, 0)
+  DVH_CASE(512, 8, 6, 0)
 #undef DVH_CASE
   return hipErrorInvalidValue;
 }
@@ -1651,11 +1827,8 @@ hipError_t launch_pdhg(const Batch& b, const Work& w, const Chunk& ch, const Opt
 
 hipError_t launch_pdhg_ell(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n, int max_m,
                            int wx, int wy, hipStream_t s, int* variant_out) {
-  constexpr int B = 512;
-  const int xs = (max_n + B - 1) / B, ys = (max_m + B - 1) / B;
-  if (variant_out) *variant_out = 2000000 + wx * 10000 + wy * 1000 + xs * 10 + ys;
-  if (wx <= 2 && wy <= 4) return ell_dispatch_xy<2, 4>(xs, ys, b, w, ch, o, max_n, max_m, s);
-  if (wx <= 4 && wy <= 8) return ell_dispatch_xy<4, 8>(xs, ys, b, w, ch, o, max_n, max_m, s);
+  if (wx <= 2 && wy <= 4) return ell_dispatch_xy<2, 4>(max_n, max_m, b, w, ch, o, s, variant_out);
+  if (wx <= 4 && wy <= 8) return ell_dispatch_xy<4, 8>(max_n, max_m, b, w, ch, o, s, variant_out);
   return hipErrorInvalidValue;
 }
 
