@@ -61,8 +61,8 @@ struct dvh_handle {
   std::vector<std::array<hipEvent_t, 3>> chunk_events;
   double timing[3] = {0, 0, 0};
   int last_variant = -1;
-  int n_ell = 0, n_generic = 0, n_large = 0;
-  bool disable_ell = false;
+  int n_ell = 0, n_generic = 0, n_large = 0, n_band = 0;
+  int kernel_path = 0;  // 0 band -> ELL -> generic, 1 generic only, 2 ELL -> generic (no band kernel)
   dvh::LargeSolver* large = nullptr;  // grid-wide path for windows above dvh::kSmallMax (created on first use)
   float large_ms[2] = {0, 0};         // setup, PDHG time of the large windows of the last solve
 };
@@ -192,7 +192,7 @@ int dvh_last_stats(const dvh_handle* h, int32_t* out4) {
   out4[0] = h->n_ell;
   out4[1] = h->n_generic;
   out4[2] = h->last_variant;
-  out4[3] = h->disable_ell ? 1 : 0;
+  out4[3] = h->kernel_path == 1 ? 1 : 0;
   return DVH_OK;
 }
 
@@ -204,9 +204,18 @@ int dvh_last_path_counts(const dvh_handle* h, int32_t* out3) {
   return DVH_OK;
 }
 
-int dvh_set_kernel_path(dvh_handle* h, int generic_only) {
-  if (!h) return DVH_ERR_ARG;
-  h->disable_ell = generic_only != 0;
+int dvh_last_path_counts4(const dvh_handle* h, int32_t* out4) {
+  if (!h || !out4) return DVH_ERR_ARG;
+  out4[0] = h->n_ell;
+  out4[1] = h->n_generic;
+  out4[2] = h->n_large;
+  out4[3] = h->n_band;
+  return DVH_OK;
+}
+
+int dvh_set_kernel_path(dvh_handle* h, int mode) {
+  if (!h || mode < 0 || mode > 2) return DVH_ERR_ARG;
+  h->kernel_path = mode;
   return DVH_OK;
 }
 
@@ -307,7 +316,7 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
               h->w_vbuf.as<double>(), h->w_wbuf.as<double>(), h->w_tmpc.as<double>(), h->w_tmpr.as<double>(),
               h->w_longk.as<int32_t>(), h->w_longt.as<int32_t>(), h->d_hinv.as<double>(), h->w_scal.as<double>()};
   DVH_HIP(h, h->d_list.ensure(I * (size_t)wc));
-  h->n_ell = h->n_generic = h->n_large = 0;
+  h->n_ell = h->n_generic = h->n_large = h->n_band = 0;
   h->large_ms[0] = h->large_ms[1] = 0.0f;
   h->chunk_events.clear();
   DVH_HIP(h, hipEventRecord(h->ev[0], s));
@@ -335,12 +344,46 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
       wx = std::max(wx, (int)sc[9]);
     }
     int variant = -1;
-    // the ELL kernel is specialised to reflection rho = 1 (the default); other values use the generic kernel
-    hipError_t e = (h->disable_ell || o.rho != 1.0) ? hipErrorInvalidValue
-                                  : dvh::launch_pdhg_ell(b, w, c.ch, o, c.mn, c.mm, wx, wy, s, &variant);
+    // Kernel cascade: battery-banded kernel over the chunk -> ELL kernel over the windows it returned (status
+    // -2) -> generic CSR kernel over the windows the ELL kernel returned (status -1).  The fast kernels are
+    // specialised to reflection rho = 1 (the default); other values use the generic kernel.
+    const bool fast = h->kernel_path != 1 && o.rho == 1.0;
+    std::vector<int32_t> ell_list;  // empty + ell_all: the whole chunk
+    bool ell_all = true;
+    if (fast && h->kernel_path == 0) {
+      DVH_HIP(h, dvh::launch_pdhg_band(b, w, c.ch, o, s));
+      ist.resize(2 * (size_t)c.ch.count);
+      DVH_HIP(h, hipMemcpyAsync(ist.data(), bt->istats + 2 * (size_t)c.ch.first, I * ist.size(),
+                                hipMemcpyDeviceToHost, s));
+      DVH_HIP(h, hipStreamSynchronize(s));
+      ell_all = false;
+      int nb = 0;
+      for (int k = 0; k < c.ch.count; ++k) {
+        if (is_large(c.ch.first + k)) continue;
+        if (ist[2 * (size_t)k] == -2)
+          ell_list.push_back(c.ch.first + k);
+        else
+          ++nb;
+      }
+      h->n_band += nb;
+      if (nb > 0) variant = 9000000 + 12;  // band kernel, 768 threads
+    }
+    hipError_t e = hipSuccess;
+    const int n_ell_in = ell_all ? c.ch.count : (int)ell_list.size();
+    if (n_ell_in > 0) {
+      if (!ell_all)
+        DVH_HIP(h, hipMemcpyAsync(h->d_list.p, ell_list.data(), I * ell_list.size(), hipMemcpyHostToDevice, s));
+      int ev = -1;
+      e = !fast ? hipErrorInvalidValue
+                : dvh::launch_pdhg_ell(b, w, c.ch, o, c.mn, c.mm, wx, wy, s, &ev,
+                                       ell_all ? nullptr : h->d_list.as<int32_t>(), (int)ell_list.size());
+      if (e == hipSuccess && variant < 0) variant = ev;
+    }
     std::vector<int32_t> generic;
-    if (e == hipSuccess) {
-      h->n_ell += c.ch.count;
+    if (n_ell_in == 0) {
+      // every window was solved by the band kernel (or is large)
+    } else if (e == hipSuccess) {
+      h->n_ell += n_ell_in;
       ist.resize(2 * (size_t)c.ch.count);
       DVH_HIP(h, hipMemcpyAsync(ist.data(), bt->istats + 2 * (size_t)c.ch.first, I * ist.size(),
                                 hipMemcpyDeviceToHost, s));
@@ -348,16 +391,20 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
       int nl = 0;
       for (int k = 0; k < c.ch.count; ++k) {
         if (is_large(c.ch.first + k)) {
-          ++nl;
+          if (ell_all) ++nl;
           continue;
         }
-        if (ist[2 * (size_t)k] < 0) generic.push_back(c.ch.first + k);
+        if (ist[2 * (size_t)k] == -1) generic.push_back(c.ch.first + k);
       }
       h->n_ell -= (int)generic.size() + nl;
-    } else if (e == hipErrorInvalidValue) {
+    } else if (e == hipErrorInvalidValue) {  // no ELL instantiation covers the chunk's sizes
       (void)hipGetLastError();
-      for (int k = 0; k < c.ch.count; ++k)
-        if (!is_large(c.ch.first + k)) generic.push_back(c.ch.first + k);
+      if (ell_all) {
+        for (int k = 0; k < c.ch.count; ++k)
+          if (!is_large(c.ch.first + k)) generic.push_back(c.ch.first + k);
+      } else {
+        generic = ell_list;
+      }
     } else {
       return hip_fail(h, e, "launch_pdhg_ell");
     }

@@ -1,0 +1,204 @@
+// dvh_device.h -- device helpers shared by the PDHG kernels (dvh_kernels.hip, dvh_band.hip): DPP / permlane
+// wave reductions, workgroup reductions with fixed summation order, LDS-address loads / stores, the
+// primal-weight update and per-window offsets into the packed batch.
+#pragma once
+#include <math.h>
+
+#include "dvh_internal.h"
+
+namespace dvh {
+namespace {
+
+constexpr int kNRed = 9;  // values reduced by a termination (KKT) check
+__host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
+
+constexpr int kOptimal = 0, kIterLimit = 3, kNumerical = 4;
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+
+// Wave-wide f64 sum on the VALU: DPP row rotations (16-lane rows) then the gfx950 permlane16/32 swaps.
+// Every lane ends with the wave total (lanes may differ in the last bit; callers use one lane's value).
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  // row rotations read every lane of the row, so the DPP "old" operand is dead: mov_dpp needs no zeroed copy
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  v += dpp_f64<0x128>(v);  // row_ror:8
+  v += dpp_f64<0x124>(v);  // row_ror:4
+  v += dpp_f64<0x122>(v);  // row_ror:2
+  v += dpp_f64<0x121>(v);  // row_ror:1
+  {
+    const unsigned lo = __double2loint(v), hi = __double2hiint(v);
+    const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    v = __hiloint2double(b[0], a[0]) + __hiloint2double(b[1], a[1]);
+  }
+  {
+    const unsigned lo = __double2loint(v), hi = __double2hiint(v);
+    const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    v = __hiloint2double(b[0], a[0]) + __hiloint2double(b[1], a[1]);
+  }
+  return v;
+}
+
+// Sum over each 16-lane row (every lane of the row gets its row's total; fixed order).
+__device__ __forceinline__ double row_sum16(double v) {
+  v += dpp_f64<0x128>(v);  // row_ror:8
+  v += dpp_f64<0x124>(v);  // row_ror:4
+  v += dpp_f64<0x122>(v);  // row_ror:2
+  v += dpp_f64<0x121>(v);  // row_ror:1
+  return v;
+}
+
+// Primal-weight update w <- exp(theta log(ratio) + (1 - theta) log(w)) (PDLP smoothing).  theta = 1 and
+// theta = 0.5 have closed forms; the general case is a separate (non-inlined) function so that the
+// exp / log polynomial constants are not hoisted into the iteration loop's registers.
+__device__ __noinline__ double pw_update_general(double ratio, double w, double theta) {
+  return exp(theta * log(ratio) + (1.0 - theta) * log(w));
+}
+__device__ __forceinline__ double pw_update(double ratio, double w, double theta) {
+  if (theta == 1.0) return ratio;
+  if (theta == 0.5) return sqrt(ratio * w);
+  return pw_update_general(ratio, w, theta);
+}
+
+// Makes an index opaque to the optimiser so that address arithmetic of cold (check-phase) code is not
+// hoisted out of the iteration loop into long-lived VGPRs.
+__device__ __forceinline__ int opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+__device__ __forceinline__ double opaque(double v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+// Workgroup barrier that orders LDS only.  __syncthreads() is a workgroup release/acquire fence, which also
+// waits for every outstanding global store of the wave to be acknowledged (s_waitcnt vmcnt(0)); in the PDHG
+// loops global memory is only read back by the lane that wrote it, so that wait is pure latency.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Block reduction of NV doubles; red must hold (NW + 1) * NV doubles.  Result identical in all threads.
+template <int B, int NV>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double* red) {
+  constexpr int NW = B / kWave;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = wave_sum(v[k]);
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) red[wid * NV + k] = v[k];
+  }
+  __syncthreads();
+  if (tid < NV) {
+    double s = 0.0;
+    for (int w = 0; w < NW; ++w) s += red[w * NV + tid];
+    red[NW * NV + tid] = s;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = red[NW * NV + k];
+  __syncthreads();
+}
+
+// One-barrier variant: per-wave partials in red[wave*NV + k], one __syncthreads, then every lane adds the
+// NW partials in wave order (identical, deterministic result in all lanes).  The caller must not reuse
+// `red` before another barrier has passed (in the PDHG loop the next use is >= 2 barriers later).
+template <int B, int NV, bool LDSB = false>
+__device__ __forceinline__ void block_sum1(double (&v)[NV], double* red) {
+  static_assert(NV <= kWave, "one lane per reduced value");
+  constexpr int NW = B / kWave;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = wave_sum_dpp(v[k]);
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) red[wid * NV + k] = v[k];
+  }
+  if constexpr (LDSB)
+    lds_barrier();
+  else
+    __syncthreads();
+  // lane k adds value k over the waves (fixed order), then every value is broadcast from its lane
+  double t = 0.0;
+  if (lane < NV) {
+#pragma unroll
+    for (int w = 0; w < NW; ++w) t += red[w * NV + lane];
+  }
+  const int lo = __double2loint(t), hi = __double2hiint(t);
+#pragma unroll
+  for (int k = 0; k < NV; ++k)
+    v[k] = __hiloint2double(__builtin_amdgcn_readlane(hi, k), __builtin_amdgcn_readlane(lo, k));
+}
+
+struct WinOff {
+  int n, m, meq, nnz;
+  int64_t row, nz, on, om;     // global offsets (inputs / outputs)
+  int64_t wn, wm, wz, wtr;     // chunk-relative workspace offsets
+};
+
+__device__ __forceinline__ WinOff win_offsets(const Batch& b, const Chunk& ch, int k) {
+  const int64_t* d = b.desc + 8 * (int64_t)k;
+  WinOff o;
+  o.n = (int)d[0];
+  o.m = (int)d[1];
+  o.meq = (int)d[2];
+  o.nnz = (int)d[3];
+  o.row = d[4];
+  o.nz = d[5];
+  o.on = d[6];
+  o.om = d[7];
+  o.wn = o.on - ch.base_n;
+  o.wm = o.om - ch.base_m;
+  o.wz = o.nz - ch.base_nz;
+  o.wtr = o.wn + (k - ch.first);
+  return o;
+}
+
+// LDS f64 load / store at an absolute LDS byte address (precomputed once in a VGPR, so a gather is a single
+// ds_read_b64 with no address arithmetic in the loop).
+typedef __attribute__((address_space(3))) double lds_f64;
+typedef __attribute__((address_space(3))) unsigned char lds_u8;
+__device__ __forceinline__ int lds_addr(const void* p) {
+  return (int)(size_t)(lds_u8*)(p);
+}
+__device__ __forceinline__ double lds_ld(int a) { return *(lds_f64*)(size_t)(unsigned)a; }
+__device__ __forceinline__ void lds_st(int a, double v) { *(lds_f64*)(size_t)(unsigned)a = v; }
+// Plain v_max_f64 / v_min_f64: the operands are finite or +-inf by construction (no NaN inputs), so the
+// IEEE-mode canonicalisation the compiler would insert before every use of a loop-invariant bound is dead.
+__device__ __forceinline__ double vmax(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double vmin(double a, double b) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double uniform(double v) {
+  return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
+                          __builtin_amdgcn_readfirstlane(__double2loint(v)));
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                          __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+
+}  // namespace
+}  // namespace dvh

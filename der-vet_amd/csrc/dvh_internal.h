@@ -78,10 +78,14 @@ hipError_t launch_setup(const Batch& b, const Work& w, const Chunk& ch, const Op
 // Generic (CSR) kernel; list = optional device list of window ids (nlist blocks) instead of the whole chunk.
 hipError_t launch_pdhg(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n, int max_m,
                        int64_t max_nnz, hipStream_t s, int* variant_out, const int32_t* list, int nlist);
-// ELL fast-path kernel over the whole chunk (wx, wy: ELL widths for K^T and K).  Windows that do not fit
-// its shape come back with istats status -1 (kNeedsGeneric) and must be re-run by launch_pdhg.
+// ELL fast-path kernel over the whole chunk, or over the listed windows (wx, wy: ELL widths for K^T and K).
+// Windows that do not fit its shape come back with istats status -1 (kNeedsGeneric) and must be re-run by
+// launch_pdhg.
 hipError_t launch_pdhg_ell(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n, int max_m,
-                           int wx, int wy, hipStream_t s, int* variant_out);
+                           int wx, int wy, hipStream_t s, int* variant_out, const int32_t* list, int nlist);
+// Battery-banded kernel (dvh_band.hip) over the whole chunk.  Windows whose CSR is not the battery + DCM
+// window shape come back with istats status -2 (kNeedsEll) and must be re-run by launch_pdhg_ell.
+hipError_t launch_pdhg_band(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, hipStream_t s);
 size_t setup_lds_bytes(int max_n);
 // Power iteration for ||Kt||_2 of the listed windows (generic path; the ELL kernel does its own on chip).
 hipError_t launch_power(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, const int32_t* list, int nlist,

@@ -64,6 +64,7 @@ SYMBOLS = {
     "dvh_last_timing": (ctypes.c_int, [ctypes.c_void_p, c_double_p]),
     "dvh_last_stats": (ctypes.c_int, [ctypes.c_void_p, c_int32_p]),
     "dvh_last_path_counts": (ctypes.c_int, [ctypes.c_void_p, c_int32_p]),
+    "dvh_last_path_counts4": (ctypes.c_int, [ctypes.c_void_p, c_int32_p]),
     "dvh_set_kernel_path": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
 }
 

@@ -115,13 +115,18 @@ class BatchSolver:
     def kernel_stats(self):
         v = (ctypes.c_int32 * 4)()
         self._check(self._lib.dvh_last_stats(self._h, v), "dvh_last_stats")
-        c = (ctypes.c_int32 * 3)()
-        self._check(self._lib.dvh_last_path_counts(self._h, c), "dvh_last_path_counts")
-        return {"ell_windows": v[0], "generic_windows": v[1], "variant": v[2], "generic_only": bool(v[3]),
-                "large_windows": c[2]}
+        c = (ctypes.c_int32 * 4)()
+        self._check(self._lib.dvh_last_path_counts4(self._h, c), "dvh_last_path_counts4")
+        return {"band_windows": c[3], "ell_windows": v[0], "generic_windows": v[1], "variant": v[2],
+                "generic_only": bool(v[3]), "large_windows": c[2]}
 
-    def set_kernel_path(self, generic_only):
-        self._check(self._lib.dvh_set_kernel_path(self._h, int(bool(generic_only))), "dvh_set_kernel_path")
+    _PATHS = {"default": 0, "generic": 1, "ell": 2}
+
+    def set_kernel_path(self, path):
+        """Kernel cascade: "default" (battery-banded -> ELL -> generic CSR), "ell" (ELL -> generic) or "generic".
+        A bool selects "generic" (True) / "default" (False)."""
+        mode = (1 if path else 0) if isinstance(path, bool) else self._PATHS[path]
+        self._check(self._lib.dvh_set_kernel_path(self._h, mode), "dvh_set_kernel_path")
 
     def solve(self, lps):
         """Solve a list of WindowLP on the GPU; returns a list of WindowResult (same order)."""

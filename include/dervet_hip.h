@@ -149,8 +149,12 @@ int dvh_last_stats(const dvh_handle* h, int32_t* out4);
 /* Windows per solver path in the most recent solve: out3 = {ELL kernel, generic CSR kernel, grid-wide
  * large-LP path (n or m > 4096: one window at a time over the whole GPU, e.g. BASELINE config 3)}. */
 int dvh_last_path_counts(const dvh_handle* h, int32_t* out3);
-/* 1 = force the generic CSR kernel for every window (testing / A-B timing), 0 = default dispatch. */
-int dvh_set_kernel_path(dvh_handle* h, int generic_only);
+/* The same plus the battery-banded kernel: out4 = {ELL kernel, generic CSR kernel, grid-wide large-LP path,
+ * battery-banded kernel (windows with the storagevet battery + DCM structure, detected on the device)}. */
+int dvh_last_path_counts4(const dvh_handle* h, int32_t* out4);
+/* Kernel cascade (testing / A-B timing): 0 = default (battery-banded -> ELL -> generic CSR), 1 = generic
+ * CSR kernel for every window, 2 = ELL -> generic (no battery-banded kernel). */
+int dvh_set_kernel_path(dvh_handle* h, int mode);
 
 #ifdef __cplusplus
 }

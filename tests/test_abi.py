@@ -18,7 +18,7 @@ HEADER = os.path.join(ROOT, "include", "dervet_hip.h")
 def header_functions():
     txt = open(HEADER).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(dvh_[a-z_]+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(dvh_[a-z_0-9]+)\s*\(", txt)))
 
 
 def test_library_exports_every_declared_symbol():

@@ -57,7 +57,7 @@ def test_config2_36_windows(gpu_solver):
     lps = _lps(scenarios.config2())
     assert len(lps) == 36
     _check(lps, gpu_solver.solve(lps), "config2")
-    assert gpu_solver.kernel_stats()["ell_windows"] == 36
+    assert gpu_solver.kernel_stats()["band_windows"] == 36
 
 
 def test_config4_sample_matches_highs(gpu_solver):
@@ -72,18 +72,28 @@ def test_config5_generic_path(gpu_solver):
     _check(lps, res, "config5")
 
 
-def test_ell_and_generic_kernels_agree():
+def test_band_ell_and_generic_kernels_agree():
+    """The three kernels run the same algorithm on the same scaled LP: objectives within 1e-7, iteration counts
+    within two check periods (summation orders differ)."""
     lps = _lps(scenarios.config4([42]))
+    out = {}
     with BatchSolver(0) as s:
-        a = s.solve(lps)
-        assert s.kernel_stats()["ell_windows"] == 12
-        s.set_kernel_path(True)
-        b = s.solve(lps)
-        assert s.kernel_stats()["generic_windows"] == 12
-    for ra, rb in zip(a, b):
-        assert ra.status == rb.status == 0
-        assert abs(ra.obj - rb.obj) <= 1e-7 * abs(rb.obj)
-        assert abs(ra.iters - rb.iters) <= 32
+        for path, key in (("default", "band_windows"), ("ell", "ell_windows"), ("generic", "generic_windows")):
+            s.set_kernel_path(path)
+            out[path] = s.solve(lps)
+            assert s.kernel_stats()[key] == 12, (path, s.kernel_stats())
+    for ra, rb, rc in zip(out["default"], out["ell"], out["generic"]):
+        assert ra.status == rb.status == rc.status == 0
+        assert abs(ra.obj - rc.obj) <= 1e-7 * abs(rc.obj)
+        assert abs(rb.obj - rc.obj) <= 1e-7 * abs(rc.obj)
+        assert abs(ra.iters - rc.iters) <= 32 and abs(rb.iters - rc.iters) <= 32
+
+
+def test_band_kernel_config1_no_dcm(gpu_solver):
+    """Config 1 (DA arbitrage, no demand charge: J = 0, no >= rows) takes the battery-banded kernel."""
+    lps = _lps(scenarios.config1())
+    _check(lps, gpu_solver.solve(lps), "config1-band")
+    assert gpu_solver.kernel_stats()["band_windows"] == len(lps)
 
 
 def test_packed_device_path_equals_host_path(gpu_solver):
@@ -190,5 +200,5 @@ def test_large_path_with_dcm_columns_in_mixed_batch(gpu_solver):
     assert lps[2].n == 3 * 8760 + 12
     res = gpu_solver.solve(lps)
     ks = gpu_solver.kernel_stats()
-    assert ks["large_windows"] == 1 and ks["ell_windows"] == 3
+    assert ks["large_windows"] == 1 and ks["band_windows"] == 3
     _check(lps, res, "mixed")
