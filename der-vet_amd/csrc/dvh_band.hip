@@ -13,11 +13,12 @@
 // within a row, DCM rows in any order); a window that does not match comes back with status kNeedsEll and
 // is solved by the ELL kernel.
 //
-// Mapping: lane t owns time step t -- its three columns, its SOE row and its DCM row -- with every coefficient,
-// bound, iterate and anchor in VGPRs (<= 80: six waves per SIMD, i.e. two 768-thread windows per CU, so one
-// window's barrier stalls are covered by the other's work).  An SpMV needs only the neighbour step's ene
-// (K x) and SOE-row dual (K^T y): one LDS store + one LDS load per lane and half-step instead of per-entry
-// gathers.  The dense tau columns are summed by wave 0 from per-lane partials (no per-wave reduction).
+// Mapping: lane g owns S consecutive time steps t = S g + s -- their columns ch, dis, ene, their SOE rows and
+// their DCM rows -- with every coefficient, bound, iterate and anchor in VGPRs.  An SpMV needs only the
+// neighbour lane's first ene (K x) and last SOE-row dual (K^T y): one LDS store + one LDS load per lane and
+// half-step instead of per-entry gathers.  The dense tau columns are summed by wave 0 from per-lane partials
+// (no per-wave reduction).  With S = 2, 384 threads cover a 768-step monthly window in <= 168 VGPRs: two
+// windows per CU, so one window's barrier and latency stalls are covered by the other window's work.
 #include <type_traits>
 
 #include "dvh_device.h"
@@ -25,21 +26,26 @@
 namespace dvh {
 namespace {
 
-constexpr int kBandB = 768;   // threads per window (T <= kBandB steps)
+#ifndef DVH_BAND_S
+#define DVH_BAND_S 1
+#endif
+constexpr int kBandS = DVH_BAND_S;    // steps per lane
+constexpr int kBandB = 768 / kBandS;  // threads per window (T <= 768)
 constexpr int kJMax = 4;      // tau (demand-period) columns per window
 constexpr int kNeedsEll = -2;
 
-// LDS layout in doubles (then ints): XE[B+1] YS[B+1] XT[kJMax] TS[6][kJMax] I0[8] red[kNRed(NW+1)+4]
-// TP[kJMax][B] XP[3][B] YP[2][B] | ints: dcm[B] flag[4]
-__host__ __device__ inline size_t band_lds_doubles(int B) {
+// LDS layout in doubles (then ints): XE[B+1] YS[B+1] XT[kJMax] red[kNRed(NW+1)+4]
+// TP[kJMax][B] XP[3S][B] YP[2S][B] | ints: dcm[S B] flag[4]
+__host__ __device__ inline size_t band_lds_doubles(int B, int S) {
   const int NW = B / kWave;
-  return 2 * (size_t)(B + 1) + 7 * kJMax + 8 + (size_t)kNRed * (NW + 1) + 4 + (size_t)kJMax * B + 5 * (size_t)B;
+  return 2 * (size_t)(B + 1) + kJMax + (size_t)kNRed * (NW + 1) + 4 + (size_t)kJMax * B +
+         5 * (size_t)S * B;
 }
-__host__ __device__ inline size_t band_lds_bytes(int B) {
-  return align16(sizeof(double) * band_lds_doubles(B)) + align16(sizeof(int32_t) * ((size_t)B + 4));
+__host__ __device__ inline size_t band_lds_bytes(int B, int S) {
+  return align16(sizeof(double) * band_lds_doubles(B, S)) + align16(sizeof(int32_t) * ((size_t)S * B + 4));
 }
 
-template <int B>
+template <int B, int S>
 __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Work w, const Chunk ch, const Opts o) {
   constexpr int NW = B / kWave;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -56,22 +62,20 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
       b.istats[2 * k + 1] = 0;
     }
   };
-  if (scal[6] != 0.0 || T < 1 || T > B || J < 0 || J > kJMax || MI > T || (J == 0 && MI > 0)) {
+  if (scal[6] != 0.0 || T < 1 || T > S * B || J < 0 || J > kJMax || MI > T || (J == 0 && MI > 0)) {
     bail();
     return;
   }
   // ---- LDS carve
-  double* XE = reinterpret_cast<double*>(smem);  // x-bar (x+) of ene_t at [t]; [T..B] stay 0
-  double* YS = XE + (B + 1);                     // y (y+) of row t at [t]: the init row (t = 0), SOE row of step t-1
+  double* XE = reinterpret_cast<double*>(smem);  // x-bar (x+) of ene at the lane's first step: [g]; [B] = 0
+  double* YS = XE + (B + 1);                     // y (y+) of row S g: the init row (g = 0) / lane g-1's last SOE row
   double* XT = YS + (B + 1);                     // x-bar (x+) of the tau columns
-  double* TS = XT + kJMax;                       // tau state [6][kJMax]: x, xa, c, lo, hi, x+
-  double* I0 = TS + 6 * kJMax;                   // init row: y, ya, y+, q, coefficient
-  double* red = I0 + 8;
+  double* red = XT + kJMax;
   double* TP = red + kNRed * (NW + 1) + 4;       // [kJMax][B] per-lane partial K'y of the tau columns
-  double* XP = TP + kJMax * B;                   // [3][B] T(z) of the lane's columns (check iterations)
-  double* YP = XP + 3 * B;                       // [2][B] T(z) of the lane's rows
-  int32_t* dcm = reinterpret_cast<int32_t*>(smem + align16(sizeof(double) * band_lds_doubles(B)));  // [B]
-  int32_t* flag = dcm + B;
+  double* XP = TP + kJMax * B;                   // [3S][B] T(z) of the lane's columns (check iterations)
+  double* YP = XP + 3 * S * B;                   // [2S][B] T(z) of the lane's rows
+  int32_t* dcm = reinterpret_cast<int32_t*>(smem + align16(sizeof(double) * band_lds_doubles(B, S)));  // [S B]
+  int32_t* flag = dcm + S * B;
 
   const int32_t* gkp = b.indptr + W.row;
   const int32_t* gkc = b.indices + W.nz;
@@ -86,7 +90,7 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
   double* yo_g = b.y + W.om;
 
   // ---- structure check (every entry of every row accounted for) and the step -> DCM row map
-  for (int t = tid; t < B; t += B) dcm[t] = -1;
+  for (int t = tid; t < S * B; t += B) dcm[t] = -1;
   if (tid == 0) flag[0] = 0;
   __syncthreads();
   int bad = 0;
@@ -146,110 +150,142 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
     return;
   }
 
-  // ---- the lane's step t: columns ch, dis, ene (v = 0, 1, 2), SOE row t+1, DCM row -- all in VGPRs
-  const int t = tid;
-  const bool val = t < T;
-  double x[3], xa[3], hi[3];
-  double cch = 0.0, cdi = 0.0, loe = 0.0;  // objective of ch / dis, lower bound of ene
-  double ks[4] = {0.0, 0.0, 0.0, 0.0};     // SOE row: coefficients of ch_t, dis_t, ene_t, ene_{t+1}
-  double kd[3] = {0.0, 0.0, 0.0};          // DCM row: coefficients of ch_t, dis_t, tau_j
-  double kp = 0.0;                         // coefficient of ene_t in row t (init row or SOE row of step t-1)
-  double ys = 0.0, yas = 0.0, qsr = 0.0, yd = 0.0, yad = 0.0, qd = 0.0;
-  int drow = -1, jt = 0;
+  // ---- the lane's steps t = S tid + s: columns ch, dis, ene (v = 0, 1, 2), SOE row t+1, DCM row -- in VGPRs
+  double x[S][3], xa[S][3], hi[S][3];
+  double cch[S], cdi[S], loe[S];  // objective of ch / dis, lower bound of ene
+  double ks[S][4];                // SOE row: coefficients of ch_t, dis_t, ene_t, ene_{t+1}
+  double kd[S][3];                // DCM row: coefficients of ch_t, dis_t, tau_j
+  double ys[S], yas[S], qsr[S], yd[S], yad[S], qd[S];
+  int drow[S], xta[S];            // DCM row index (-1: none), LDS address of XT[its tau]
+  int jt[S];
+  bool val[S];
+  double kp = 0.0;                // coefficient of ene_{S tid} in row S tid (init row or lane tid-1's last SOE row)
 #pragma unroll
-  for (int v = 0; v < 3; ++v) x[v] = xa[v] = hi[v] = 0.0;
-  if (val) {
+  for (int s = 0; s < S; ++s) {
+    const int t = S * tid + s;
+    val[s] = t < T;
+    drow[s] = -1;
+    jt[s] = 0;
+    cch[s] = cdi[s] = loe[s] = 0.0;
+    ys[s] = yas[s] = qsr[s] = yd[s] = yad[s] = qd[s] = 0.0;
 #pragma unroll
-    for (int v = 0; v < 3; ++v) {
-      hi[v] = us[v * T + t];
-      x[v] = xa[v] = fmin(fmax(0.0, ls[v * T + t]), hi[v]);
-    }
-    cch = cs[t];
-    cdi = cs[T + t];
-    loe = ls[2 * T + t];
-    for (int p = gkp[t + 1]; p < gkp[t + 2]; ++p) {
-      const int c = gkc[p];
-      const double a = gkv[p];
-      if (c == t) ks[0] = a;
-      else if (c == T + t) ks[1] = a;
-      else if (c == 2 * T + t) ks[2] = a;
-      else ks[3] = a;
-    }
-    for (int p = gkp[t]; p < gkp[t + 1]; ++p)
-      if (gkc[p] == 2 * T + t) kp = gkv[p];
-    qsr = qs[t + 1];
-    const int dv = dcm[t];
-    if (dv >= 0) {
-      drow = dv >> 3;
-      jt = dv & 7;
-      for (int p = gkp[drow]; p < gkp[drow + 1]; ++p) {
+    for (int v = 0; v < 3; ++v) x[s][v] = xa[s][v] = hi[s][v] = kd[s][v] = 0.0;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) ks[s][v] = 0.0;
+    if (val[s]) {
+#pragma unroll
+      for (int v = 0; v < 3; ++v) {
+        hi[s][v] = us[v * T + t];
+        x[s][v] = xa[s][v] = fmin(fmax(0.0, ls[v * T + t]), hi[s][v]);
+      }
+      cch[s] = cs[t];
+      cdi[s] = cs[T + t];
+      loe[s] = ls[2 * T + t];
+      for (int p = gkp[t + 1]; p < gkp[t + 2]; ++p) {
         const int c = gkc[p];
         const double a = gkv[p];
-        if (c < T) kd[0] = a;
-        else if (c < 2 * T) kd[1] = a;
-        else kd[2] = a;
+        if (c == t) ks[s][0] = a;
+        else if (c == T + t) ks[s][1] = a;
+        else if (c == 2 * T + t) ks[s][2] = a;
+        else ks[s][3] = a;
       }
-      qd = qs[drow];
+      if (s == 0)
+        for (int p = gkp[t]; p < gkp[t + 1]; ++p)
+          if (gkc[p] == 2 * T + t) kp = gkv[p];
+      qsr[s] = qs[t + 1];
+      const int dv = dcm[t];
+      if (dv >= 0) {
+        drow[s] = dv >> 3;
+        jt[s] = dv & 7;
+        for (int p = gkp[drow[s]]; p < gkp[drow[s] + 1]; ++p) {
+          const int c = gkc[p];
+          const double a = gkv[p];
+          if (c < T) kd[s][0] = a;
+          else if (c < 2 * T) kd[s][1] = a;
+          else kd[s][2] = a;
+        }
+        qd[s] = qs[drow[s]];
+      }
     }
+    xta[s] = lds_addr(XT + jt[s]);
   }
-  const int xta = lds_addr(XT + jt);
-  if (tid < kJMax) {  // tau columns
-    const bool tv = tid < J;
-    const double l0 = tv ? ls[3 * T + tid] : 0.0, h0 = tv ? us[3 * T + tid] : 0.0, x0 = fmin(fmax(0.0, l0), h0);
-    TS[tid] = TS[kJMax + tid] = TS[5 * kJMax + tid] = x0;
-    TS[2 * kJMax + tid] = tv ? cs[3 * T + tid] : 0.0;
-    TS[3 * kJMax + tid] = l0;
-    TS[4 * kJMax + tid] = h0;
-    XT[tid] = 0.0;
+  // Special state in wave 0 (registers sp[], meaning by lane): lane j < J holds tau column j {x, xa, c, lo, hi, x+};
+  // lane kInitLane holds the init row (row 0: ene_0 = target) {y, ya, y+, q, coefficient, -}.
+  constexpr int kInitLane = kWave - 1;
+  static_assert(kJMax < kInitLane, "tau lanes and the init-row lane are distinct");
+  const bool tlane = wid == 0 && lane < J, ilane = wid == 0 && lane == kInitLane;
+  double sp[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  if (tlane) {
+    const double l0 = ls[3 * T + lane], h0 = us[3 * T + lane];
+    sp[0] = sp[1] = sp[5] = fmin(fmax(0.0, l0), h0);
+    sp[2] = cs[3 * T + lane];
+    sp[3] = l0;
+    sp[4] = h0;
   }
-  if (tid == 0) {  // init row
-    I0[0] = I0[1] = I0[2] = 0.0;
-    I0[3] = qs[0];
-    I0[4] = gkv[gkp[0]];
-    XE[B] = YS[B] = 0.0;
+  if (ilane) {
+    sp[3] = qs[0];
+    sp[4] = gkv[gkp[0]];
   }
+  if (tid < kJMax) XT[tid] = 0.0;
+  if (tid == 0) XE[B] = YS[B] = 0.0;
   XE[tid] = YS[tid] = 0.0;
   for (int u = tid; u < kJMax * B; u += B) TP[u] = 0.0;
 #pragma unroll
-  for (int v = 0; v < 3; ++v) XP[v * B + tid] = x[v];
-  YP[tid] = YP[B + tid] = 0.0;
+  for (int s = 0; s < S; ++s) {
+#pragma unroll
+    for (int v = 0; v < 3; ++v) XP[(3 * s + v) * B + tid] = x[s][v];
+    YP[(2 * s) * B + tid] = YP[(2 * s + 1) * B + tid] = 0.0;
+  }
   __syncthreads();
 
   // ---- SpMV pieces (fixed summation order)
-  // K^T of the lane's columns from its rows' values (vs: SOE row, vd: DCM row) and vprev = value of row t
-  auto ktr = [&](double vs, double vd, double vprev, double (&out)[3]) {
-    out[0] = fma(kd[0], vd, ks[0] * vs);
-    out[1] = fma(kd[1], vd, ks[1] * vs);
-    out[2] = fma(ks[2], vs, kp * vprev);
+  // K^T of the lane's columns from its rows' values (vs: SOE rows, vd: DCM rows) and vprev = value of row S tid
+  auto ktr = [&](const double (&vs)[S], const double (&vd)[S], double vprev, double (&out)[S][3]) {
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      out[s][0] = fma(kd[s][0], vd[s], ks[s][0] * vs[s]);
+      out[s][1] = fma(kd[s][1], vd[s], ks[s][1] * vs[s]);
+      out[s][2] = fma(ks[s][2], vs[s], s == 0 ? kp * vprev : ks[s > 0 ? s - 1 : 0][3] * vs[s > 0 ? s - 1 : 0]);
+    }
   };
-  // K of the lane's rows, own-column part (the neighbour's ene and the tau term are added by kfin)
-  auto kown = [&](const double (&v)[3], double& os, double& od) {
-    os = fma(ks[2], v[2], fma(ks[1], v[1], ks[0] * v[0]));
-    od = fma(kd[1], v[1], kd[0] * v[0]);
+  // K of the lane's rows, own-column part (kfin adds the next lane's ene and the tau terms)
+  auto kown = [&](const double (&v)[S][3], double (&os)[S], double (&od)[S]) {
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      os[s] = fma(ks[s][2], v[s][2], fma(ks[s][1], v[s][1], ks[s][0] * v[s][0]));
+      if (s + 1 < S) os[s] = fma(ks[s][3], v[s + 1 < S ? s + 1 : s][2], os[s]);
+      od[s] = fma(kd[s][1], v[s][1], kd[s][0] * v[s][0]);
+    }
   };
-  auto kfin = [&](double& os, double& od, double vnext) {
-    os = fma(ks[3], vnext, os);
-    od = fma(kd[2], lds_ld(xta), od);
+  auto kfin = [&](double (&os)[S], double (&od)[S], double vnext) {
+    os[S - 1] = fma(ks[S - 1][3], vnext, os[S - 1]);
+#pragma unroll
+    for (int s = 0; s < S; ++s) od[s] = fma(kd[s][2], lds_ld(xta[s]), od[s]);
   };
-  // per-lane partial K'y of the tau columns from the DCM row's value
-  auto tau_parts = [&](double vd) {
+  // per-lane partial K'y of the tau columns from the DCM rows' values
+  auto tau_parts = [&](const double (&vd)[S]) {
     if (J == 1) {
-      TP[tid] = kd[2] * vd;
+      double a = kd[0][2] * vd[0];
+#pragma unroll
+      for (int s = 1; s < S; ++s) a = fma(kd[s][2], vd[s], a);
+      TP[tid] = a;
     } else {
-      for (int j = 0; j < J; ++j) TP[j * B + tid] = (jt == j ? kd[2] : 0.0) * vd;
+      for (int j = 0; j < J; ++j) {
+        double a = 0.0;
+#pragma unroll
+        for (int s = 0; s < S; ++s) a = fma(jt[s] == j ? kd[s][2] : 0.0, vd[s], a);
+        TP[j * B + tid] = a;
+      }
     }
   };
   // wave 0: lane j < J gets the sum over all lanes of TP[j][.] (fixed order; uniform per column)
   auto tau_kt = [&]() {
     double res = 0.0;
     for (int j = 0; j < J; ++j) {
-      double a0 = 0.0, a1 = 0.0;
+      double a = 0.0;
 #pragma unroll
-      for (int r = 0; r < NW; r += 2) {
-        a0 += TP[j * B + r * kWave + lane];
-        if (r + 1 < NW) a1 += TP[j * B + (r + 1) * kWave + lane];
-      }
-      const double a = uniform(wave_sum_dpp(a0 + a1));
+      for (int r = 0; r < NW; ++r) a += TP[j * B + r * kWave + lane];
+      a = uniform(wave_sum_dpp(a));
       if (lane == j) res = a;
     }
     return res;
@@ -260,12 +296,16 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
   if (o.power_iters > 0) {
     const int P = o.power_iters;
     const double v0 = 1.0 / sqrt((double)n);
-    double vc[3];
+    double vc[S][3];
 #pragma unroll
-    for (int v = 0; v < 3; ++v) vc[v] = val ? v0 : 0.0;
+    for (int s = 0; s < S; ++s)
+#pragma unroll
+      for (int v = 0; v < 3; ++v) vc[s][v] = val[s] ? v0 : 0.0;
     double vtau = (wid == 0 && lane < J) ? v0 : 0.0;
     double nv[2] = {0.0, 0.0};
-    double ws = 0.0, wd = 0.0;
+    double ws[S], wd[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) ws[s] = wd[s] = 0.0;
     for (int pi = 0; pi <= P; ++pi) {
       if (pi > 0) {
         ktr(ws, wd, YS[tid], vc);
@@ -274,15 +314,22 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
           vtau = lane < J ? kt : 0.0;
         }
       }
-      if (pi >= P - 1) nv[pi - (P - 1)] = fma(vtau, vtau, fma(vc[2], vc[2], fma(vc[1], vc[1], vc[0] * vc[0])));
+      if (pi >= P - 1) {
+        double a = vtau * vtau;
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+#pragma unroll
+          for (int v = 0; v < 3; ++v) a = fma(vc[s][v], vc[s][v], a);
+        nv[pi - (P - 1)] = a;
+      }
       if (pi == P) break;
-      XE[tid] = vc[2];
+      XE[tid] = vc[0][2];
       if (wid == 0 && lane < J) XT[lane] = vtau;
       __syncthreads();
       kown(vc, ws, wd);
       kfin(ws, wd, XE[tid + 1]);
-      YS[tid + 1] = ws;
-      if (tid == 0) YS[0] = I0[4] * vc[2];
+      YS[tid + 1] = ws[S - 1];
+      if (ilane) YS[0] = sp[4] * XE[0];
       tau_parts(wd);
       __syncthreads();
     }
@@ -312,9 +359,29 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
   };
   double hw = hload(0);
 
+  // wave 0 with one tau column: the tau reduction is interleaved with its own column work (straight-line code,
+  // the partial loads are issued first); J >= 2 takes the generic per-column loop
+  const bool w0 = wid == 0 && J == 1;
   double mv0, mv1, mv2, mv3;
-  auto iterate = [&](auto chk_tag) __attribute__((always_inline)) {
+  auto tau_update = [&](double kt, double ca, double cb, auto chk_tag) __attribute__((always_inline)) {
     constexpr bool CHECK = decltype(chk_tag)::value;
+    if (tlane) {
+      const double xo = sp[0], xan = sp[1];
+      const double p1 = vmin(vmax(fma(-tau, sp[2] - kt, xo), sp[3]), sp[4]);
+      const double xbt = fma(2.0, p1, -xo);
+      XT[lane] = xbt;
+      sp[0] = fma(ca, xbt, cb * xan);
+      if (CHECK) {
+        const double d = xo - p1, da = p1 - xan;
+        mv0 += d * d;
+        mv1 += da * da;
+        sp[5] = p1;
+      }
+    }
+  };
+  auto iterate = [&](auto chk_tag, auto w0_tag) __attribute__((always_inline)) {
+    constexpr bool CHECK = decltype(chk_tag)::value;
+    constexpr bool W0 = decltype(w0_tag)::value;
     if (kin - kbase >= kWave) {
       kbase = kin;
       hw = hload(kin);
@@ -322,73 +389,77 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
     const double cb = readlane_f64(hw, kin - kbase), ca = 1.0 - cb;
     mv0 = mv1 = mv2 = mv3 = 0.0;
     // ---------------- primal half-step (reflected Halpern, rho = 1)
-    double kxs, kxd;  // own-column part of K x-bar for the dual half-step
+    double kxs[S], kxd[S];  // own-column part of K x-bar for the dual half-step
     {
-      double kty[3], xb[3];
-      ktr(ys, yd, YS[tid], kty);
-      const double cv[3] = {cch, cdi, 0.0};
-      const double lv[3] = {0.0, 0.0, loe};
+      double ta0 = 0.0, ta1 = 0.0;
+      if constexpr (W0) {
 #pragma unroll
-      for (int v = 0; v < 3; ++v) {  // branch-free: padding steps have c = lo = hi = 0 and stay at 0
-        const double p1 = vmin(vmax(fma(-tau, cv[v] - kty[v], x[v]), lv[v]), hi[v]);
-        xb[v] = fma(2.0, p1, -x[v]);
-        if (CHECK) {
-          const double d = x[v] - p1, da = p1 - xa[v];
-          mv0 += d * d;
-          mv1 += da * da;
-          XP[v * B + tid] = p1;
+        for (int r = 0; r < NW; r += 2) {
+          ta0 += TP[r * kWave + lane];
+          if (r + 1 < NW) ta1 += TP[(r + 1) * kWave + lane];
         }
-        x[v] = fma(ca, xb[v], cb * xa[v]);
       }
-      XE[tid] = xb[2];
-      kown(xb, kxs, kxd);
-      if (wid == 0 && J > 0) {  // tau columns: K'y summed from the DCM rows' per-lane partials
-        const double kt = tau_kt();
-        if (lane < J) {
-          const double xo = TS[lane], xan = TS[kJMax + lane];
-          const double p1 = vmin(vmax(fma(-tau, TS[2 * kJMax + lane] - kt, xo), TS[3 * kJMax + lane]),
-                                 TS[4 * kJMax + lane]);
-          const double xbt = fma(2.0, p1, -xo);
-          XT[lane] = xbt;
-          TS[lane] = fma(ca, xbt, cb * xan);
+      double kty[S][3], xb[S][3];
+      ktr(ys, yd, YS[tid], kty);
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const double cv[3] = {cch[s], cdi[s], 0.0};
+        const double lv[3] = {0.0, 0.0, loe[s]};
+#pragma unroll
+        for (int v = 0; v < 3; ++v) {  // branch-free: padding steps have c = lo = hi = 0 and stay at 0
+          const double p1 = vmin(vmax(fma(-tau, cv[v] - kty[s][v], x[s][v]), lv[v]), hi[s][v]);
+          xb[s][v] = fma(2.0, p1, -x[s][v]);
           if (CHECK) {
-            const double d = xo - p1, da = p1 - xan;
+            const double d = x[s][v] - p1, da = p1 - xa[s][v];
             mv0 += d * d;
             mv1 += da * da;
-            TS[5 * kJMax + lane] = p1;
+            XP[(3 * s + v) * B + tid] = p1;
           }
+          x[s][v] = fma(ca, xb[s][v], cb * xa[s][v]);
         }
+      }
+      XE[tid] = xb[0][2];
+      kown(xb, kxs, kxd);
+      if constexpr (W0) {
+        tau_update(uniform(wave_sum_dpp(ta0 + ta1)), ca, cb, chk_tag);
+      } else {
+        if (wid == 0 && J > 1) tau_update(tau_kt(), ca, cb, chk_tag);
       }
     }
     lds_barrier();
     // ---------------- dual half-step
     {
       kfin(kxs, kxd, XE[tid + 1]);
-      const double p1 = fma(sigma, qsr - kxs, ys);               // SOE row: equality
-      const double p2 = vmax(fma(sigma, qd - kxd, yd), 0.0);    // DCM row: >=, its dual stays >= 0
-      if (CHECK) {
-        const double d = ys - p1, da = p1 - yas, e = yd - p2, ea = p2 - yad;
-        mv2 += d * d + e * e;
-        mv3 += da * da + ea * ea;
-        YP[tid] = p1;
-        YP[B + tid] = p2;
-      }
-      ys = fma(ca, fma(2.0, p1, -ys), cb * yas);
-      yd = fma(ca, fma(2.0, p2, -yd), cb * yad);
-      YS[tid + 1] = ys;
-      if (J > 0) tau_parts(yd);
-      if (tid == 0) {  // init row: ene_0 = target
-        const double y0 = I0[0], ya0 = I0[1];
-        const double q1 = fma(sigma, I0[3] - I0[4] * XE[0], y0);
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const double p1 = fma(sigma, qsr[s] - kxs[s], ys[s]);             // SOE row: equality
+        const double p2 = vmax(fma(sigma, qd[s] - kxd[s], yd[s]), 0.0);  // DCM row: >=, its dual stays >= 0
         if (CHECK) {
-          const double d = y0 - q1, da = q1 - ya0;
-          mv2 += d * d;
-          mv3 += da * da;
-          I0[2] = q1;
+          const double d = ys[s] - p1, da = p1 - yas[s], e = yd[s] - p2, ea = p2 - yad[s];
+          mv2 += d * d + e * e;
+          mv3 += da * da + ea * ea;
+          YP[(2 * s) * B + tid] = p1;
+          YP[(2 * s + 1) * B + tid] = p2;
         }
-        const double yn = fma(ca, fma(2.0, q1, -y0), cb * ya0);
-        I0[0] = yn;
-        YS[0] = yn;
+        ys[s] = fma(ca, fma(2.0, p1, -ys[s]), cb * yas[s]);
+        yd[s] = fma(ca, fma(2.0, p2, -yd[s]), cb * yad[s]);
+      }
+      YS[tid + 1] = ys[S - 1];
+      if (J > 0) tau_parts(yd);
+      if (W0 || wid == 0) {  // init row (lane kInitLane): ene_0 = target
+        if (ilane) {
+          const double y0 = sp[0], ya0 = sp[1];
+          const double q1 = fma(sigma, sp[3] - sp[4] * XE[0], y0);
+          if (CHECK) {
+            const double d = y0 - q1, da = q1 - ya0;
+            mv2 += d * d;
+            mv3 += da * da;
+            sp[2] = q1;
+          }
+          const double yn = fma(ca, fma(2.0, q1, -y0), cb * ya0);
+          sp[0] = yn;
+          YS[0] = yn;
+        }
       }
     }
     ++it;
@@ -400,11 +471,17 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
   using Tt = std::integral_constant<bool, true>;
   while (it < o.max_iters) {
     if (--ck != 0) {
-      iterate(F());
+      if (w0)
+        iterate(F(), Tt());
+      else
+        iterate(F(), F());
       continue;
     }
     ck = chk;
-    iterate(Tt());
+    if (w0)
+      iterate(Tt(), Tt());
+    else
+      iterate(Tt(), F());
     // ---------------- check: fixed-point residual of z_k, restart test; every kkt_every-th check the relative
     // KKT error of T(z_k) in the unscaled space (as pdhg_ell_kernel)
     const bool kkt = (--kk_ == 0) || (it + chk > o.max_iters);
@@ -418,14 +495,18 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
     for (int u = 4; u < kNRed; ++u) acc[u] = 0.0;
     if (kkt) {
       // images of T(z_k) in XE / XT / YS / TP (rewritten from z after the check)
-      double xp[3];
+      double xp[S][3], yps[S], ypd[S];
 #pragma unroll
-      for (int v = 0; v < 3; ++v) xp[v] = XP[v * B + tid];
-      const double yps = YP[tid], ypd = YP[B + tid];
-      XE[tid] = xp[2];
-      YS[tid + 1] = yps;
-      if (tid == 0) YS[0] = I0[2];
-      if (wid == 0 && lane < J) XT[lane] = TS[5 * kJMax + lane];
+      for (int s = 0; s < S; ++s) {
+#pragma unroll
+        for (int v = 0; v < 3; ++v) xp[s][v] = XP[(3 * s + v) * B + tid];
+        yps[s] = YP[(2 * s) * B + tid];
+        ypd[s] = YP[(2 * s + 1) * B + tid];
+      }
+      XE[tid] = xp[0][2];
+      YS[tid + 1] = yps[S - 1];
+      if (ilane) YS[0] = sp[2];
+      if (tlane) XT[lane] = sp[5];
       if (J > 0) tau_parts(ypd);
       lds_barrier();
       auto col_kkt = [&](int j, double kt, double cj, double loj, double hij, double xj) {
@@ -446,25 +527,29 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
         acc[4] += r * r;
         acc[7] += qi * yi;
       };
-      double kt[3];
+      double kt[S][3];
       ktr(yps, ypd, YS[tid], kt);
-      if (val) {
-        col_kkt(t, kt[0], cch, 0.0, hi[0], xp[0]);
-        col_kkt(T + t, kt[1], cdi, 0.0, hi[1], xp[1]);
-        col_kkt(2 * T + t, kt[2], 0.0, loe, hi[2], xp[2]);
-      }
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+        if (val[s]) {
+          const int t = S * tid + s;
+          col_kkt(t, kt[s][0], cch[s], 0.0, hi[s][0], xp[s][0]);
+          col_kkt(T + t, kt[s][1], cdi[s], 0.0, hi[s][1], xp[s][1]);
+          col_kkt(2 * T + t, kt[s][2], 0.0, loe[s], hi[s][2], xp[s][2]);
+        }
       if (wid == 0 && J > 0) {
         const double ktt = tau_kt();
-        if (lane < J)
-          col_kkt(3 * T + lane, ktt, TS[2 * kJMax + lane], TS[3 * kJMax + lane], TS[4 * kJMax + lane],
-                  TS[5 * kJMax + lane]);
+        if (tlane) col_kkt(3 * T + lane, ktt, sp[2], sp[3], sp[4], sp[5]);
       }
-      double kxs, kxd;
+      double kxs[S], kxd[S];
       kown(xp, kxs, kxd);
       kfin(kxs, kxd, XE[tid + 1]);
-      if (val) row_kkt(t + 1, kxs, qsr, yps, false);
-      if (drow >= 0) row_kkt(drow, kxd, qd, ypd, true);
-      if (tid == 0) row_kkt(0, I0[4] * xp[2], I0[3], I0[2], false);
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        if (val[s]) row_kkt(S * tid + s + 1, kxs[s], qsr[s], yps[s], false);
+        if (drow[s] >= 0) row_kkt(drow[s], kxd[s], qd[s], ypd[s], true);
+      }
+      if (ilane) row_kkt(0, sp[4] * XE[0], sp[3], sp[2], false);
     }
     if (kkt) {
       block_sum1<B, kNRed, true>(acc, red);
@@ -503,11 +588,14 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
       tau = uniform(eta / pw);
       sigma = uniform(eta * pw);
 #pragma unroll
-      for (int v = 0; v < 3; ++v) x[v] = xa[v] = XP[v * B + tid];
-      ys = yas = YP[tid];
-      yd = yad = YP[B + tid];
-      if (tid == 0) I0[0] = I0[1] = I0[2];
-      if (wid == 0 && lane < J) TS[lane] = TS[kJMax + lane] = TS[5 * kJMax + lane];
+      for (int s = 0; s < S; ++s) {
+#pragma unroll
+        for (int v = 0; v < 3; ++v) x[s][v] = xa[s][v] = XP[(3 * s + v) * B + tid];
+        ys[s] = yas[s] = YP[(2 * s) * B + tid];
+        yd[s] = yad[s] = YP[(2 * s + 1) * B + tid];
+      }
+      if (ilane) sp[0] = sp[1] = sp[2];
+      if (tlane) sp[0] = sp[1] = sp[5];
       kin = 0;
       kbase = 0;
       hw = hload(0);
@@ -517,22 +605,25 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
       rprev = r;
     }
     if (restart || kkt) {  // the y images must hold z again (after a restart z = T(z_k))
-      YS[tid + 1] = ys;
-      if (tid == 0) YS[0] = I0[0];
+      YS[tid + 1] = ys[S - 1];
+      if (ilane) YS[0] = sp[0];
       if (J > 0) tau_parts(yd);
     }
     lds_barrier();
   }
   // outputs: the last check's T(z_k), unscaled
-  if (val) {
 #pragma unroll
-    for (int v = 0; v < 3; ++v) xo_g[v * T + t] = XP[v * B + tid] * dcv[v * T + t];
-    yo_g[t + 1] = YP[tid] * drv[t + 1];
-    if (drow >= 0) yo_g[drow] = YP[B + tid] * drv[drow];
-  }
-  if (tid < J) xo_g[3 * T + tid] = TS[5 * kJMax + tid] * dcv[3 * T + tid];
+  for (int s = 0; s < S; ++s)
+    if (val[s]) {
+      const int t = S * tid + s;
+#pragma unroll
+      for (int v = 0; v < 3; ++v) xo_g[v * T + t] = XP[(3 * s + v) * B + tid] * dcv[v * T + t];
+      yo_g[t + 1] = YP[(2 * s) * B + tid] * drv[t + 1];
+      if (drow[s] >= 0) yo_g[drow[s]] = YP[(2 * s + 1) * B + tid] * drv[drow[s]];
+    }
+  if (tlane) xo_g[3 * T + lane] = sp[5] * dcv[3 * T + lane];
+  if (ilane) yo_g[0] = sp[2] * drv[0];
   if (tid == 0) {
-    yo_g[0] = I0[2] * drv[0];
     b.istats[2 * k] = status;
     b.istats[2 * k + 1] = it;
     for (int u = 0; u < 4; ++u) b.stats[4 * k + u] = fin[u];
@@ -542,9 +633,9 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
 }  // namespace
 
 hipError_t launch_pdhg_band(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, hipStream_t s) {
-  constexpr int B = kBandB;
-  const size_t lds = band_lds_bytes(B);
-  auto kern = pdhg_band_kernel<B>;
+  constexpr int B = kBandB, S = kBandS;
+  const size_t lds = band_lds_bytes(B, S);
+  auto kern = pdhg_band_kernel<B, S>;
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3(ch.count), dim3(B), lds, s, b, w, ch, o);
