@@ -91,7 +91,7 @@ void dvh_default_options(dvh_options* o) {
   std::memset(o, 0, sizeof(*o));
   o->eps = 1e-6;
   o->max_iters = 100000;
-  o->check_every = 16;
+  o->check_every = 32;
   o->kkt_every = 4;
   o->ruiz_iters = 10;
   o->power_iters = 64;

@@ -54,7 +54,7 @@ extern "C" {
 typedef struct dvh_options {
   double eps;                 /* relative KKT tolerance (primal, dual, gap), default 1e-6          */
   int32_t max_iters;          /* per window, default 100000                                       */
-  int32_t check_every;        /* restart-check period (iterations), default 16                    */
+  int32_t check_every;        /* restart-check period (iterations), default 32                    */
   int32_t ruiz_iters;         /* Ruiz equilibration passes, default 10                            */
   int32_t power_iters;        /* power-iteration steps for ||K||_2, default 64                    */
   double step_safety;         /* eta = step_safety / ||K||_2, default 0.998                       */

@@ -27,7 +27,7 @@ import numpy as np
 OPTIMAL, PRIMAL_INFEASIBLE, DUAL_INFEASIBLE, ITER_LIMIT, NUMERICAL = 0, 1, 2, 3, 4
 
 # defaults mirror dvh_default_options (der-vet_amd/csrc/dvh_api.cpp)
-DEFAULTS = dict(eps=1e-6, max_iters=100000, check_every=16, kkt_every=4, ruiz_iters=10, power_iters=64,
+DEFAULTS = dict(eps=1e-6, max_iters=100000, check_every=32, kkt_every=4, ruiz_iters=10, power_iters=64,
                 step_safety=0.998, rho=1.0, b_suff=0.2, b_nec=0.8, b_art=0.1, theta=1.0)
 
 

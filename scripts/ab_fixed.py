@@ -10,7 +10,7 @@ import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-DEFAULT_SETS = {"plain": dict(check_every=1000000, kkt_every=1), "default": dict(check_every=16, kkt_every=4)}
+DEFAULT_SETS = {"plain": dict(check_every=1000000, kkt_every=1), "default": dict(check_every=32, kkt_every=4)}
 CHILD = r'''
 import sys, os, json
 sys.path.insert(0, os.path.join(%r, "..", "der-vet_amd"))

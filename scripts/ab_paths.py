@@ -24,12 +24,12 @@ def main():
     objs = {}
     for path in ("default", "ell"):
         s.set_kernel_path(path)
-        for label, kw in (("plain", dict(check_every=1000000, kkt_every=1)), ("checks", dict(check_every=16, kkt_every=4))):
+        for label, kw in (("plain", dict(check_every=1000000, kkt_every=1)), ("checks", dict(check_every=32, kkt_every=4))):
             s.set_options(eps=1e-30, max_iters=fixed, **kw)
             best = min((s.solve_packed(dev), torch.cuda.synchronize(), s.timing()["pdhg_ms"])[2] for _ in range(3))
             print(f"{path:8s} fixed {fixed} {label:6s}: {best * 1e3 / units / fixed:.3f} us/iter/CU  {s.kernel_stats()}",
                   flush=True)
-        s.set_options(eps=1e-6, max_iters=100000, check_every=16, kkt_every=4)
+        s.set_options(eps=1e-6, max_iters=100000, check_every=32, kkt_every=4)
         best = None
         for _ in range(2):
             s.solve_packed(dev)

@@ -5,7 +5,8 @@ Usage: python scripts/pmc_traffic.py <fetch_dir> <write_dir> <windows_per_launch
 FETCH_SIZE / WRITE_SIZE are in KB (rocprofv3 derived counters).  Per MI355X_MICROARCH.md section HBM: on
 gfx950 FETCH_SIZE reports half of the bytes of wide coalesced reads, so it is doubled; WRITE_SIZE is taken
 as is.  Both include Infinity-Cache hits (memory-side L2 requests), so they are an upper bound on HBM bytes.
-The dominant kernel is the ELL PDHG kernel (pdhg_ell_kernel<...>); values are averaged over its dispatches.
+The dominant kernel is the PDHG kernel (pdhg_band_kernel<...> for battery-banded windows, else
+pdhg_ell_kernel<...>); values are averaged over its dispatches.
 """
 import csv
 import glob
@@ -40,15 +41,15 @@ def main():
                                                               "pdhg_traffic.json")
     fetch = read_counter(fdir, "FETCH_SIZE")
     write = read_counter(wdir, "WRITE_SIZE")
-    kern = [k for k in fetch if "pdhg_ell_kernel" in k]
+    kern = [k for k in fetch if "pdhg_band_kernel" in k] or [k for k in fetch if "pdhg_ell_kernel" in k]
     if not kern:
-        raise SystemExit(f"pdhg_ell_kernel not in {list(fetch)}")
+        raise SystemExit(f"no PDHG kernel in {list(fetch)}")
     fv = [v for k in kern for v in fetch[k]]
     wv = [v for k in kern for v in write.get(k, [])]
     f_kb = sum(fv) / len(fv)
     w_kb = sum(wv) / len(wv) if wv else 0.0
     res = {
-        "kernel": re.search(r"pdhg_ell_kernel<[^>]*>", kern[0]).group(0),
+        "kernel": re.search(r"pdhg_(band|ell)_kernel<[^>]*>", kern[0]).group(0),
         "windows": windows,
         "dispatches_fetch": len(fv), "dispatches_write": len(wv),
         "fetch_size_kb_raw": f_kb, "write_size_kb": w_kb,
