@@ -243,6 +243,7 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
   o.kkt_every = h->opts.kkt_every;
   o.ruiz_iters = h->opts.ruiz_iters;
   o.power_iters = h->opts.power_iters;
+  o.warm = h->opts.warm_start != 0;
   o.small_max = dvh::kSmallMax;
   dvh::Batch b{bt->desc, bt->indptr, bt->indices, bt->data, bt->c, bt->c0, bt->q, bt->l, bt->u,
                bt->x, bt->y, bt->stats, bt->istats};
@@ -579,6 +580,18 @@ extern "C" int dvh_solve_batch(dvh_handle* h, const dvh_lp* lps, int32_t count, 
   DVH_HIP(h, hipMemcpyAsync(h->d_u.p, u.data(), D * tn, hipMemcpyHostToDevice, s));
   if (tm) DVH_HIP(h, hipMemcpyAsync(h->d_q.p, q.data(), D * tm, hipMemcpyHostToDevice, s));
   DVH_HIP(h, hipMemcpyAsync(h->d_c0.p, c0.data(), D * count, hipMemcpyHostToDevice, s));
+  std::vector<double> x0, y0;
+  if (h->opts.warm_start) {  // starting points: the caller's x / y buffers (zero where absent)
+    x0.assign(tn, 0.0);
+    y0.assign(std::max<int64_t>(tm, 1), 0.0);
+    for (int k = 0; k < count; ++k) {
+      const int64_t* d = &desc[8 * (size_t)k];
+      if (out[k].x) std::memcpy(&x0[d[6]], out[k].x, D * d[0]);
+      if (out[k].y && d[1]) std::memcpy(&y0[d[7]], out[k].y, D * d[1]);
+    }
+    DVH_HIP(h, hipMemcpyAsync(h->d_x.p, x0.data(), D * tn, hipMemcpyHostToDevice, s));
+    DVH_HIP(h, hipMemcpyAsync(h->d_y.p, y0.data(), D * y0.size(), hipMemcpyHostToDevice, s));
+  }
   dvh_packed bt{};
   bt.count = count;
   bt.total_n = tn;

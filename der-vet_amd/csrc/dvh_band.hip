@@ -193,6 +193,14 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
         for (int p = gkp[t]; p < gkp[t + 1]; ++p)
           if (gkc[p] == 2 * T + t) kp = gkv[p];
       qsr[s] = qs[t + 1];
+      if (o.warm) {  // warm start from the unscaled x / y in the output buffers
+#pragma unroll
+        for (int v = 0; v < 3; ++v) {
+          const int j = v * T + t;
+          x[s][v] = xa[s][v] = fmin(fmax(xo_g[j] / dcv[j], ls[j]), hi[s][v]);
+        }
+        ys[s] = yas[s] = yo_g[t + 1] / drv[t + 1];
+      }
       const int dv = dcm[t];
       if (dv >= 0) {
         drow[s] = dv >> 3;
@@ -205,6 +213,7 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
           else kd[s][2] = a;
         }
         qd[s] = qs[drow[s]];
+        if (o.warm) yd[s] = yad[s] = fmax(yo_g[drow[s]] / drv[drow[s]], 0.0);
       }
     }
     xta[s] = lds_addr(XT + jt[s]);
@@ -226,6 +235,10 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
     sp[3] = qs[0];
     sp[4] = gkv[gkp[0]];
   }
+  if (o.warm) {
+    if (tlane) sp[0] = sp[1] = sp[5] = fmin(fmax(xo_g[3 * T + lane] / dcv[3 * T + lane], sp[3]), sp[4]);
+    if (ilane) sp[0] = sp[1] = sp[2] = yo_g[0] / drv[0];
+  }
   if (tid < kJMax) XT[tid] = 0.0;
   if (tid == 0) XE[B] = YS[B] = 0.0;
   XE[tid] = YS[tid] = 0.0;
@@ -234,7 +247,8 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
   for (int s = 0; s < S; ++s) {
 #pragma unroll
     for (int v = 0; v < 3; ++v) XP[(3 * s + v) * B + tid] = x[s][v];
-    YP[(2 * s) * B + tid] = YP[(2 * s + 1) * B + tid] = 0.0;
+    YP[(2 * s) * B + tid] = ys[s];
+    YP[(2 * s + 1) * B + tid] = yd[s];
   }
   __syncthreads();
 
@@ -338,6 +352,12 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
     YS[tid] = 0.0;
     if (tid == 0) YS[B] = 0.0;
     for (int u = tid; u < kJMax * B; u += B) TP[u] = 0.0;
+    __syncthreads();
+  }
+  if (o.warm) {  // y images of the starting point
+    YS[tid + 1] = ys[S - 1];
+    if (ilane) YS[0] = sp[0];
+    if (J > 0) tau_parts(yd);
     __syncthreads();
   }
   eta = uniform(eta);

@@ -20,6 +20,7 @@ struct Opts {
   int max_iters, check_every, kkt_every, ruiz_iters, power_iters;
   int setup_segments;  // set by launch_setup
   int small_max;       // setup skips (scal[6] = 2) windows with n or m above this
+  int warm;            // start from the (unscaled) x / y in the output buffers (band kernel; others cold)
 };
 
 // Inputs of one chunk of the packed batch (device pointers, global offsets from desc).

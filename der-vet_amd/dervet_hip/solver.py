@@ -128,8 +128,11 @@ class BatchSolver:
         mode = (1 if path else 0) if isinstance(path, bool) else self._PATHS[path]
         self._check(self._lib.dvh_set_kernel_path(self._h, mode), "dvh_set_kernel_path")
 
-    def solve(self, lps):
-        """Solve a list of WindowLP on the GPU; returns a list of WindowResult (same order)."""
+    def solve(self, lps, start=None):
+        """Solve a list of WindowLP on the GPU; returns a list of WindowResult (same order).
+
+        start: optional list of (x, y) starting points (unscaled; None entries start cold), used when the
+        solver's ``warm_start`` option is set (battery-banded windows)."""
         count = len(lps)
         if count == 0:
             return []
@@ -158,8 +161,11 @@ class BatchSolver:
             L.u = ptr(lp.u, np.float64, _lib.c_double_p)
             L.c0 = lp.c0
             L.structure = lp.structure
-            x = np.empty(lp.n)
-            y = np.empty(m)
+            x = np.zeros(lp.n)
+            y = np.zeros(m)
+            if start is not None and start[k] is not None:
+                x[:] = start[k][0]
+                y[:] = start[k][1]
             outs.append((x, y))
             res[k].x = x.ctypes.data_as(_lib.c_double_p)
             res[k].y = y.ctypes.data_as(_lib.c_double_p) if m else None

@@ -65,7 +65,9 @@ typedef struct dvh_options {
   double primal_weight_theta; /* default 1.0  */
   int32_t verbose;            /* 0 silent                                                           */
   int32_t kkt_every;          /* termination (KKT) check every kkt_every restart checks, default 4 */
-  int32_t reserved[6];
+  int32_t warm_start;         /* 1: start each window from the x / y already in the output buffers     */
+                              /*    (unscaled, e.g. a similar window's solution); 0: x = proj(0), y = 0 */
+  int32_t reserved[5];
 } dvh_options;
 
 typedef struct dvh_lp {

@@ -202,3 +202,21 @@ def test_large_path_with_dcm_columns_in_mixed_batch(gpu_solver):
     ks = gpu_solver.kernel_stats()
     assert ks["large_windows"] == 1 and ks["band_windows"] == 3
     _check(lps, res, "mixed")
+
+
+def test_warm_start_from_own_solution_and_neighbour():
+    """warm_start: windows started at their own solution need far fewer iterations than cold starts (the
+    relative KKT test sits at 1e-6, so a few restart periods are still needed) and end at the HiGHS optimum;
+    started from another scenario's solution of the same month they still converge to the HiGHS optimum
+    (battery-banded kernel)."""
+    lps = _lps(scenarios.config4([11, 12]))
+    with BatchSolver(0) as s:
+        cold = s.solve(lps)
+        s.set_options(warm_start=1)
+        own = s.solve(lps, start=[(r.x, r.y) for r in cold])
+        assert s.kernel_stats()["band_windows"] == len(lps)
+        nb = s.solve(lps, start=[(cold[k ^ 1].x, cold[k ^ 1].y) for k in range(len(lps))])  # other scenario
+    assert all(r.status == 0 for r in own)
+    assert sum(r.iters for r in own) < 0.6 * sum(r.iters for r in cold), ([r.iters for r in own], [r.iters for r in cold])
+    _check(lps, own, "config4-warm-own")
+    _check(lps, nb, "config4-warm-neighbour")
