@@ -57,6 +57,8 @@ struct dvh_handle {
   DevBuf w_tptr, w_tind, w_tval, w_kval, w_rowof, w_perm, w_dr, w_dc, w_cs, w_ls, w_us, w_qs, w_vbuf, w_wbuf,
       w_tmpc, w_tmpr, w_longk, w_longt, w_scal;
   DevBuf d_list, d_hinv;
+  DevBuf o_data, o_cases, o_len, o_hist;  // reliability sweep
+  double outage_ms = 0.0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<std::array<hipEvent_t, 3>> chunk_events;
   double timing[3] = {0, 0, 0};
@@ -169,7 +171,8 @@ int dvh_destroy(dvh_handle* h) {
   DevBuf* bufs[] = {&h->d_desc, &h->d_indptr, &h->d_indices, &h->d_data, &h->d_c, &h->d_c0, &h->d_q, &h->d_l,
                     &h->d_u, &h->d_list, &h->d_hinv, &h->d_x, &h->d_y, &h->d_stats, &h->d_istats, &h->w_tptr, &h->w_tind, &h->w_tval,
                     &h->w_kval, &h->w_rowof, &h->w_perm, &h->w_dr, &h->w_dc, &h->w_cs, &h->w_ls, &h->w_us,
-                    &h->w_qs, &h->w_vbuf, &h->w_wbuf, &h->w_tmpc, &h->w_tmpr, &h->w_longk, &h->w_longt, &h->w_scal};
+                    &h->w_qs, &h->w_vbuf, &h->w_wbuf, &h->w_tmpc, &h->w_tmpr, &h->w_longk, &h->w_longt, &h->w_scal,
+                    &h->o_data, &h->o_cases, &h->o_len, &h->o_hist};
   for (DevBuf* b : bufs) b->release();
   for (auto& e : h->ev)
     if (e) hipEventDestroy(e);
@@ -216,6 +219,117 @@ int dvh_last_path_counts4(const dvh_handle* h, int32_t* out4) {
 int dvh_set_kernel_path(dvh_handle* h, int mode) {
   if (!h || mode < 0 || mode > 2) return DVH_ERR_ARG;
   h->kernel_path = mode;
+  return DVH_OK;
+}
+
+int dvh_outage_coverage(dvh_handle* h, const dvh_outage_case* cases, int32_t count, int32_t* lengths,
+                        double* lcp) {
+  if (!h) return DVH_ERR_ARG;
+  if (count < 0 || (count > 0 && (!cases || !lcp))) return fail(h, DVH_ERR_ARG, "cases and lcp are required");
+  if (count == 0) return DVH_OK;
+  hipSetDevice(h->device);
+  // validate, size the packed inputs
+  size_t nd = 0, nlen = 0, nhist = 0;
+  int max_n = 0, max_bins = 0;
+  std::vector<int> olen(count);
+  for (int k = 0; k < count; ++k) {
+    const dvh_outage_case& c = cases[k];
+    const std::string w = "outage case " + std::to_string(k) + ": ";
+    if (c.n_steps < 1 || !c.critical_load) return fail(h, DVH_ERR_ARG, w + "n_steps >= 1 and critical_load required");
+    if (!(c.dt > 0.0) || c.max_outage < 1 || c.max_outage / c.dt < 1.0)
+      return fail(h, DVH_ERR_ARG, w + "dt > 0 and max_outage >= dt required");
+    if (!(c.rte > 0.0)) return fail(h, DVH_ERR_ARG, w + "rte must be > 0");
+    olen[k] = (int)(c.max_outage / c.dt);  // int(self.max_outage_duration / self.dt), Reliability.py:917
+    if (olen[k] + 1 > 16384) return fail(h, DVH_ERR_UNSUPPORTED, w + "more than 16384 outage steps");
+    nd += (size_t)c.n_steps * (1 + (c.pv_max ? 1 : 0) + (c.pv_vari ? 1 : 0) + (c.init_soe ? 1 : 0)) +
+          (c.load_shed_pct ? (size_t)c.max_outage : 0);
+    nlen += (size_t)c.n_steps;
+    nhist += (size_t)olen[k] + 1;
+    max_n = std::max(max_n, c.n_steps);
+    max_bins = std::max(max_bins, olen[k] + 1);
+  }
+  std::vector<double> data(std::max<size_t>(nd, 1));
+  std::vector<dvh::OutageCase> dc(count);
+  DVH_HIP(h, h->o_data.ensure(sizeof(double) * data.size()));
+  DVH_HIP(h, h->o_cases.ensure(sizeof(dvh::OutageCase) * count));
+  DVH_HIP(h, h->o_len.ensure(sizeof(int32_t) * nlen));
+  DVH_HIP(h, h->o_hist.ensure(sizeof(int32_t) * nhist));
+  const double* dbase = h->o_data.as<double>();
+  size_t off = 0, lo = 0, ho = 0;
+  auto put = [&](const double* src, size_t n) -> const double* {
+    if (!src) return nullptr;
+    std::memcpy(&data[off], src, sizeof(double) * n);
+    const double* d = dbase + off;
+    off += n;
+    return d;
+  };
+  for (int k = 0; k < count; ++k) {
+    const dvh_outage_case& c = cases[k];
+    dvh::OutageCase& o = dc[k];
+    o.n_steps = c.n_steps;
+    o.max_steps = c.max_outage;
+    o.outage_len = olen[k];
+    o.pad = 0;
+    o.len_off = (int64_t)lo;
+    o.hist_off = (int64_t)ho;
+    o.dt = c.dt;
+    o.soe0 = c.soe0;
+    o.dg_gen = c.dg_gen;
+    o.gamma = c.gamma;
+    o.soe_min = c.soe_min;
+    o.soe_max = c.soe_max;
+    o.charge_max = c.charge_max;
+    o.discharge_max = c.discharge_max;
+    o.rte = c.rte;
+    o.critical_load = put(c.critical_load, c.n_steps);
+    o.pv_max = put(c.pv_max, c.n_steps);
+    o.pv_vari = put(c.pv_vari, c.n_steps);
+    o.init_soe = put(c.init_soe, c.n_steps);
+    o.load_shed = put(c.load_shed_pct, c.max_outage);
+    lo += c.n_steps;
+    ho += olen[k] + 1;
+  }
+  hipStream_t s = h->stream;
+  DVH_HIP(h, hipMemcpyAsync(h->o_data.p, data.data(), sizeof(double) * data.size(), hipMemcpyHostToDevice, s));
+  DVH_HIP(h, hipMemcpyAsync(h->o_cases.p, dc.data(), sizeof(dvh::OutageCase) * count, hipMemcpyHostToDevice, s));
+  DVH_HIP(h, hipMemsetAsync(h->o_hist.p, 0, sizeof(int32_t) * nhist, s));
+  DVH_HIP(h, hipEventRecord(h->ev[0], s));
+  hipError_t e = dvh::launch_outage(h->o_cases.as<dvh::OutageCase>(), count, max_n, max_bins,
+                                    lengths ? h->o_len.as<int32_t>() : nullptr, h->o_hist.as<int32_t>(), s);
+  if (e != hipSuccess) return hip_fail(h, e, "launch_outage");
+  DVH_HIP(h, hipEventRecord(h->ev[3], s));
+  std::vector<int32_t> hist(nhist);
+  DVH_HIP(h, hipMemcpyAsync(hist.data(), h->o_hist.p, sizeof(int32_t) * nhist, hipMemcpyDeviceToHost, s));
+  if (lengths) DVH_HIP(h, hipMemcpyAsync(lengths, h->o_len.p, sizeof(int32_t) * nlen, hipMemcpyDeviceToHost, s));
+  DVH_HIP(h, hipStreamSynchronize(s));
+  float ms = 0.0f;
+  if (hipEventElapsedTime(&ms, h->ev[0], h->ev[3]) == hipSuccess) h->outage_ms = ms;
+  // the curve, in the reference's float64 arithmetic (Reliability.py:947-957)
+  size_t po = 0;
+  ho = 0;
+  for (int k = 0; k < count; ++k) {
+    const dvh_outage_case& c = cases[k];
+    double length = c.dt;
+    int j = 0;
+    while (length <= (double)c.max_outage && j < olen[k]) {
+      const int first = (int)(length / c.dt);
+      double covered = 0.0;
+      for (int b = first; b <= olen[k]; ++b) covered += (double)hist[ho + b];
+      const double total = (double)c.n_steps - (length / c.dt) + 1.0;
+      lcp[po + j] = covered / total;
+      ++j;
+      length += c.dt;
+    }
+    for (; j < olen[k]; ++j) lcp[po + j] = NAN;
+    po += olen[k];
+    ho += olen[k] + 1;
+  }
+  return DVH_OK;
+}
+
+int dvh_last_outage_ms(const dvh_handle* h, double* ms) {
+  if (!h || !ms) return DVH_ERR_ARG;
+  *ms = h->outage_ms;
   return DVH_OK;
 }
 

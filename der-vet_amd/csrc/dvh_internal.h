@@ -92,6 +92,17 @@ size_t setup_lds_bytes(int max_n);
 hipError_t launch_power(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, const int32_t* list, int nlist,
                         hipStream_t s);
 
+// Post-facto reliability sweep (dvh_outage.hip): one case of dvh_outage_case with device pointers.
+struct OutageCase {
+  int n_steps, max_steps, outage_len, pad;
+  int64_t len_off, hist_off;  // offsets into the lengths / histogram outputs
+  double dt, soe0, dg_gen, gamma, soe_min, soe_max, charge_max, discharge_max, rte;
+  const double *critical_load, *pv_max, *pv_vari, *init_soe, *load_shed;
+};
+// One thread per (case, start step); hist must be zeroed (sum of outage_len + 1 bins); lengths may be null.
+hipError_t launch_outage(const OutageCase* d_cases, int ncase, int max_steps_n, int max_bins, int32_t* d_lengths,
+                         int32_t* d_hist, hipStream_t s);
+
 // Grid-wide PDHG for one window too large for the workgroup-per-window kernels (dvh_large.hip).
 struct LargeSolver;
 LargeSolver* large_create();

@@ -51,6 +51,15 @@ class Packed(ctypes.Structure):
                 ("stats", ctypes.c_void_p), ("istats", ctypes.c_void_p)]
 
 
+class OutageCase(ctypes.Structure):
+    _fields_ = [("n_steps", ctypes.c_int32), ("max_outage", ctypes.c_int32), ("dt", ctypes.c_double),
+                ("critical_load", c_double_p), ("pv_max", c_double_p), ("pv_vari", c_double_p),
+                ("init_soe", c_double_p), ("load_shed_pct", c_double_p), ("soe0", ctypes.c_double),
+                ("dg_gen", ctypes.c_double), ("gamma", ctypes.c_double), ("soe_min", ctypes.c_double),
+                ("soe_max", ctypes.c_double), ("charge_max", ctypes.c_double), ("discharge_max", ctypes.c_double),
+                ("rte", ctypes.c_double)]
+
+
 # symbol -> (restype, argtypes); every symbol declared in include/dervet_hip.h
 SYMBOLS = {
     "dvh_version": (ctypes.c_char_p, []),
@@ -67,6 +76,9 @@ SYMBOLS = {
     "dvh_last_path_counts": (ctypes.c_int, [ctypes.c_void_p, c_int32_p]),
     "dvh_last_path_counts4": (ctypes.c_int, [ctypes.c_void_p, c_int32_p]),
     "dvh_set_kernel_path": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "dvh_outage_coverage": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(OutageCase), ctypes.c_int32, c_int32_p,
+                                           c_double_p]),
+    "dvh_last_outage_ms": (ctypes.c_int, [ctypes.c_void_p, c_double_p]),
 }
 
 _lib = None

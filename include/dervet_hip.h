@@ -154,6 +154,38 @@ int dvh_last_path_counts(const dvh_handle* h, int32_t* out3);
 /* The same plus the battery-banded kernel: out4 = {ELL kernel, generic CSR kernel, grid-wide large-LP path,
  * battery-banded kernel (windows with the storagevet battery + DCM structure, detected on the device)}. */
 int dvh_last_path_counts4(const dvh_handle* h, int32_t* out4);
+/* ---- Post-facto reliability sweep.
+ * Replaces Reliability.load_coverage_probability (dervet/MicrogridValueStreams/Reliability.py:876-967) and the
+ * serial recursion it drives (data_process :447-487, simulate_outage :489-570): for every case, an outage is
+ * simulated from EVERY start step (one GPU thread each) and the covered lengths give the load coverage
+ * probability curve P(outage of L hours covered), L = dt, 2 dt, .., max_outage.  The DER aggregates are the
+ * caller's (Reliability.get_der_mix_properties :276-332): pv_vari = sum of pv_max x nu, gamma = largest gamma,
+ * dg_gen = total ICE power (minus the largest unit for N-2), ESS limits = llsoc / ulsoc x energy rating. */
+typedef struct dvh_outage_case {
+  int32_t n_steps;                /* len(critical load)                                              */
+  int32_t max_outage;             /* max_outage_duration (hours; also the data window in steps, :462) */
+  double dt;                      /* hours per step                                                  */
+  const double* critical_load;    /* [n_steps] kW                                                    */
+  const double* pv_max;           /* [n_steps] total PV maximum generation, or NULL (no PV)          */
+  const double* pv_vari;          /* [n_steps] total PV generation x nu, or NULL (no PV)             */
+  const double* init_soe;         /* [n_steps] ESS energy at each outage start, or NULL: soe0        */
+  const double* load_shed_pct;    /* [max_outage] % of the critical load kept per outage hour, or NULL */
+  double soe0;                    /* energy at every start when init_soe == NULL (soc_init x rating) */
+  double dg_gen;                  /* total generator power, kW (constant)                            */
+  double gamma;                   /* largest PV gamma (fraction)                                     */
+  double soe_min, soe_max;        /* ESS operation energy limits, kWh                                */
+  double charge_max, discharge_max; /* kW                                                            */
+  double rte;                     /* round-trip efficiency (fraction)                                */
+} dvh_outage_case;
+
+/* lengths: caller-allocated [sum n_steps] covered steps per start (case-major), or NULL;
+ * lcp: caller-allocated [sum int(max_outage / dt)] load coverage probability per outage length.
+ * Bit-exact with the reference's numpy arithmetic.  Blocks until done. */
+int dvh_outage_coverage(dvh_handle* h, const dvh_outage_case* cases, int32_t count, int32_t* lengths,
+                        double* lcp);
+/* Kernel time of the last dvh_outage_coverage call (HIP events, milliseconds). */
+int dvh_last_outage_ms(const dvh_handle* h, double* ms);
+
 /* Kernel cascade (testing / A-B timing): 0 = default (battery-banded -> ELL -> generic CSR), 1 = generic
  * CSR kernel for every window, 2 = ELL -> generic (no battery-banded kernel). */
 int dvh_set_kernel_path(dvh_handle* h, int mode);

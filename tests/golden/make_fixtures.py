@@ -147,6 +147,53 @@ def make_bench_data():
     print("wrote bench data")
 
 
+# Post-facto reliability (dervet/MicrogridValueStreams/Reliability.py:876-967 load_coverage_probability):
+# name: (results dir, result suffix, model params csv, load-shed csv or None)
+REL_CASES = {
+    "uc2_es": ("test_validation_report_sept1/Results/Usecase2/es/step2", "uc3_es_step2",
+               "test_validation_report_sept1/" + CASES["es"][3], None),
+    "uc2_es+pv+dg": ("test_validation_report_sept1/Results/Usecase2/es+pv+dg/step2", "uc3_es+pv+dg_step2",
+                     "test_validation_report_sept1/" + CASES["es+pv+dg"][3], None),
+    "uc2_es+pv": ("test_validation_report_sept1/Results/Usecase2/es+pv/step2", "uc3_es+pv_step2",
+                  "test_validation_report_sept1/" + CASES["es+pv"][3], None),
+    "ls_w_ls1": ("test_load_shedding/results/reliability_load_shed1", "_2mw_5hr",
+                 "test_load_shedding/mp/Model_Parameters_Template_DER_w_ls1.csv",
+                 "test_load_shedding/load_shed_percentage.csv"),
+    "ls_wo_ls1": ("test_load_shedding/results/reliability_load_shed_wo_ls1", "_2mw_5hr",
+                  "test_load_shedding/mp/Model_Parameters_Template_DER_wo_ls1.csv", None),
+}
+
+
+def make_reliability_cases():
+    """Inputs and golden load-coverage-probability curves of the post-facto reliability runs."""
+    arrays, meta = {}, {}
+    for name, (resdir, suf, mp, lsf) in REL_CASES.items():
+        base = os.path.join(REF, "test", resdir)
+        _, ts = read_csv_cols(os.path.join(base, f"timeseries_results{suf}.csv"))
+        _, lcp = read_csv_cols(os.path.join(base, f"load_coverage_prob{suf}.csv"))
+        params = read_params(os.path.join(REF, "test", mp))
+        arrays[f"{name}__critical_load"] = fcol(ts, "Critical Load (kW)")
+        if "Aggregated State of Energy (kWh)" in ts:
+            arrays[f"{name}__aggregated_soe"] = fcol(ts, "Aggregated State of Energy (kWh)")
+        if "Aggregate Energy Min (kWh)" in ts:
+            arrays[f"{name}__aggregate_energy_min"] = fcol(ts, "Aggregate Energy Min (kWh)")
+        pvcols = [k for k in ts if k.startswith("PV: ") and k.endswith("Maximum (kW)")]
+        if pvcols:
+            arrays[f"{name}__pv_max"] = np.sum([fcol(ts, k) for k in pvcols], axis=0)
+        arrays[f"{name}__golden_lcp"] = fcol(lcp, "Load Coverage Probability (%)")
+        arrays[f"{name}__golden_length"] = fcol(lcp, "Outage Length (hrs)")
+        if lsf:
+            _, ls = read_csv_cols(os.path.join(REF, "test", lsf))
+            arrays[f"{name}__load_shed_pct"] = fcol(ls, "Load Shed (%)")
+        meta[name] = {"source_results": os.path.join("test", resdir), "active_tags": sorted(params.keys()),
+                      "params": {t: params[t] for t in ("Scenario", "Battery", "PV", "ICE", "Reliability") if t in params}}
+    np.savez_compressed(os.path.join(HERE, "reliability_cases.npz"), **arrays)
+    with open(os.path.join(HERE, "reliability_cases.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+    print("wrote reliability cases", sorted(meta))
+
+
 if __name__ == "__main__":
     make_golden_cases()
     make_bench_data()
+    make_reliability_cases()

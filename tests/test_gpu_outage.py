@@ -1,0 +1,74 @@
+"""GPU reliability sweep (dvh_outage_coverage) vs the oracle and the reference's golden curves: covered
+lengths bit-exact per start step, load coverage probability curves bit-exact."""
+import numpy as np
+import pytest
+
+import outage_cases
+from dervet_hip import reliability
+
+pytestmark = pytest.mark.gpu
+
+
+def _case(c):
+    return reliability.OutageCase(critical_load=c["critical_load"], dt=c["dt"],
+                                  max_outage_duration=c["max_outage_duration"], ess=c["ess"], init_soe=c["init_soe"],
+                                  soc_init=c["soc_init"], pv_max=c["pv_max"], pv_nu=c["pv_nu"],
+                                  pv_gamma=c["pv_gamma"], load_shed_pct=c["load_shed_pct"])
+
+
+def test_golden_cases_bit_exact(gpu_solver):
+    cases = outage_cases.load()
+    names = sorted(cases)
+    lengths, curves = reliability.outage_coverage([_case(cases[n]) for n in names], gpu_solver)
+    for n, L, lcp in zip(names, lengths, curves):
+        Lo, _ = outage_cases.oracle_curve(cases[n])
+        np.testing.assert_array_equal(L, Lo, err_msg=n)
+        np.testing.assert_array_equal(lcp, cases[n]["golden_lcp"], err_msg=n)
+    dfs = reliability.load_coverage_probability([_case(cases["uc2_es"])], gpu_solver)
+    assert list(dfs[0].columns) == ["Load Coverage Probability (%)"] and dfs[0].index.name == "Outage Length (hrs)"
+    assert len(dfs[0]) == 80 and dfs[0].index[0] == 1.0
+
+
+def _random_case(rng, N, dt=1.0, max_out=24, pv=True, dg=True, shed=True, soe_series=True):
+    cl = rng.uniform(200.0, 1500.0, N).round(5)
+    E = float(rng.uniform(500, 6000))
+    ess = dict(E=E, P_ch=E / rng.uniform(2, 6), P_dis=E / rng.uniform(2, 6), rte=float(rng.uniform(0.8, 0.95)),
+               llsoc=float(rng.uniform(0, 0.2)), ulsoc=float(rng.uniform(0.85, 1.0)))
+    pvs = [np.maximum(0.0, rng.normal(600, 400, N))] if pv else []
+    return reliability.OutageCase(
+        critical_load=cl, dt=dt, max_outage_duration=max_out, ess=ess,
+        init_soe=rng.uniform(0, E, N) if soe_series else None, soc_init=float(rng.uniform(0.3, 1.0)),
+        pv_max=pvs, pv_nu=[float(rng.uniform(0.2, 1.0))] if pv else [], pv_gamma=[float(rng.uniform(0.3, 1.0))] if pv else [],
+        dg_power=[float(rng.uniform(0, 600))] if dg else [],
+        load_shed_pct=rng.choice([100.0, 80.0, 50.0, 30.0], size=max_out) if shed else None)
+
+
+def _oracle(c):
+    from oracle import outage
+    dg, pmax, props, pvar, gamma = reliability.der_mix_properties(c)
+    gen = np.repeat(dg, len(c.critical_load))
+    soe = c.init_soe if c.init_soe is not None else c.soc_init * props["energy rating"]
+    L = outage.coverage_lengths(np.asarray(c.critical_load), gen, pmax, pvar, gamma, props, soe,
+                                c.max_outage_duration, c.dt, c.load_shed_pct)
+    return L, outage.lcp_curve(L, c.max_outage_duration, c.dt)
+
+
+def test_randomised_cases_bit_exact(gpu_solver):
+    """PV (nu, gamma), generators, load-shed multipliers, llsoc / ulsoc limits, SOE series or soc_init, short
+    series (N < max outage), dt = 0.5 -- every covered length equals the oracle's."""
+    rng = np.random.default_rng(20250217)
+    cases = [_random_case(rng, 700), _random_case(rng, 700, pv=False), _random_case(rng, 700, dg=False, shed=False),
+             _random_case(rng, 700, soe_series=False), _random_case(rng, 13, max_out=40),
+             _random_case(rng, 300, dt=0.5, max_out=12)]
+    lengths, curves = reliability.outage_coverage(cases, gpu_solver)
+    for k, (c, L, lcp) in enumerate(zip(cases, lengths, curves)):
+        Lo, lo = _oracle(c)
+        np.testing.assert_array_equal(L, Lo, err_msg=f"case {k}")
+        np.testing.assert_array_equal(lcp, lo[:len(lcp)], err_msg=f"case {k}")
+        assert len(np.unique(L)) > 1 or k == 4, f"case {k} exercises only one outcome"
+
+
+def test_invalid_case_raises(gpu_solver):
+    bad = reliability.OutageCase(critical_load=np.ones(10), dt=1.0, max_outage_duration=0, ess=dict(E=1, rte=0.9))
+    with pytest.raises(Exception, match="max_outage >= dt"):
+        reliability.outage_coverage([bad], gpu_solver)
