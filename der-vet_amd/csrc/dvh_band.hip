@@ -45,6 +45,24 @@ __host__ __device__ inline size_t band_lds_bytes(int B, int S) {
   return align16(sizeof(double) * band_lds_doubles(B, S)) + align16(sizeof(int32_t) * ((size_t)S * B + 4));
 }
 
+// KKT pieces of one column / one row (out of line: the KKT check runs every 128 iterations, and inlined it
+// would raise the whole kernel's register allocation)
+struct ColKkt {
+  double rd2, cx, bt;
+};
+__device__ __noinline__ ColKkt col_kkt_fn(double kt, double cj, double loj, double hij, double xj, double d) {
+  const double rc = (cj - kt) / d;
+  const bool fl = isfinite(loj), fh = isfinite(hij);
+  const double lam = (fl && fh) ? rc : (fl ? fmax(rc, 0.0) : (fh ? fmin(rc, 0.0) : 0.0));
+  const double rd = rc - lam;
+  return {rd * rd, cj * xj, (fl ? loj * d * fmax(lam, 0.0) : 0.0) + (fh ? hij * d * fmin(lam, 0.0) : 0.0)};
+}
+__device__ __noinline__ double row_kkt_fn(double kv, double qi, double dr, int ge) {
+  double r = (qi - kv) / dr;
+  if (ge) r = fmax(r, 0.0);
+  return r * r;
+}
+
 template <int B, int S>
 __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Work w, const Chunk ch, const Opts o) {
   constexpr int NW = B / kWave;
@@ -530,21 +548,13 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
       if (J > 0) tau_parts(ypd);
       lds_barrier();
       auto col_kkt = [&](int j, double kt, double cj, double loj, double hij, double xj) {
-        loj = opaque(loj);
-        hij = opaque(hij);
-        const double d = dcv[opaque(j)];
-        const double rc = (cj - kt) / d;
-        const bool fl = isfinite(loj), fh = isfinite(hij);
-        const double lam = (fl && fh) ? rc : (fl ? fmax(rc, 0.0) : (fh ? fmin(rc, 0.0) : 0.0));
-        const double rd = rc - lam;
-        acc[5] += rd * rd;
-        acc[6] += cj * xj;
-        acc[8] += (fl ? loj * d * fmax(lam, 0.0) : 0.0) + (fh ? hij * d * fmin(lam, 0.0) : 0.0);
+        const ColKkt r = col_kkt_fn(kt, cj, loj, hij, xj, dcv[opaque(j)]);
+        acc[5] += r.rd2;
+        acc[6] += r.cx;
+        acc[8] += r.bt;
       };
       auto row_kkt = [&](int i, double kv, double qi, double yi, bool ge) {
-        double r = (qi - kv) / drv[opaque(i)];
-        if (ge) r = fmax(r, 0.0);
-        acc[4] += r * r;
+        acc[4] += row_kkt_fn(kv, qi, drv[opaque(i)], ge);
         acc[7] += qi * yi;
       };
       double kt[S][3];
