@@ -57,7 +57,7 @@ struct dvh_handle {
   DevBuf w_tptr, w_tind, w_tval, w_kval, w_rowof, w_perm, w_dr, w_dc, w_cs, w_ls, w_us, w_qs, w_vbuf, w_wbuf,
       w_tmpc, w_tmpr, w_longk, w_longt, w_scal;
   DevBuf d_list, d_hinv;
-  DevBuf o_data, o_cases, o_len, o_hist;  // reliability sweep
+  DevBuf o_data, o_cases, o_len, o_hist, o_soe;  // reliability sweep
   double outage_ms = 0.0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<std::array<hipEvent_t, 3>> chunk_events;
@@ -172,7 +172,7 @@ int dvh_destroy(dvh_handle* h) {
                     &h->d_u, &h->d_list, &h->d_hinv, &h->d_x, &h->d_y, &h->d_stats, &h->d_istats, &h->w_tptr, &h->w_tind, &h->w_tval,
                     &h->w_kval, &h->w_rowof, &h->w_perm, &h->w_dr, &h->w_dc, &h->w_cs, &h->w_ls, &h->w_us,
                     &h->w_qs, &h->w_vbuf, &h->w_wbuf, &h->w_tmpc, &h->w_tmpr, &h->w_longk, &h->w_longt, &h->w_scal,
-                    &h->o_data, &h->o_cases, &h->o_len, &h->o_hist};
+                    &h->o_data, &h->o_cases, &h->o_len, &h->o_hist, &h->o_soe};
   for (DevBuf* b : bufs) b->release();
   for (auto& e : h->ev)
     if (e) hipEventDestroy(e);
@@ -222,16 +222,20 @@ int dvh_set_kernel_path(dvh_handle* h, int mode) {
   return DVH_OK;
 }
 
-int dvh_outage_coverage(dvh_handle* h, const dvh_outage_case* cases, int32_t count, int32_t* lengths,
-                        double* lcp) {
-  if (!h) return DVH_ERR_ARG;
-  if (count < 0 || (count > 0 && (!cases || !lcp))) return fail(h, DVH_ERR_ARG, "cases and lcp are required");
-  if (count == 0) return DVH_OK;
+// Validates the outage cases and moves them to the device (o_data / o_cases); olen[k] = simulated outage steps
+// (int(max_outage / dt), or int(target_hours[k] / dt) for the min-SOE mode).
+struct OutagePack {
+  std::vector<int> olen;
+  size_t nlen = 0, nhist = 0;
+  int max_n = 0, max_bins = 0;
+};
+static int outage_pack(dvh_handle* h, const dvh_outage_case* cases, int32_t count, const int32_t* target_hours,
+                       OutagePack& P) {
   hipSetDevice(h->device);
-  // validate, size the packed inputs
   size_t nd = 0, nlen = 0, nhist = 0;
   int max_n = 0, max_bins = 0;
-  std::vector<int> olen(count);
+  std::vector<int>& olen = P.olen;
+  olen.assign(count, 0);
   for (int k = 0; k < count; ++k) {
     const dvh_outage_case& c = cases[k];
     const std::string w = "outage case " + std::to_string(k) + ": ";
@@ -240,6 +244,11 @@ int dvh_outage_coverage(dvh_handle* h, const dvh_outage_case* cases, int32_t cou
       return fail(h, DVH_ERR_ARG, w + "dt > 0 and max_outage >= dt required");
     if (!(c.rte > 0.0)) return fail(h, DVH_ERR_ARG, w + "rte must be > 0");
     olen[k] = (int)(c.max_outage / c.dt);  // int(self.max_outage_duration / self.dt), Reliability.py:917
+    if (target_hours) {  // outage_len = self.outage_duration / self.dt (min_soe_iterative, :712)
+      if (target_hours[k] < 1 || target_hours[k] / c.dt < 1.0)
+        return fail(h, DVH_ERR_ARG, w + "target outage hours must be >= dt");
+      olen[k] = (int)(target_hours[k] / c.dt);
+    }
     if (olen[k] + 1 > 16384) return fail(h, DVH_ERR_UNSUPPORTED, w + "more than 16384 outage steps");
     nd += (size_t)c.n_steps * (1 + (c.pv_max ? 1 : 0) + (c.pv_vari ? 1 : 0) + (c.init_soe ? 1 : 0)) +
           (c.load_shed_pct ? (size_t)c.max_outage : 0);
@@ -292,6 +301,25 @@ int dvh_outage_coverage(dvh_handle* h, const dvh_outage_case* cases, int32_t cou
   hipStream_t s = h->stream;
   DVH_HIP(h, hipMemcpyAsync(h->o_data.p, data.data(), sizeof(double) * data.size(), hipMemcpyHostToDevice, s));
   DVH_HIP(h, hipMemcpyAsync(h->o_cases.p, dc.data(), sizeof(dvh::OutageCase) * count, hipMemcpyHostToDevice, s));
+  DVH_HIP(h, hipStreamSynchronize(s));  // the host staging vectors end here
+  P.nlen = nlen;
+  P.nhist = nhist;
+  P.max_n = max_n;
+  P.max_bins = max_bins;
+  return DVH_OK;
+}
+
+int dvh_outage_coverage(dvh_handle* h, const dvh_outage_case* cases, int32_t count, int32_t* lengths,
+                        double* lcp) {
+  if (!h) return DVH_ERR_ARG;
+  if (count < 0 || (count > 0 && (!cases || !lcp))) return fail(h, DVH_ERR_ARG, "cases and lcp are required");
+  if (count == 0) return DVH_OK;
+  OutagePack P;
+  if (int rc = outage_pack(h, cases, count, nullptr, P)) return rc;
+  const std::vector<int>& olen = P.olen;
+  const size_t nlen = P.nlen, nhist = P.nhist;
+  const int max_n = P.max_n, max_bins = P.max_bins;
+  hipStream_t s = h->stream;
   DVH_HIP(h, hipMemsetAsync(h->o_hist.p, 0, sizeof(int32_t) * nhist, s));
   DVH_HIP(h, hipEventRecord(h->ev[0], s));
   hipError_t e = dvh::launch_outage(h->o_cases.as<dvh::OutageCase>(), count, max_n, max_bins,
@@ -305,8 +333,7 @@ int dvh_outage_coverage(dvh_handle* h, const dvh_outage_case* cases, int32_t cou
   float ms = 0.0f;
   if (hipEventElapsedTime(&ms, h->ev[0], h->ev[3]) == hipSuccess) h->outage_ms = ms;
   // the curve, in the reference's float64 arithmetic (Reliability.py:947-957)
-  size_t po = 0;
-  ho = 0;
+  size_t po = 0, ho = 0;
   for (int k = 0; k < count; ++k) {
     const dvh_outage_case& c = cases[k];
     double length = c.dt;
@@ -324,6 +351,27 @@ int dvh_outage_coverage(dvh_handle* h, const dvh_outage_case* cases, int32_t cou
     po += olen[k];
     ho += olen[k] + 1;
   }
+  return DVH_OK;
+}
+
+int dvh_outage_min_soe(dvh_handle* h, const dvh_outage_case* cases, int32_t count, const int32_t* target_hours,
+                       double* min_soe) {
+  if (!h) return DVH_ERR_ARG;
+  if (count < 0 || (count > 0 && (!cases || !target_hours || !min_soe)))
+    return fail(h, DVH_ERR_ARG, "cases, target_hours and min_soe are required");
+  if (count == 0) return DVH_OK;
+  OutagePack P;
+  if (int rc = outage_pack(h, cases, count, target_hours, P)) return rc;
+  hipStream_t s = h->stream;
+  DVH_HIP(h, h->o_soe.ensure(sizeof(double) * P.nlen));
+  DVH_HIP(h, hipEventRecord(h->ev[0], s));
+  hipError_t e = dvh::launch_outage_min_soe(h->o_cases.as<dvh::OutageCase>(), count, P.max_n, h->o_soe.as<double>(), s);
+  if (e != hipSuccess) return hip_fail(h, e, "launch_outage_min_soe");
+  DVH_HIP(h, hipEventRecord(h->ev[3], s));
+  DVH_HIP(h, hipMemcpyAsync(min_soe, h->o_soe.p, sizeof(double) * P.nlen, hipMemcpyDeviceToHost, s));
+  DVH_HIP(h, hipStreamSynchronize(s));
+  float ms = 0.0f;
+  if (hipEventElapsedTime(&ms, h->ev[0], h->ev[3]) == hipSuccess) h->outage_ms = ms;
   return DVH_OK;
 }
 

@@ -102,6 +102,9 @@ struct OutageCase {
 // One thread per (case, start step); hist must be zeroed (sum of outage_len + 1 bins); lengths may be null.
 hipError_t launch_outage(const OutageCase* d_cases, int ncase, int max_steps_n, int max_bins, int32_t* d_lengths,
                          int32_t* d_hist, hipStream_t s);
+// min_soe_iterative mode: soe_used (max - min SOE of a target-length outage from soe0) per start.
+hipError_t launch_outage_min_soe(const OutageCase* d_cases, int ncase, int max_steps_n, double* d_soe_used,
+                                 hipStream_t s);
 
 // Grid-wide PDHG for one window too large for the workgroup-per-window kernels (dvh_large.hip).
 struct LargeSolver;

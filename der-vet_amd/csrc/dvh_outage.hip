@@ -34,17 +34,25 @@ __device__ __forceinline__ double pymin3(double a, double b, double c) {
   return r;
 }
 
-__global__ __launch_bounds__(kOutB) void outage_kernel(const OutageCase* cases, int32_t* lengths, int32_t* hist) {
+// MINSOE = false: covered length per start + histogram (load_coverage_probability :876-967).
+// MINSOE = true: soe_used per start = max - min of the SOE profile including the start (min_soe_iterative
+// :685-756, the reliability minimum-SOE requirement), written to soe_used[len_off + t].
+template <bool MINSOE>
+__global__ __launch_bounds__(kOutB) void outage_kernel(const OutageCase* cases, int32_t* lengths, int32_t* hist,
+                                                      double* soe_used) {
 #pragma clang fp contract(off)
   extern __shared__ int32_t lh[];  // [outage_len + 1] histogram of this workgroup
   const OutageCase c = cases[blockIdx.y];
   const int nb = c.outage_len + 1;
-  for (int i = threadIdx.x; i < nb; i += kOutB) lh[i] = 0;
-  __syncthreads();
+  if (!MINSOE) {
+    for (int i = threadIdx.x; i < nb; i += kOutB) lh[i] = 0;
+    __syncthreads();
+  }
   const int t = blockIdx.x * kOutB + threadIdx.x;
   if (t < c.n_steps) {
     const int stop = min(t + c.max_steps, c.n_steps);  // data_process slices max_steps entries (:462-465)
-    double soe = c.init_soe ? c.init_soe[t] : c.soe0;
+    double soe = (!MINSOE && c.init_soe) ? c.init_soe[t] : c.soe0;
+    double smax = soe, smin = soe;
     int k = 0;
     for (; k < c.outage_len; ++k) {
       const int i = t + k;
@@ -69,13 +77,23 @@ __global__ __launch_bounds__(kOutB) void outage_kernel(const OutageCase* cases, 
         if (0.0 < around(dl - discharge, 1e2)) break;
         soe = soe - (discharge * c.dt);
       }
+      if (MINSOE) {
+        smax = soe > smax ? soe : smax;
+        smin = soe < smin ? soe : smin;
+      }
     }
-    if (lengths) lengths[c.len_off + t] = k;
-    atomicAdd(&lh[k], 1);
+    if (MINSOE) {
+      soe_used[c.len_off + t] = smax - smin;
+    } else {
+      if (lengths) lengths[c.len_off + t] = k;
+      atomicAdd(&lh[k], 1);
+    }
   }
-  __syncthreads();
-  for (int i = threadIdx.x; i < nb; i += kOutB)
-    if (lh[i]) atomicAdd(&hist[c.hist_off + i], lh[i]);
+  if (!MINSOE) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < nb; i += kOutB)
+      if (lh[i]) atomicAdd(&hist[c.hist_off + i], lh[i]);
+  }
 }
 
 }  // namespace
@@ -86,7 +104,15 @@ hipError_t launch_outage(const OutageCase* d_cases, int ncase, int max_steps_n, 
   const size_t lds = sizeof(int32_t) * (size_t)max_bins;
   if (lds > 64 * 1024) return hipErrorInvalidValue;
   dim3 grid((max_steps_n + kOutB - 1) / kOutB, ncase);
-  hipLaunchKernelGGL(outage_kernel, grid, dim3(kOutB), lds, s, d_cases, d_lengths, d_hist);
+  hipLaunchKernelGGL(outage_kernel<false>, grid, dim3(kOutB), lds, s, d_cases, d_lengths, d_hist, nullptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_outage_min_soe(const OutageCase* d_cases, int ncase, int max_steps_n, double* d_soe_used,
+                                 hipStream_t s) {
+  if (ncase <= 0 || max_steps_n <= 0) return hipSuccess;
+  dim3 grid((max_steps_n + kOutB - 1) / kOutB, ncase);
+  hipLaunchKernelGGL(outage_kernel<true>, grid, dim3(kOutB), 0, s, d_cases, nullptr, nullptr, d_soe_used);
   return hipGetLastError();
 }
 

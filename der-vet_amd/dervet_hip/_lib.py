@@ -78,6 +78,8 @@ SYMBOLS = {
     "dvh_set_kernel_path": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "dvh_outage_coverage": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(OutageCase), ctypes.c_int32, c_int32_p,
                                            c_double_p]),
+    "dvh_outage_min_soe": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(OutageCase), ctypes.c_int32, c_int32_p,
+                                          c_double_p]),
     "dvh_last_outage_ms": (ctypes.c_int, [ctypes.c_void_p, c_double_p]),
 }
 

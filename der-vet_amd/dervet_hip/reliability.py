@@ -57,9 +57,7 @@ def der_mix_properties(case):
     return dg, pv_max, props, pv_vari, gamma
 
 
-def outage_coverage(cases, solver):
-    """Covered length per start (list of int32 arrays) and the LCP curve per case (list of float arrays)."""
-    lib = solver._lib
+def _cases_struct(cases):
     arr = (_lib.OutageCase * len(cases))()
     keep, sizes = [], []
 
@@ -85,6 +83,13 @@ def outage_coverage(cases, solver):
         o.soe_min, o.soe_max = props["operation SOE min"], props["operation SOE max"]
         o.charge_max, o.discharge_max, o.rte = props["charge max"], props["discharge max"], props["rte"]
         sizes.append((N, int(c.max_outage_duration / c.dt)))
+    return arr, keep, sizes
+
+
+def outage_coverage(cases, solver):
+    """Covered length per start (list of int32 arrays) and the LCP curve per case (list of float arrays)."""
+    lib = solver._lib
+    arr, keep, sizes = _cases_struct(cases)
     lengths = np.zeros(sum(n for n, _ in sizes), np.int32)
     lcp = np.zeros(sum(L for _, L in sizes), np.float64)
     solver._check(lib.dvh_outage_coverage(solver._h, arr, len(cases), lengths.ctypes.data_as(_lib.c_int32_p),
@@ -96,6 +101,23 @@ def outage_coverage(cases, solver):
         a += N
         b += L
     return out_l, out_c
+
+
+def min_soe(cases, target_hours, solver):
+    """Reliability.min_soe_iterative (:685-756) per case: [N] minimum SOE (kWh) the ESS must hold at each step
+    to ride through a target_hours outage from soc_init x energy rating (the 'Reliability Min State of Energy
+    (kWh)' requirement applied to every window as an ene lower bound, :334-354)."""
+    lib = solver._lib
+    arr, keep, sizes = _cases_struct(cases)
+    tgt = np.ascontiguousarray(np.broadcast_to(np.asarray(target_hours, np.int32), (len(cases),)))
+    out = np.zeros(sum(n for n, _ in sizes), np.float64)
+    solver._check(lib.dvh_outage_min_soe(solver._h, arr, len(cases), tgt.ctypes.data_as(_lib.c_int32_p),
+                                         out.ctypes.data_as(_lib.c_double_p)), "dvh_outage_min_soe")
+    res, a = [], 0
+    for N, _ in sizes:
+        res.append(out[a:a + N])
+        a += N
+    return res
 
 
 def load_coverage_probability(cases, solver):

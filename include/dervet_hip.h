@@ -183,7 +183,14 @@ typedef struct dvh_outage_case {
  * Bit-exact with the reference's numpy arithmetic.  Blocks until done. */
 int dvh_outage_coverage(dvh_handle* h, const dvh_outage_case* cases, int32_t count, int32_t* lengths,
                         double* lcp);
-/* Kernel time of the last dvh_outage_coverage call (HIP events, milliseconds). */
+/* Reliability minimum-SOE requirement (Reliability.min_soe_iterative, Reliability.py:685-756, which feeds the
+ * 'energy' 'min' system requirement of every window, :334-354): for every start step, an outage of
+ * target_hours[k] (the Reliability 'target') simulated from soe0 (= soc_init x energy rating; init_soe and
+ * load_shed_pct as above, init_soe ignored); min_soe[start] = max - min of its SOE profile including the start.
+ * min_soe: caller-allocated [sum n_steps] (case-major).  Bit-exact with the numpy reference. */
+int dvh_outage_min_soe(dvh_handle* h, const dvh_outage_case* cases, int32_t count, const int32_t* target_hours,
+                       double* min_soe);
+/* Kernel time of the last dvh_outage_coverage / dvh_outage_min_soe call (HIP events, milliseconds). */
 int dvh_last_outage_ms(const dvh_handle* h, double* ms);
 
 /* Kernel cascade (testing / A-B timing): 0 = default (battery-banded -> ELL -> generic CSR), 1 = generic

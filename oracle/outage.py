@@ -10,6 +10,8 @@ Follows dervet/MicrogridValueStreams/Reliability.py, line by line in semantics:
                                           into the ESS, else discharge to cover the load (checks rounded to 2
                                           decimals); the outage is covered up to the first step that fails
   * get_der_mix_properties     :276-332   DER aggregates (pv_max, pv_max * nu, largest gamma, DG power)
+  * min_soe_iterative          :685-756   minimum SOE per start = max - min of the SOE profile of a
+                                          target-length outage (the config-5 reliability requirement, a10)
 Rounding is numpy's ``around`` (x * 10**d, round half to even, / 10**d), restated with Python floats.
 Pinned against the reference's golden ``load_coverage_prob*.csv`` curves (tests/test_outage_oracle.py).
 """
@@ -83,6 +85,22 @@ def coverage_lengths(cl, gen, pmax, pvar, gamma, ess, init_soe, max_outage_durat
     for t in range(N):
         out[t], _ = simulate_outage(t, cl, gen, pmax, pvar, gamma, ess, soe0[t], outage_len,
                                     int(max_outage_duration), dt, load_shed_pct)
+    return out
+
+
+def min_soe(cl, gen, pmax, pvar, gamma, ess, soc_init, outage_duration, max_outage_duration, dt,
+            load_shed_pct=None):
+    """Reliability.min_soe_iterative (Reliability.py:685-733): for every start, simulate an outage of
+    outage_duration / dt steps from soc_init x energy rating and return soe_used (:734-756) = max - min of the
+    SOE profile including the starting SOE.  [N] array (the 'Reliability Min State of Energy (kWh)')."""
+    N = len(cl)
+    soe0 = soc_init * ess["energy rating"]
+    out = np.zeros(N)
+    for t in range(N):
+        _, prof = simulate_outage(t, cl, gen, pmax, pvar, gamma, ess, soe0, int(outage_duration / dt),
+                                  int(max_outage_duration), dt, load_shed_pct)
+        prof.insert(0, soe0)
+        out[t] = np.max(prof) - np.min(prof)
     return out
 
 

@@ -72,3 +72,23 @@ def test_invalid_case_raises(gpu_solver):
     bad = reliability.OutageCase(critical_load=np.ones(10), dt=1.0, max_outage_duration=0, ess=dict(E=1, rte=0.9))
     with pytest.raises(Exception, match="max_outage >= dt"):
         reliability.outage_coverage([bad], gpu_solver)
+
+
+def test_min_soe_bit_exact(gpu_solver):
+    """Reliability.min_soe_iterative (the config-5 'Reliability Min State of Energy' requirement) on the golden
+    sites and randomized cases: every start's soe_used equals the oracle's (parity unpinned vs the reference:
+    no reference run writes this column)."""
+    from oracle import outage
+    golden = outage_cases.load()
+    rng = np.random.default_rng(7)
+    cases = [_case(golden["uc2_es+pv"]), _case(golden["ls_w_ls1"]), _random_case(rng, 600),
+             _random_case(rng, 400, pv=False, shed=False), _random_case(rng, 9, max_out=30)]
+    targets = [4, 4, 6, 3, 12]
+    got = reliability.min_soe(cases, targets, gpu_solver)
+    for k, (c, tgt, g) in enumerate(zip(cases, targets, got)):
+        dg, pmax, props, pvar, gamma = reliability.der_mix_properties(c)
+        ref = outage.min_soe(np.asarray(c.critical_load, np.float64), np.repeat(dg, len(pmax)), pmax, pvar, gamma,
+                             props, c.soc_init, tgt, c.max_outage_duration, c.dt, c.load_shed_pct)
+        np.testing.assert_array_equal(g, ref, err_msg=f"case {k}")
+        assert (g >= 0).all()
+    assert got[0].max() > 0
