@@ -514,22 +514,48 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
     std::vector<int32_t> ell_list;  // empty + ell_all: the whole chunk
     bool ell_all = true;
     if (fast && h->kernel_path == 0) {
-      DVH_HIP(h, dvh::launch_pdhg_band(b, w, c.ch, o, s));
-      ist.resize(2 * (size_t)c.ch.count);
-      DVH_HIP(h, hipMemcpyAsync(ist.data(), bt->istats + 2 * (size_t)c.ch.first, I * ist.size(),
-                                hipMemcpyDeviceToHost, s));
-      DVH_HIP(h, hipStreamSynchronize(s));
+      // pass 1: battery (+ DCM) windows over the whole chunk; pass 2: the ICE variant over what pass 1 returned
+      auto band_pass = [&](bool ice, const std::vector<int32_t>* in, std::vector<int32_t>& out) -> hipError_t {
+        hipError_t r;
+        if (in) {
+          r = hipMemcpyAsync(h->d_list.p, in->data(), I * in->size(), hipMemcpyHostToDevice, s);
+          if (r != hipSuccess) return r;
+          r = dvh::launch_pdhg_band(b, w, c.ch, o, s, ice, h->d_list.as<int32_t>(), (int)in->size());
+        } else {
+          r = dvh::launch_pdhg_band(b, w, c.ch, o, s, ice, nullptr, 0);
+        }
+        if (r != hipSuccess) return r;
+        ist.resize(2 * (size_t)c.ch.count);
+        r = hipMemcpyAsync(ist.data(), bt->istats + 2 * (size_t)c.ch.first, I * ist.size(), hipMemcpyDeviceToHost,
+                           s);
+        if (r != hipSuccess) return r;
+        r = hipStreamSynchronize(s);
+        if (r != hipSuccess) return r;
+        out.clear();
+        int nb = 0;
+        auto visit = [&](int kg) {
+          if (is_large(kg)) return;
+          if (ist[2 * (size_t)(kg - c.ch.first)] == -2)
+            out.push_back(kg);
+          else
+            ++nb;
+        };
+        if (in) {
+          for (int kg : *in) visit(kg);
+        } else {
+          for (int k = 0; k < c.ch.count; ++k) visit(c.ch.first + k);
+        }
+        h->n_band += nb;
+        if (nb > 0 && variant < 0) variant = 9000000 + 12 + (ice ? 100 : 0);  // band kernel, 768 threads
+        return hipSuccess;
+      };
       ell_all = false;
-      int nb = 0;
-      for (int k = 0; k < c.ch.count; ++k) {
-        if (is_large(c.ch.first + k)) continue;
-        if (ist[2 * (size_t)k] == -2)
-          ell_list.push_back(c.ch.first + k);
-        else
-          ++nb;
+      DVH_HIP(h, band_pass(false, nullptr, ell_list));
+      if (!ell_list.empty()) {
+        std::vector<int32_t> rest;
+        DVH_HIP(h, band_pass(true, &ell_list, rest));
+        ell_list.swap(rest);
       }
-      h->n_band += nb;
-      if (nb > 0) variant = 9000000 + 12;  // band kernel, 768 threads
     }
     hipError_t e = hipSuccess;
     const int n_ell_in = ell_all ? c.ch.count : (int)ell_list.size();

@@ -2,23 +2,23 @@
 //
 // Same algorithm, scaling and check logic as pdhg_ell_kernel (dvh_kernels.hip; restated in oracle/pdlp_ref.py),
 // for windows whose CSR is the storagevet battery + DCM window (dervet/MicrogridScenario.py:319 solves it per
-// window; SURVEY.md Appendix A, dervet_hip/lp/builder.py):
-//   x = [ch(T), dis(T), ene(T), tau(J)],  J <= 4 demand periods in the window
+// window; SURVEY.md Appendix A, dervet_hip/lp/builder.py), optionally with an LP-relaxed ICE (ICE = true):
+//   x = [ch(T), dis(T), ene(T), tau(J)] (+ [elec(T), on(T)]),  J <= 4 demand periods in the window
 //   row 0          ene_0                                      (= target)
 //   row t+1        ch_t, dis_t, ene_t, ene_{t+1}               t = 0 .. T-2  (SOE recurrence)
 //   row T          ch_{T-1}, dis_{T-1}, ene_{T-1}              (end-of-window target)
-//   >= rows        ch_t, dis_t, tau_j                          at most one per step t (DCM epigraph)
-//   bounds         ch, dis >= 0 (scaled lower bound exactly 0), objective coefficient of ene = 0
+//   >= rows        ch_t, dis_t, tau_j (+ elec_t)               at most one per step t (DCM epigraph)
+//   >= rows (ICE)  elec_t, on_t                                exactly two per step (rated / minimum power,
+//                                                              RotatingGeneratorSizing.py:110-136)
+//   bounds         ch, dis (, elec, on) >= 0 (scaled lower bound exactly 0)
 // The structure is detected and verified on the device from the CSR pattern (any values, any entry order
-// within a row, DCM rows in any order); a window that does not match comes back with status kNeedsEll and
-// is solved by the ELL kernel.
+// within a row, >= rows in any order); a window that does not match comes back with status kNeedsEll.
 //
-// Mapping: lane g owns S consecutive time steps t = S g + s -- their columns ch, dis, ene, their SOE rows and
-// their DCM rows -- with every coefficient, bound, iterate and anchor in VGPRs.  An SpMV needs only the
-// neighbour lane's first ene (K x) and last SOE-row dual (K^T y): one LDS store + one LDS load per lane and
-// half-step instead of per-entry gathers.  The dense tau columns are summed by wave 0 from per-lane partials
-// (no per-wave reduction).  With S = 2, 384 threads cover a 768-step monthly window in <= 168 VGPRs: two
-// windows per CU, so one window's barrier and latency stalls are covered by the other window's work.
+// Mapping: lane t owns time step t -- its columns, its SOE / DCM (/ ICE) rows -- with every coefficient, bound,
+// objective, iterate and anchor in VGPRs.  An SpMV needs only the next step's ene (K x) and the previous SOE
+// row's dual (K^T y): one LDS store + one LDS load per lane and half-step instead of per-entry gathers.  The
+// dense tau columns are summed by wave 0 from per-lane partials (no per-wave reduction).  768 threads per
+// window, 12 waves, <= 168 VGPRs.
 #include <type_traits>
 
 #include "dvh_device.h"
@@ -26,23 +26,19 @@
 namespace dvh {
 namespace {
 
-#ifndef DVH_BAND_S
-#define DVH_BAND_S 1
-#endif
-constexpr int kBandS = DVH_BAND_S;    // steps per lane
-constexpr int kBandB = 768 / kBandS;  // threads per window (T <= 768)
+constexpr int kBandB = 768;   // threads per window (T <= kBandB steps)
 constexpr int kJMax = 4;      // tau (demand-period) columns per window
 constexpr int kNeedsEll = -2;
 
-// LDS layout in doubles (then ints): XE[B+1] YS[B+1] XT[kJMax] red[kNRed(NW+1)+4]
-// TP[kJMax][B] XP[3S][B] YP[2S][B] | ints: dcm[S B] flag[4]
-__host__ __device__ inline size_t band_lds_doubles(int B, int S) {
-  const int NW = B / kWave;
-  return 2 * (size_t)(B + 1) + kJMax + (size_t)kNRed * (NW + 1) + 4 + (size_t)kJMax * B +
-         5 * (size_t)S * B;
+// LDS layout in doubles (then ints): XE[B+1] YS[B+1] XT[kJMax] red[kNRed(NW+1)+4] TP[kJMax][B] XP[NC][B] YP[NR][B]
+// (ICE: RO[6][B]) | ints: dcm[B] ice_a[B] ice_b[B] ice_n[B] flag[4]
+__host__ __device__ inline size_t band_lds_doubles(int B, bool ice) {
+  const int NW = B / kWave, NC = ice ? 5 : 3, NR = ice ? 4 : 2;
+  return 2 * (size_t)(B + 1) + kJMax + (size_t)kNRed * (NW + 1) + 4 + (size_t)kJMax * B + (size_t)(NC + NR) * B +
+         (ice ? 6 * (size_t)B : 0);
 }
-__host__ __device__ inline size_t band_lds_bytes(int B, int S) {
-  return align16(sizeof(double) * band_lds_doubles(B, S)) + align16(sizeof(int32_t) * ((size_t)S * B + 4));
+__host__ __device__ inline size_t band_lds_bytes(int B, bool ice) {
+  return align16(sizeof(double) * band_lds_doubles(B, ice)) + align16(sizeof(int32_t) * (4 * (size_t)B + 4));
 }
 
 // KKT pieces of one column / one row (out of line: the KKT check runs every 128 iterations, and inlined it
@@ -63,37 +59,49 @@ __device__ __noinline__ double row_kkt_fn(double kv, double qi, double dr, int g
   return r * r;
 }
 
-template <int B, int S>
-__global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Work w, const Chunk ch, const Opts o) {
+template <int B, bool ICE>
+__global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Work w, const Chunk ch, const Opts o,
+                                                        const int32_t* list) {
   constexpr int NW = B / kWave;
+  constexpr int NC = ICE ? 5 : 3;  // columns per step: ch, dis, ene (, elec, on)
+  constexpr int NR = ICE ? 4 : 2;  // rows per step: SOE, DCM (, ICE rated, ICE minimum)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int k = ch.first + blockIdx.x;
-  const int kl = blockIdx.x;
+  const int k = list ? list[blockIdx.x] : ch.first + (int)blockIdx.x;
+  const int kl = k - ch.first;
   const WinOff W = win_offsets(b, ch, k);
   const int n = W.n, m = W.m, meq = W.meq;
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const double* scal = w.scal + (int64_t)kl * kScal;
-  const int T = meq - 1, J = n - 3 * T, MI = m - meq;
+  const int T = meq - 1, J = n - (ICE ? 5 : 3) * T, MI = m - meq;
+  const int MD = ICE ? MI - 2 * T : MI;  // DCM rows
   auto bail = [&]() {
     if (tid == 0) {
       b.istats[2 * k] = kNeedsEll;
       b.istats[2 * k + 1] = 0;
     }
   };
-  if (scal[6] != 0.0 || T < 1 || T > S * B || J < 0 || J > kJMax || MI > T || (J == 0 && MI > 0)) {
+  if (scal[6] != 0.0 || T < 1 || T > B || J < 0 || J > kJMax || MD < 0 || MD > T || (J == 0 && MD > 0)) {
     bail();
     return;
   }
+  const int CE = 3 * T + J, CO = 4 * T + J;  // first elec / on column (ICE)
   // ---- LDS carve
-  double* XE = reinterpret_cast<double*>(smem);  // x-bar (x+) of ene at the lane's first step: [g]; [B] = 0
-  double* YS = XE + (B + 1);                     // y (y+) of row S g: the init row (g = 0) / lane g-1's last SOE row
+  double* XE = reinterpret_cast<double*>(smem);  // x-bar (x+) of ene_t at [t]; [T..B] stay 0
+  double* YS = XE + (B + 1);                     // y (y+) of row t at [t]: the init row (t = 0), SOE row of step t-1
   double* XT = YS + (B + 1);                     // x-bar (x+) of the tau columns
   double* red = XT + kJMax;
   double* TP = red + kNRed * (NW + 1) + 4;       // [kJMax][B] per-lane partial K'y of the tau columns
-  double* XP = TP + kJMax * B;                   // [3S][B] T(z) of the lane's columns (check iterations)
-  double* YP = XP + 3 * S * B;                   // [2S][B] T(z) of the lane's rows
-  int32_t* dcm = reinterpret_cast<int32_t*>(smem + align16(sizeof(double) * band_lds_doubles(B, S)));  // [S B]
-  int32_t* flag = dcm + S * B;
+  double* XP = TP + kJMax * B;                   // [NC][B] T(z) of the lane's columns (check iterations)
+  double* YP = XP + NC * B;                      // [NR][B] T(z) of the lane's rows
+  // ICE: read-only data of the ICE columns / rows in LDS instead of VGPRs (the register budget at 3 waves per
+  // SIMD is 168): RO[0..1][.] = c of elec / on, RO[2..3][.] = upper bound of elec / on, RO[4..5][.] = q of the
+  // two ICE rows
+  double* RO = YP + NR * B;
+  int32_t* dcm = reinterpret_cast<int32_t*>(smem + align16(sizeof(double) * band_lds_doubles(B, ICE)));  // [B]
+  int32_t* ice_a = dcm + B;   // [B] ICE rows of each step (lower / higher row index), and their count
+  int32_t* ice_b = ice_a + B;
+  int32_t* ice_n = ice_b + B;
+  int32_t* flag = ice_n + B;
 
   const int32_t* gkp = b.indptr + W.row;
   const int32_t* gkc = b.indices + W.nz;
@@ -107,8 +115,11 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
   double* xo_g = b.x + W.on;
   double* yo_g = b.y + W.om;
 
-  // ---- structure check (every entry of every row accounted for) and the step -> DCM row map
-  for (int t = tid; t < S * B; t += B) dcm[t] = -1;
+  // ---- structure check (every entry of every row accounted for) and the step -> row maps
+  dcm[tid] = -1;
+  ice_a[tid] = 0x7fffffff;
+  ice_b[tid] = -1;
+  ice_n[tid] = 0;
   if (tid == 0) flag[0] = 0;
   __syncthreads();
   int bad = 0;
@@ -130,17 +141,34 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
       if (kind == 4 || ((seen >> kind) & 1u)) bad = 1;
       seen |= 1u << kind;
     }
-    // the kernel keeps no lower bound for ch / dis and no objective for ene
-    bad |= ls[t] != 0.0 || ls[T + t] != 0.0 || cs[2 * T + t] != 0.0;
+    // the kernel keeps no lower bound for ch / dis (/ elec / on)
+    bad |= ls[t] != 0.0 || ls[T + t] != 0.0;
+    if (ICE) bad |= ls[CE + t] != 0.0 || ls[CO + t] != 0.0;
   }
   for (int i = meq + tid; i < m; i += B) {
     const int p0 = gkp[i], len = gkp[i + 1] - p0;
-    if (len != 3) {
+    if (ICE && len == 2) {  // ICE row: elec_t, on_t
+      int te = -1, to = -1;
+      for (int e = 0; e < 2; ++e) {
+        const int c = gkc[p0 + e];
+        if (c >= CE && c < CE + T) te = c - CE;
+        else if (c >= CO && c < CO + T) to = c - CO;
+      }
+      if (te < 0 || te != to) {
+        bad = 1;
+        continue;
+      }
+      atomicMin(&ice_a[te], i);
+      atomicMax(&ice_b[te], i);
+      atomicAdd(&ice_n[te], 1);
+      continue;
+    }
+    if (len != (ICE ? 4 : 3)) {
       bad = 1;
       continue;
     }
-    int tc = -1, td = -1, jj = -1;
-    for (int e = 0; e < 3; ++e) {
+    int tc = -1, td = -1, jj = -1, te = ICE ? -1 : -2;
+    for (int e = 0; e < len; ++e) {
       const int c = gkc[p0 + e];
       if (c < T) {
         bad |= tc >= 0;
@@ -151,11 +179,14 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
       } else if (c >= 3 * T && c < 3 * T + J) {
         bad |= jj >= 0;
         jj = c - 3 * T;
+      } else if (ICE && c >= CE && c < CE + T) {
+        bad |= te >= 0;
+        te = c - CE;
       } else {
         bad = 1;
       }
     }
-    if (tc < 0 || td != tc || jj < 0) {
+    if (tc < 0 || td != tc || jj < 0 || (ICE && te != tc)) {
       bad = 1;
       continue;
     }
@@ -163,79 +194,99 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
   }
   if (bad) flag[0] = 1;
   __syncthreads();
+  if (ICE && tid < T && ice_n[tid] != 2) flag[0] = 1;  // exactly two ICE rows per step
+  __syncthreads();
   if (flag[0] != 0) {
     bail();
     return;
   }
 
-  // ---- the lane's steps t = S tid + s: columns ch, dis, ene (v = 0, 1, 2), SOE row t+1, DCM row -- in VGPRs
-  double x[S][3], xa[S][3], hi[S][3];
-  double cch[S], cdi[S], loe[S];  // objective of ch / dis, lower bound of ene
-  double ks[S][4];                // SOE row: coefficients of ch_t, dis_t, ene_t, ene_{t+1}
-  double kd[S][3];                // DCM row: coefficients of ch_t, dis_t, tau_j
-  double ys[S], yas[S], qsr[S], yd[S], yad[S], qd[S];
-  int drow[S], xta[S];            // DCM row index (-1: none), LDS address of XT[its tau]
-  int jt[S];
-  bool val[S];
-  double kp = 0.0;                // coefficient of ene_{S tid} in row S tid (init row or lane tid-1's last SOE row)
+  // ---- the lane's step t: columns (v) ch, dis, ene (, elec, on), rows (r) SOE, DCM (, ICE a, ICE b) -- VGPRs
+  const int t = tid;
+  const bool val = t < T;
+  auto col = [&](int v) { return v < 3 ? v * T + t : (v == 3 ? CE : CO) + t; };
+  double x[NC], xa[NC], cc[3], hi[3];
+  double loe = 0.0;                        // lower bound of ene (the others are 0)
+  double ks[4] = {0.0, 0.0, 0.0, 0.0};     // SOE row: coefficients of ch_t, dis_t, ene_t, ene_{t+1}
+  double kd[4] = {0.0, 0.0, 0.0, 0.0};     // DCM row: coefficients of ch_t, dis_t, tau_j, elec_t
+  double ka[2] = {0.0, 0.0}, kb[2] = {0.0, 0.0};  // ICE rows: coefficients of elec_t, on_t
+  double kp = 0.0;                         // coefficient of ene_t in row t (init row or SOE row of step t-1)
+  double y[NR], ya[NR], q[2];
+  int drow = -1, jt = 0, ra = -1, rb = -1;
 #pragma unroll
-  for (int s = 0; s < S; ++s) {
-    const int t = S * tid + s;
-    val[s] = t < T;
-    drow[s] = -1;
-    jt[s] = 0;
-    cch[s] = cdi[s] = loe[s] = 0.0;
-    ys[s] = yas[s] = qsr[s] = yd[s] = yad[s] = qd[s] = 0.0;
+  for (int v = 0; v < NC; ++v) x[v] = xa[v] = 0.0;
 #pragma unroll
-    for (int v = 0; v < 3; ++v) x[s][v] = xa[s][v] = hi[s][v] = kd[s][v] = 0.0;
+  for (int v = 0; v < 3; ++v) cc[v] = hi[v] = 0.0;
 #pragma unroll
-    for (int v = 0; v < 4; ++v) ks[s][v] = 0.0;
-    if (val[s]) {
+  for (int r = 0; r < NR; ++r) y[r] = ya[r] = 0.0;
+  q[0] = q[1] = 0.0;
+  if (ICE)
+    for (int u = 0; u < 6; ++u) RO[u * B + tid] = 0.0;
+  auto cof = [&](int v) -> double { return v < 3 ? cc[v] : RO[(v - 3) * B + tid]; };
+  auto hib = [&](int v) -> double { return v < 3 ? hi[v] : RO[(v - 1) * B + tid]; };
+  auto rhs = [&](int r) -> double { return r < 2 ? q[r] : RO[(r + 2) * B + tid]; };
+  if (val) {
 #pragma unroll
-      for (int v = 0; v < 3; ++v) {
-        hi[s][v] = us[v * T + t];
-        x[s][v] = xa[s][v] = fmin(fmax(0.0, ls[v * T + t]), hi[s][v]);
+    for (int v = 0; v < NC; ++v) {
+      const int j = col(v);
+      if (v < 3) {
+        hi[v] = us[j];
+        cc[v] = cs[j];
+      } else {
+        RO[(v - 1) * B + tid] = us[j];
+        RO[(v - 3) * B + tid] = cs[j];
       }
-      cch[s] = cs[t];
-      cdi[s] = cs[T + t];
-      loe[s] = ls[2 * T + t];
-      for (int p = gkp[t + 1]; p < gkp[t + 2]; ++p) {
+      x[v] = xa[v] = fmin(fmax(0.0, ls[j]), us[j]);
+    }
+    loe = ls[2 * T + t];
+    for (int p = gkp[t + 1]; p < gkp[t + 2]; ++p) {
+      const int c = gkc[p];
+      const double a = gkv[p];
+      if (c == t) ks[0] = a;
+      else if (c == T + t) ks[1] = a;
+      else if (c == 2 * T + t) ks[2] = a;
+      else ks[3] = a;
+    }
+    for (int p = gkp[t]; p < gkp[t + 1]; ++p)
+      if (gkc[p] == 2 * T + t) kp = gkv[p];
+    q[0] = qs[t + 1];
+    const int dv = dcm[t];
+    if (dv >= 0) {
+      drow = dv >> 3;
+      jt = dv & 7;
+      for (int p = gkp[drow]; p < gkp[drow + 1]; ++p) {
         const int c = gkc[p];
         const double a = gkv[p];
-        if (c == t) ks[s][0] = a;
-        else if (c == T + t) ks[s][1] = a;
-        else if (c == 2 * T + t) ks[s][2] = a;
-        else ks[s][3] = a;
+        if (c < T) kd[0] = a;
+        else if (c < 2 * T) kd[1] = a;
+        else if (c < 3 * T + J) kd[2] = a;
+        else kd[3] = a;
       }
-      if (s == 0)
-        for (int p = gkp[t]; p < gkp[t + 1]; ++p)
-          if (gkc[p] == 2 * T + t) kp = gkv[p];
-      qsr[s] = qs[t + 1];
-      if (o.warm) {  // warm start from the unscaled x / y in the output buffers
+      q[1] = qs[drow];
+    }
+    if (ICE) {
+      ra = ice_a[t];
+      rb = ice_b[t];
+      for (int p = gkp[ra]; p < gkp[ra + 1]; ++p) (gkc[p] < CO ? ka[0] : ka[1]) = gkv[p];
+      for (int p = gkp[rb]; p < gkp[rb + 1]; ++p) (gkc[p] < CO ? kb[0] : kb[1]) = gkv[p];
+      RO[4 * B + tid] = qs[ra];
+      RO[5 * B + tid] = qs[rb];
+    }
+    if (o.warm) {  // warm start from the unscaled x / y in the output buffers
 #pragma unroll
-        for (int v = 0; v < 3; ++v) {
-          const int j = v * T + t;
-          x[s][v] = xa[s][v] = fmin(fmax(xo_g[j] / dcv[j], ls[j]), hi[s][v]);
-        }
-        ys[s] = yas[s] = yo_g[t + 1] / drv[t + 1];
+      for (int v = 0; v < NC; ++v) {
+        const int j = col(v);
+        x[v] = xa[v] = fmin(fmax(xo_g[j] / dcv[j], ls[j]), us[j]);
       }
-      const int dv = dcm[t];
-      if (dv >= 0) {
-        drow[s] = dv >> 3;
-        jt[s] = dv & 7;
-        for (int p = gkp[drow[s]]; p < gkp[drow[s] + 1]; ++p) {
-          const int c = gkc[p];
-          const double a = gkv[p];
-          if (c < T) kd[s][0] = a;
-          else if (c < 2 * T) kd[s][1] = a;
-          else kd[s][2] = a;
-        }
-        qd[s] = qs[drow[s]];
-        if (o.warm) yd[s] = yad[s] = fmax(yo_g[drow[s]] / drv[drow[s]], 0.0);
+      y[0] = ya[0] = yo_g[t + 1] / drv[t + 1];
+      if (drow >= 0) y[1] = ya[1] = fmax(yo_g[drow] / drv[drow], 0.0);
+      if (ICE) {
+        y[2] = ya[2] = fmax(yo_g[ra] / drv[ra], 0.0);
+        y[3] = ya[3] = fmax(yo_g[rb] / drv[rb], 0.0);
       }
     }
-    xta[s] = lds_addr(XT + jt[s]);
   }
+  const int xta = lds_addr(XT + jt);
   // Special state in wave 0 (registers sp[], meaning by lane): lane j < J holds tau column j {x, xa, c, lo, hi, x+};
   // lane kInitLane holds the init row (row 0: ene_0 = target) {y, ya, y+, q, coefficient, -}.
   constexpr int kInitLane = kWave - 1;
@@ -262,52 +313,42 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
   XE[tid] = YS[tid] = 0.0;
   for (int u = tid; u < kJMax * B; u += B) TP[u] = 0.0;
 #pragma unroll
-  for (int s = 0; s < S; ++s) {
+  for (int v = 0; v < NC; ++v) XP[v * B + tid] = x[v];
 #pragma unroll
-    for (int v = 0; v < 3; ++v) XP[(3 * s + v) * B + tid] = x[s][v];
-    YP[(2 * s) * B + tid] = ys[s];
-    YP[(2 * s + 1) * B + tid] = yd[s];
-  }
+  for (int r = 0; r < NR; ++r) YP[r * B + tid] = y[r];
   __syncthreads();
 
   // ---- SpMV pieces (fixed summation order)
-  // K^T of the lane's columns from its rows' values (vs: SOE rows, vd: DCM rows) and vprev = value of row S tid
-  auto ktr = [&](const double (&vs)[S], const double (&vd)[S], double vprev, double (&out)[S][3]) {
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-      out[s][0] = fma(kd[s][0], vd[s], ks[s][0] * vs[s]);
-      out[s][1] = fma(kd[s][1], vd[s], ks[s][1] * vs[s]);
-      out[s][2] = fma(ks[s][2], vs[s], s == 0 ? kp * vprev : ks[s > 0 ? s - 1 : 0][3] * vs[s > 0 ? s - 1 : 0]);
+  // K^T of the lane's columns from its rows' values vr and vprev = the value of row t
+  auto ktr = [&](const double (&vr)[NR], double vprev, double (&out)[NC]) {
+    out[0] = fma(kd[0], vr[1], ks[0] * vr[0]);
+    out[1] = fma(kd[1], vr[1], ks[1] * vr[0]);
+    out[2] = fma(ks[2], vr[0], kp * vprev);
+    if constexpr (ICE) {
+      out[3] = fma(kb[0], vr[3], fma(ka[0], vr[2], kd[3] * vr[1]));
+      out[4] = fma(kb[1], vr[3], ka[1] * vr[2]);
     }
   };
-  // K of the lane's rows, own-column part (kfin adds the next lane's ene and the tau terms)
-  auto kown = [&](const double (&v)[S][3], double (&os)[S], double (&od)[S]) {
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-      os[s] = fma(ks[s][2], v[s][2], fma(ks[s][1], v[s][1], ks[s][0] * v[s][0]));
-      if (s + 1 < S) os[s] = fma(ks[s][3], v[s + 1 < S ? s + 1 : s][2], os[s]);
-      od[s] = fma(kd[s][1], v[s][1], kd[s][0] * v[s][0]);
+  // K of the lane's rows, own-column part (kfin adds the next step's ene and the tau term)
+  auto kown = [&](const double (&v)[NC], double (&os)[NR]) {
+    os[0] = fma(ks[2], v[2], fma(ks[1], v[1], ks[0] * v[0]));
+    os[1] = fma(kd[1], v[1], kd[0] * v[0]);
+    if constexpr (ICE) {
+      os[1] = fma(kd[3], v[3], os[1]);
+      os[2] = fma(ka[1], v[4], ka[0] * v[3]);
+      os[3] = fma(kb[1], v[4], kb[0] * v[3]);
     }
   };
-  auto kfin = [&](double (&os)[S], double (&od)[S], double vnext) {
-    os[S - 1] = fma(ks[S - 1][3], vnext, os[S - 1]);
-#pragma unroll
-    for (int s = 0; s < S; ++s) od[s] = fma(kd[s][2], lds_ld(xta[s]), od[s]);
+  auto kfin = [&](double (&os)[NR], double vnext) {
+    os[0] = fma(ks[3], vnext, os[0]);
+    os[1] = fma(kd[2], lds_ld(xta), os[1]);
   };
-  // per-lane partial K'y of the tau columns from the DCM rows' values
-  auto tau_parts = [&](const double (&vd)[S]) {
+  // per-lane partial K'y of the tau columns from the DCM row's value
+  auto tau_parts = [&](double vd) {
     if (J == 1) {
-      double a = kd[0][2] * vd[0];
-#pragma unroll
-      for (int s = 1; s < S; ++s) a = fma(kd[s][2], vd[s], a);
-      TP[tid] = a;
+      TP[tid] = kd[2] * vd;
     } else {
-      for (int j = 0; j < J; ++j) {
-        double a = 0.0;
-#pragma unroll
-        for (int s = 0; s < S; ++s) a = fma(jt[s] == j ? kd[s][2] : 0.0, vd[s], a);
-        TP[j * B + tid] = a;
-      }
+      for (int j = 0; j < J; ++j) TP[j * B + tid] = (jt == j ? kd[2] : 0.0) * vd;
     }
   };
   // wave 0: lane j < J gets the sum over all lanes of TP[j][.] (fixed order; uniform per column)
@@ -328,19 +369,17 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
   if (o.power_iters > 0) {
     const int P = o.power_iters;
     const double v0 = 1.0 / sqrt((double)n);
-    double vc[S][3];
+    double vc[NC];
 #pragma unroll
-    for (int s = 0; s < S; ++s)
-#pragma unroll
-      for (int v = 0; v < 3; ++v) vc[s][v] = val[s] ? v0 : 0.0;
+    for (int v = 0; v < NC; ++v) vc[v] = val ? v0 : 0.0;
     double vtau = (wid == 0 && lane < J) ? v0 : 0.0;
     double nv[2] = {0.0, 0.0};
-    double ws[S], wd[S];
+    double wr[NR];
 #pragma unroll
-    for (int s = 0; s < S; ++s) ws[s] = wd[s] = 0.0;
+    for (int r = 0; r < NR; ++r) wr[r] = 0.0;
     for (int pi = 0; pi <= P; ++pi) {
       if (pi > 0) {
-        ktr(ws, wd, YS[tid], vc);
+        ktr(wr, YS[tid], vc);
         if (wid == 0) {
           const double kt = tau_kt();
           vtau = lane < J ? kt : 0.0;
@@ -349,20 +388,18 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
       if (pi >= P - 1) {
         double a = vtau * vtau;
 #pragma unroll
-        for (int s = 0; s < S; ++s)
-#pragma unroll
-          for (int v = 0; v < 3; ++v) a = fma(vc[s][v], vc[s][v], a);
+        for (int v = 0; v < NC; ++v) a = fma(vc[v], vc[v], a);
         nv[pi - (P - 1)] = a;
       }
       if (pi == P) break;
-      XE[tid] = vc[0][2];
+      XE[tid] = vc[2];
       if (wid == 0 && lane < J) XT[lane] = vtau;
       __syncthreads();
-      kown(vc, ws, wd);
-      kfin(ws, wd, XE[tid + 1]);
-      YS[tid + 1] = ws[S - 1];
+      kown(vc, wr);
+      kfin(wr, XE[tid + 1]);
+      YS[tid + 1] = wr[0];
       if (ilane) YS[0] = sp[4] * XE[0];
-      tau_parts(wd);
+      tau_parts(wr[1]);
       __syncthreads();
     }
     block_sum<B, 2>(nv, red);
@@ -373,9 +410,9 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
     __syncthreads();
   }
   if (o.warm) {  // y images of the starting point
-    YS[tid + 1] = ys[S - 1];
+    YS[tid + 1] = y[0];
     if (ilane) YS[0] = sp[0];
-    if (J > 0) tau_parts(yd);
+    if (J > 0) tau_parts(y[1]);
     __syncthreads();
   }
   eta = uniform(eta);
@@ -427,7 +464,7 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
     const double cb = readlane_f64(hw, kin - kbase), ca = 1.0 - cb;
     mv0 = mv1 = mv2 = mv3 = 0.0;
     // ---------------- primal half-step (reflected Halpern, rho = 1)
-    double kxs[S], kxd[S];  // own-column part of K x-bar for the dual half-step
+    double kx[NR];  // own-column part of K x-bar for the dual half-step
     {
       double ta0 = 0.0, ta1 = 0.0;
       if constexpr (W0) {
@@ -437,27 +474,23 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
           if (r + 1 < NW) ta1 += TP[(r + 1) * kWave + lane];
         }
       }
-      double kty[S][3], xb[S][3];
-      ktr(ys, yd, YS[tid], kty);
+      double kty[NC], xb[NC];
+      ktr(y, YS[tid], kty);
 #pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const double cv[3] = {cch[s], cdi[s], 0.0};
-        const double lv[3] = {0.0, 0.0, loe[s]};
-#pragma unroll
-        for (int v = 0; v < 3; ++v) {  // branch-free: padding steps have c = lo = hi = 0 and stay at 0
-          const double p1 = vmin(vmax(fma(-tau, cv[v] - kty[s][v], x[s][v]), lv[v]), hi[s][v]);
-          xb[s][v] = fma(2.0, p1, -x[s][v]);
-          if (CHECK) {
-            const double d = x[s][v] - p1, da = p1 - xa[s][v];
-            mv0 += d * d;
-            mv1 += da * da;
-            XP[(3 * s + v) * B + tid] = p1;
-          }
-          x[s][v] = fma(ca, xb[s][v], cb * xa[s][v]);
+      for (int v = 0; v < NC; ++v) {  // branch-free: padding steps have c = lo = hi = 0 and stay at 0
+        const double lo = v == 2 ? loe : 0.0;
+        const double p1 = vmin(vmax(fma(-tau, cof(v) - kty[v], x[v]), lo), hib(v));
+        xb[v] = fma(2.0, p1, -x[v]);
+        if (CHECK) {
+          const double d = x[v] - p1, da = p1 - xa[v];
+          mv0 += d * d;
+          mv1 += da * da;
+          XP[v * B + tid] = p1;
         }
+        x[v] = fma(ca, xb[v], cb * xa[v]);
       }
-      XE[tid] = xb[0][2];
-      kown(xb, kxs, kxd);
+      XE[tid] = xb[2];
+      kown(xb, kx);
       if constexpr (W0) {
         tau_update(uniform(wave_sum_dpp(ta0 + ta1)), ca, cb, chk_tag);
       } else {
@@ -467,23 +500,21 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
     lds_barrier();
     // ---------------- dual half-step
     {
-      kfin(kxs, kxd, XE[tid + 1]);
+      kfin(kx, XE[tid + 1]);
 #pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const double p1 = fma(sigma, qsr[s] - kxs[s], ys[s]);             // SOE row: equality
-        const double p2 = vmax(fma(sigma, qd[s] - kxd[s], yd[s]), 0.0);  // DCM row: >=, its dual stays >= 0
+      for (int r = 0; r < NR; ++r) {  // row 0 (SOE) is an equality; DCM / ICE rows are >=: duals stay >= 0
+        double p1 = fma(sigma, rhs(r) - kx[r], y[r]);
+        if (r > 0) p1 = vmax(p1, 0.0);
         if (CHECK) {
-          const double d = ys[s] - p1, da = p1 - yas[s], e = yd[s] - p2, ea = p2 - yad[s];
-          mv2 += d * d + e * e;
-          mv3 += da * da + ea * ea;
-          YP[(2 * s) * B + tid] = p1;
-          YP[(2 * s + 1) * B + tid] = p2;
+          const double d = y[r] - p1, da = p1 - ya[r];
+          mv2 += d * d;
+          mv3 += da * da;
+          YP[r * B + tid] = p1;
         }
-        ys[s] = fma(ca, fma(2.0, p1, -ys[s]), cb * yas[s]);
-        yd[s] = fma(ca, fma(2.0, p2, -yd[s]), cb * yad[s]);
+        y[r] = fma(ca, fma(2.0, p1, -y[r]), cb * ya[r]);
       }
-      YS[tid + 1] = ys[S - 1];
-      if (J > 0) tau_parts(yd);
+      YS[tid + 1] = y[0];
+      if (J > 0) tau_parts(y[1]);
       if (W0 || wid == 0) {  // init row (lane kInitLane): ene_0 = target
         if (ilane) {
           const double y0 = sp[0], ya0 = sp[1];
@@ -533,19 +564,16 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
     for (int u = 4; u < kNRed; ++u) acc[u] = 0.0;
     if (kkt) {
       // images of T(z_k) in XE / XT / YS / TP (rewritten from z after the check)
-      double xp[S][3], yps[S], ypd[S];
+      double xp[NC], yp[NR];
 #pragma unroll
-      for (int s = 0; s < S; ++s) {
+      for (int v = 0; v < NC; ++v) xp[v] = XP[v * B + tid];
 #pragma unroll
-        for (int v = 0; v < 3; ++v) xp[s][v] = XP[(3 * s + v) * B + tid];
-        yps[s] = YP[(2 * s) * B + tid];
-        ypd[s] = YP[(2 * s + 1) * B + tid];
-      }
-      XE[tid] = xp[0][2];
-      YS[tid + 1] = yps[S - 1];
+      for (int r = 0; r < NR; ++r) yp[r] = YP[r * B + tid];
+      XE[tid] = xp[2];
+      YS[tid + 1] = yp[0];
       if (ilane) YS[0] = sp[2];
       if (tlane) XT[lane] = sp[5];
-      if (J > 0) tau_parts(ypd);
+      if (J > 0) tau_parts(yp[1]);
       lds_barrier();
       auto col_kkt = [&](int j, double kt, double cj, double loj, double hij, double xj) {
         const ColKkt r = col_kkt_fn(kt, cj, loj, hij, xj, dcv[opaque(j)]);
@@ -557,27 +585,24 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
         acc[4] += row_kkt_fn(kv, qi, drv[opaque(i)], ge);
         acc[7] += qi * yi;
       };
-      double kt[S][3];
-      ktr(yps, ypd, YS[tid], kt);
+      double kt[NC];
+      ktr(yp, YS[tid], kt);
+      if (val) {
 #pragma unroll
-      for (int s = 0; s < S; ++s)
-        if (val[s]) {
-          const int t = S * tid + s;
-          col_kkt(t, kt[s][0], cch[s], 0.0, hi[s][0], xp[s][0]);
-          col_kkt(T + t, kt[s][1], cdi[s], 0.0, hi[s][1], xp[s][1]);
-          col_kkt(2 * T + t, kt[s][2], 0.0, loe[s], hi[s][2], xp[s][2]);
-        }
+        for (int v = 0; v < NC; ++v) col_kkt(col(v), kt[v], cof(v), v == 2 ? loe : 0.0, hib(v), xp[v]);
+      }
       if (wid == 0 && J > 0) {
         const double ktt = tau_kt();
         if (tlane) col_kkt(3 * T + lane, ktt, sp[2], sp[3], sp[4], sp[5]);
       }
-      double kxs[S], kxd[S];
-      kown(xp, kxs, kxd);
-      kfin(kxs, kxd, XE[tid + 1]);
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        if (val[s]) row_kkt(S * tid + s + 1, kxs[s], qsr[s], yps[s], false);
-        if (drow[s] >= 0) row_kkt(drow[s], kxd[s], qd[s], ypd[s], true);
+      double kv[NR];
+      kown(xp, kv);
+      kfin(kv, XE[tid + 1]);
+      if (val) row_kkt(t + 1, kv[0], q[0], yp[0], false);
+      if (drow >= 0) row_kkt(drow, kv[1], q[1], yp[1], true);
+      if (ICE && val) {
+        row_kkt(ra, kv[2], rhs(2), yp[2], true);
+        row_kkt(rb, kv[3], rhs(3), yp[3], true);
       }
       if (ilane) row_kkt(0, sp[4] * XE[0], sp[3], sp[2], false);
     }
@@ -618,12 +643,9 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
       tau = uniform(eta / pw);
       sigma = uniform(eta * pw);
 #pragma unroll
-      for (int s = 0; s < S; ++s) {
+      for (int v = 0; v < NC; ++v) x[v] = xa[v] = XP[v * B + tid];
 #pragma unroll
-        for (int v = 0; v < 3; ++v) x[s][v] = xa[s][v] = XP[(3 * s + v) * B + tid];
-        ys[s] = yas[s] = YP[(2 * s) * B + tid];
-        yd[s] = yad[s] = YP[(2 * s + 1) * B + tid];
-      }
+      for (int rr = 0; rr < NR; ++rr) y[rr] = ya[rr] = YP[rr * B + tid];
       if (ilane) sp[0] = sp[1] = sp[2];
       if (tlane) sp[0] = sp[1] = sp[5];
       kin = 0;
@@ -635,22 +657,23 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
       rprev = r;
     }
     if (restart || kkt) {  // the y images must hold z again (after a restart z = T(z_k))
-      YS[tid + 1] = ys[S - 1];
+      YS[tid + 1] = y[0];
       if (ilane) YS[0] = sp[0];
-      if (J > 0) tau_parts(yd);
+      if (J > 0) tau_parts(y[1]);
     }
     lds_barrier();
   }
   // outputs: the last check's T(z_k), unscaled
+  if (val) {
 #pragma unroll
-  for (int s = 0; s < S; ++s)
-    if (val[s]) {
-      const int t = S * tid + s;
-#pragma unroll
-      for (int v = 0; v < 3; ++v) xo_g[v * T + t] = XP[(3 * s + v) * B + tid] * dcv[v * T + t];
-      yo_g[t + 1] = YP[(2 * s) * B + tid] * drv[t + 1];
-      if (drow[s] >= 0) yo_g[drow[s]] = YP[(2 * s + 1) * B + tid] * drv[drow[s]];
+    for (int v = 0; v < NC; ++v) xo_g[col(v)] = XP[v * B + tid] * dcv[col(v)];
+    yo_g[t + 1] = YP[tid] * drv[t + 1];
+    if (drow >= 0) yo_g[drow] = YP[B + tid] * drv[drow];
+    if (ICE) {
+      yo_g[ra] = YP[2 * B + tid] * drv[ra];
+      yo_g[rb] = YP[3 * B + tid] * drv[rb];
     }
+  }
   if (tlane) xo_g[3 * T + lane] = sp[5] * dcv[3 * T + lane];
   if (ilane) yo_g[0] = sp[2] * drv[0];
   if (tid == 0) {
@@ -660,16 +683,23 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
   }
 }
 
-}  // namespace
-
-hipError_t launch_pdhg_band(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, hipStream_t s) {
-  constexpr int B = kBandB, S = kBandS;
-  const size_t lds = band_lds_bytes(B, S);
-  auto kern = pdhg_band_kernel<B, S>;
+template <bool ICE>
+hipError_t launch_band_one(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, hipStream_t s,
+                           const int32_t* list, int nlist) {
+  constexpr int B = kBandB;
+  const size_t lds = band_lds_bytes(B, ICE);
+  auto kern = pdhg_band_kernel<B, ICE>;
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(kern, dim3(ch.count), dim3(B), lds, s, b, w, ch, o);
+  hipLaunchKernelGGL(kern, dim3(list ? nlist : ch.count), dim3(B), lds, s, b, w, ch, o, list);
   return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_pdhg_band(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, hipStream_t s, bool ice,
+                            const int32_t* list, int nlist) {
+  return ice ? launch_band_one<true>(b, w, ch, o, s, list, nlist) : launch_band_one<false>(b, w, ch, o, s, list, nlist);
 }
 
 }  // namespace dvh

@@ -86,7 +86,10 @@ hipError_t launch_pdhg_ell(const Batch& b, const Work& w, const Chunk& ch, const
                            int wx, int wy, hipStream_t s, int* variant_out, const int32_t* list, int nlist);
 // Battery-banded kernel (dvh_band.hip) over the whole chunk.  Windows whose CSR is not the battery + DCM
 // window shape come back with istats status -2 (kNeedsEll) and must be re-run by launch_pdhg_ell.
-hipError_t launch_pdhg_band(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, hipStream_t s);
+// ice: the variant with LP-relaxed ICE columns (elec, on) and rows; list (nlist entries): global window indices,
+// or null for the whole chunk.
+hipError_t launch_pdhg_band(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, hipStream_t s, bool ice,
+                            const int32_t* list, int nlist);
 size_t setup_lds_bytes(int max_n);
 // Power iteration for ||Kt||_2 of the listed windows (generic path; the ELL kernel does its own on chip).
 hipError_t launch_power(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, const int32_t* list, int nlist,

@@ -65,11 +65,30 @@ def test_config4_sample_matches_highs(gpu_solver):
     _check(lps, gpu_solver.solve(lps), "config4")
 
 
-def test_config5_generic_path(gpu_solver):
+def test_config5_band_ice_path(gpu_solver):
+    """Config 5 (battery + LP-relaxed ICE + DCM, 744-step windows) takes the ICE variant of the band kernel."""
     g = scenarios.config5([3], years=1)
     lps = _lps([g[0], g[6]])
     res = gpu_solver.solve(lps)
     _check(lps, res, "config5")
+    st = gpu_solver.kernel_stats()
+    assert st["band_windows"] == 2 and st["variant"] == 9000112, st
+
+
+def test_config5_band_ice_and_generic_kernels_agree():
+    """ICE band kernel vs the generic CSR kernel on config-5 windows: same algorithm, objectives within 1e-7."""
+    g = scenarios.config5([7], years=1)
+    lps = _lps([g[1], g[9]])
+    out = {}
+    with BatchSolver(0) as s:
+        for path, key in (("default", "band_windows"), ("generic", "generic_windows")):
+            s.set_kernel_path(path)
+            out[path] = s.solve(lps)
+            assert s.kernel_stats()[key] == 2, (path, s.kernel_stats())
+    for ra, rc in zip(out["default"], out["generic"]):
+        assert ra.status == rc.status == 0
+        assert abs(ra.obj - rc.obj) <= 1e-7 * abs(rc.obj)
+        assert abs(ra.iters - rc.iters) <= 64
 
 
 def test_band_ell_and_generic_kernels_agree():
