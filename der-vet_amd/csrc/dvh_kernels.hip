@@ -16,6 +16,7 @@
 #include "dvh_device.h"
 
 #include <math.h>
+#include <stdlib.h>
 
 #include <type_traits>
 
@@ -800,9 +801,11 @@ __host__ __device__ inline size_t ell_lds_bytes(int n, int m, int B, int XS, int
 }
 
 
-template <int B, int XS, int YS, int WX, int WY, int KR>
-__global__ __launch_bounds__(B) void pdhg_ell_kernel(const Batch b, const Work w, const Chunk ch, const Opts o,
-                                                     const int32_t* list) {
+// WPE: minimum waves per SIMD the register allocation must allow (the small-window variants run several
+// single- or two-wave workgroups per CU and need the occupancy; the large ones are sized by B alone).
+template <int B, int XS, int YS, int WX, int WY, int KR, int WPE = 1>
+__global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(WPE))) void pdhg_ell_kernel(
+    const Batch b, const Work w, const Chunk ch, const Opts o, const int32_t* list) {
   constexpr int NW = B / kWave;
   constexpr int RX = XS * B, RY = YS * B;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1556,12 +1559,12 @@ hipError_t dispatch_xy(int xs, int ys, const Batch& b, const Work& w, const Chun
   return hipErrorInvalidValue;
 }
 
-template <int B, int XS, int YS, int WX, int WY, int KR>
+template <int B, int XS, int YS, int WX, int WY, int KR, int WPE = 1>
 hipError_t launch_ell_one(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n, int max_m,
                           hipStream_t s, const int32_t* list, int nlist) {
   const size_t lds = ell_lds_bytes(max_n, max_m, B, XS, YS, WX, WY, KR);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  auto kern = pdhg_ell_kernel<B, XS, YS, WX, WY, KR>;
+  auto kern = pdhg_ell_kernel<B, XS, YS, WX, WY, KR, WPE>;
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3(list ? nlist : ch.count), dim3(B), lds, s, b, w, ch, o, list);
@@ -1638,8 +1641,37 @@ hipError_t launch_pdhg(const Batch& b, const Work& w, const Chunk& ch, const Opt
               : dispatch_xy<false>(xs, ys, b, w, ch, o, lds, s, list, nlist);
 }
 
+// Small windows (the daily market-service window: T = 24, n = 168, m <= 217, K^T rows <= 6, K rows <= 8): one
+// single-wave workgroup per window, so the loop's barriers are one-wave barriers and several windows share a
+// CU (a 512-thread workgroup per window would leave most lanes without a column or a row).
+static int small_variant() {  // DVH_SMALL=-1: off (A/B against the 512-thread kernels); 0..4: force a variant
+  static const int v = getenv("DVH_SMALL") ? atoi(getenv("DVH_SMALL")) : 99;
+  return v;
+}
+
+hipError_t small_dispatch(int max_n, int max_m, int wx, int wy, const Batch& b, const Work& w, const Chunk& ch,
+                          const Opts& o, hipStream_t s, int* variant_out, const int32_t* list, int nlist) {
+  const int sv = small_variant();
+#define DVH_SMALL(V_, B_, X_, Y_, WX_, WY_, KR_, WPE_)                                                          \
+  if ((sv == 99 || sv == V_) && max_n <= X_ * B_ && max_m <= Y_ * B_ && wx <= WX_ && wy <= WY_) {             \
+    if (variant_out)                                                                                          \
+      *variant_out = (2000000 + 1000000 * KR_) + WX_ * 100000 + WY_ * 10000 + (B_ / 64) * 100 + X_ * 10 + Y_; \
+    return launch_ell_one<B_, X_, Y_, WX_, WY_, KR_, WPE_>(b, w, ch, o, max_n, max_m, s, list, nlist);       \
+  }
+  DVH_SMALL(0, 64, 3, 5, 6, 8, 3, 1)
+  DVH_SMALL(1, 64, 3, 5, 6, 8, 0, 2)
+  DVH_SMALL(2, 128, 2, 3, 6, 8, 3, 2)
+  DVH_SMALL(3, 128, 2, 3, 6, 8, 1, 3)
+  DVH_SMALL(4, 128, 2, 3, 6, 8, 0, 4)
+#undef DVH_SMALL
+  return hipErrorInvalidValue;
+}
+static bool small_enabled() { return small_variant() >= 0; }
+
 hipError_t launch_pdhg_ell(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n, int max_m,
                            int wx, int wy, hipStream_t s, int* variant_out, const int32_t* list, int nlist) {
+  if (max_n <= 256 && max_m <= 384 && wx <= 6 && wy <= 8 && small_enabled())
+    return small_dispatch(max_n, max_m, wx, wy, b, w, ch, o, s, variant_out, list, nlist);
   if (wx <= 2 && wy <= 4) return ell_dispatch_xy<2, 4>(max_n, max_m, b, w, ch, o, s, variant_out, list, nlist);
   if (wx <= 4 && wy <= 8) return ell_dispatch_xy<4, 8>(max_n, max_m, b, w, ch, o, s, variant_out, list, nlist);
   return hipErrorInvalidValue;

@@ -216,6 +216,144 @@ def battery_group(T, dt, base_load, bat, retail_price=None, da_price=None, deman
                        q=q, l=l, u=u, terms=terms, tags=list(tags) if tags is not None else [None] * G)
 
 
+def _assemble(G, m, blocks):
+    """CSR pattern + per-window values from COO blocks (rows [k], cols [k], vals [G, k]): entries sorted by
+    (row, col), one pattern shared by the G windows."""
+    rows = np.concatenate([np.asarray(r, np.int64) for r, _, _ in blocks])
+    cols = np.concatenate([np.asarray(c, np.int64) for _, c, _ in blocks])
+    vals = np.concatenate([np.broadcast_to(np.asarray(v, np.float64), (G, len(r))) for r, _, v in blocks], axis=1)
+    order = np.lexsort((cols, rows))
+    indptr = np.zeros(m + 1, np.int64)
+    np.cumsum(np.bincount(rows, minlength=m), out=indptr[1:])
+    return indptr.astype(np.int32), cols[order].astype(np.int32), np.ascontiguousarray(vals[:, order])
+
+
+def market_group(T, dt, bat, da_price, fr, base=None, ene_min=None, ene_max=None, binary_relax=False, name="es",
+                 tags=None):
+    """G windows of battery dispatch with the DA energy term and frequency-regulation reservations (storagevet
+    MarketServiceUpAndDown / FrequencyRegulation + EnergyStorage).  Formulation and
+    row order as oracle/window_lp.py (pinned to the Usecase 3 goldens: with binaries the restatement reproduces
+    every golden daily objective; ``binary_relax`` is the opt-in LP relaxation of binary = 1 windows):
+
+      x = [ch, dis, ene, up_ch, up_dis, down_ch, down_dis]  (T each)
+      row 0 ene_0 = target; SOE rows with the energy option dt (rte uch - udis), uch = eou up_ch - eod down_ch,
+      udis = eou up_dis - eod down_dis; final row back to target; [CombinedMarket: up = down]
+      >= rows per block of T: P_ch - ch - down_ch, P_dis - dis - up_dis, ch - up_ch, dis - down_dis,
+      (1 - rte) uch + 2 udis, [regu_max / regu_min], [regd_max / regd_min], [1 - ch / P_ch - dis / P_dis]
+      objective keys 'DA', 'regup_prof', 'regdown_prof', 'fr_energy_settlement', '<es> fixed_om', '<es> var_om'
+
+    da_price [G, T]; base [G, T] = load - fixed generation (kW) of the DA net term (zeros: incl_site_load = 0);
+    fr: dict eou, eod (scalars), regu_price, regd_price, fr_price [G, T], optional regu_max, regu_min, regd_max,
+    regd_min [G, T], combined (bool)."""
+    da_price = np.atleast_2d(np.asarray(da_price, np.float64))
+    G = da_price.shape[0]
+    base = np.zeros((G, T)) if base is None else _col(base, G, T)
+    E = _col(bat["E"], G)
+    pch, pdis = _col(bat["Pch"], G), _col(bat["Pdis"], G)
+    eta, sdr = _col(bat["rte"], G), _col(bat.get("sdr", 0.0), G) / 100.0
+    target = _col(bat.get("soc_target", 1.0), G) * E
+    eou, eod = float(fr["eou"]), float(fr["eod"])
+    combined = bool(fr.get("combined", False))
+    ich, idis, iene, iuc, iud, idc, idd = (k * T for k in range(7))
+    n = 7 * T
+    t = np.arange(T)
+    tt = t[:-1]
+    one = np.ones((G, 1))
+    col = lambda v: np.asarray(v, np.float64).reshape(G, 1) * np.ones((1, len(tt)))
+    blocks = [([0], [iene], np.ones((G, 1)))]
+    # SOE rows 1..T-1 (step t = row - 1): ene_{t+1} - (1 - dt sdr) ene_t - dt eta ch_t + dt dis_t
+    #   - dt eta eou up_ch_t + dt eta eod down_ch_t + dt eou up_dis_t - dt eod down_dis_t = 0
+    r = 1 + tt
+    for c0_, v in ((iene + tt + 1, one), (iene + tt, -(1.0 - dt * sdr)[:, None]), (ich + tt, -dt * eta[:, None]),
+                   (idis + tt, dt * one), (iuc + tt, -dt * eou * eta[:, None]), (idc + tt, dt * eod * eta[:, None]),
+                   (iud + tt, dt * eou * one), (idd + tt, -dt * eod * one)):
+        blocks.append((r, c0_, v * np.ones((1, len(tt)))))
+    # final row: (1 - dt sdr) ene + dt eta ch - dt dis + dt (eta uch - udis) = target   (step T-1)
+    k = T - 1
+    for c0_, v in ((iene + k, 1.0 - dt * sdr), (ich + k, dt * eta), (idis + k, -dt * np.ones(G)),
+                   (iuc + k, dt * eou * eta), (idc + k, -dt * eod * eta), (iud + k, -dt * eou * np.ones(G)),
+                   (idd + k, dt * eod * np.ones(G))):
+        blocks.append(([T], [c0_], np.asarray(v).reshape(G, 1)))
+    m = T + 1
+    q_eq = [target[:, None], np.zeros((G, T - 1)), target[:, None]]
+    if combined:
+        for c0_, v in ((iuc, 1.0), (iud, 1.0), (idc, -1.0), (idd, -1.0)):
+            blocks.append((m + t, c0_ + t, np.full((G, T), v)))
+        q_eq.append(np.zeros((G, T)))
+        m += T
+    m_eq = m
+    q_ge = []
+
+    def ge(entries, rhs):
+        nonlocal m
+        for c0_, v in entries:
+            blocks.append((m + t, c0_ + t, np.broadcast_to(np.asarray(v, np.float64), (G, T))))
+        q_ge.append(np.broadcast_to(np.asarray(rhs, np.float64), (G, T)))
+        m += T
+
+    ge([(ich, -1.0), (idc, -1.0)], -pch[:, None])
+    ge([(idis, -1.0), (iud, -1.0)], -pdis[:, None])
+    ge([(ich, 1.0), (iuc, -1.0)], 0.0)
+    ge([(idis, 1.0), (idd, -1.0)], 0.0)
+    ge([(iuc, ((1.0 - eta) * eou)[:, None]), (idc, (-(1.0 - eta) * eod)[:, None]), (iud, 2.0 * eou),
+        (idd, -2.0 * eod)], 0.0)
+    if fr.get("regu_max") is not None:
+        ge([(iuc, -1.0), (iud, -1.0)], -_col(fr["regu_max"], G, T))
+        ge([(iuc, 1.0), (iud, 1.0)], _col(fr["regu_min"], G, T))
+    if fr.get("regd_max") is not None:
+        ge([(idc, -1.0), (idd, -1.0)], -_col(fr["regd_max"], G, T))
+        ge([(idc, 1.0), (idd, 1.0)], _col(fr["regd_min"], G, T))
+    if binary_relax:
+        ge([(ich, (-1.0 / pch)[:, None]), (idis, (-1.0 / pdis)[:, None])], -1.0)
+    indptr, indices, data = _assemble(G, m, blocks)
+    q = np.concatenate(q_eq + q_ge, axis=1)
+
+    l = np.zeros((G, n))
+    u = np.full((G, n), np.inf)
+    u[:, ich:ich + T] = pch[:, None]
+    u[:, idis:idis + T] = pdis[:, None]
+    lo = (_col(bat.get("llsoc", 0.0), G) * E)[:, None] * np.ones((1, T))
+    hi = (_col(bat.get("ulsoc", 1.0), G) * E)[:, None] * np.ones((1, T))
+    if ene_min is not None:
+        lo = np.maximum(lo, _col(ene_min, G, T))
+    if ene_max is not None:
+        hi = np.minimum(hi, _col(ene_max, G, T))
+    l[:, iene:iene + T] = lo
+    u[:, iene:iene + T] = hi
+
+    terms = {}
+    coef = np.zeros((G, n))
+    coef[:, ich:ich + T] = da_price * dt
+    coef[:, idis:idis + T] = -da_price * dt
+    terms["DA"] = (coef, (da_price * dt * base).sum(axis=1))
+    pu, pd_, pe = (_col(fr[k], G, T) for k in ("regu_price", "regd_price", "fr_price"))
+    coef = np.zeros((G, n))
+    coef[:, iuc:iuc + T] = -pu
+    coef[:, iud:iud + T] = -pu
+    terms["regup_prof"] = (coef, np.zeros(G))
+    coef = np.zeros((G, n))
+    coef[:, idc:idc + T] = -pd_
+    coef[:, idd:idd + T] = -pd_
+    terms["regdown_prof"] = (coef, np.zeros(G))
+    coef = np.zeros((G, n))
+    coef[:, iuc:iuc + T] = -pe * dt * eou
+    coef[:, iud:iud + T] = -pe * dt * eou
+    coef[:, idc:idc + T] = pe * dt * eod
+    coef[:, idd:idd + T] = pe * dt * eod
+    terms["fr_energy_settlement"] = (coef, np.zeros(G))
+    terms[f"{name} fixed_om"] = (np.zeros((G, n)), _col(bat.get("fixedOM", 0.0), G) * pdis)
+    coef = np.zeros((G, n))
+    coef[:, idis:idis + T] = (_col(bat.get("OMexpenses", 0.0), G) / 1000.0 * dt)[:, None]
+    terms[f"{name} var_om"] = (coef, np.zeros(G))
+    c = np.zeros((G, n))
+    c0 = np.zeros(G)
+    for coef, const in terms.values():
+        c += coef
+        c0 += const
+    return WindowGroup(T=T, J=0, m_eq=m_eq, indptr=indptr, indices=indices, data=data, c=c, c0=c0, q=q, l=l, u=u,
+                       terms=terms, tags=list(tags) if tags is not None else [None] * G)
+
+
 def group_window_lps(g):
     """Per-window solver.WindowLP objects of a group (small batches, tests, the drop-in)."""
     from ..solver import WindowLP

@@ -199,3 +199,34 @@ def config5(scenarios, years=20, start_year=2017):
                                     demand_price_override=P["demand"], price_scale=P["price_scale"],
                                     ene_min=emin, ice=ice, tags_prefix=scen)
     return groups
+
+
+def market_days(signals, params, relax=True, days=None, name="es"):
+    """Daily DA + frequency-regulation windows (Usecase 3 style) as one
+    market_group.  signals: dict of [N] arrays da_price, regu_price, regd_price, fr_price, agg_emin, agg_emax,
+    pv_gen (fixed PV, curtail = 0), regu_max/min, regd_max/min; params: model parameters (Tag -> Key -> value
+    strings, as the reference's model-parameter CSV).  Windows are consecutive blocks of n steps
+    (``optimization_levels`` for an integer n); ``relax`` applies the opt-in LP relaxation to binary = 1."""
+    from .builder import market_group
+    sc, b, fr = params["Scenario"], params["Battery"], params["FR"]
+    n, dt = int(sc["n"]), float(sc["dt"])
+    flag = lambda v: str(v).strip() not in ("0", "0.0", "", "no")
+    N = len(signals["da_price"]) // n * n
+    sel = np.arange(N).reshape(-1, n)
+    if days is not None:
+        sel = sel[np.asarray(days)]
+    blk = lambda k: np.asarray(signals[k], np.float64)[sel]
+    bat = dict(E=float(b["ene_max_rated"]), Pch=float(b["ch_max_rated"]), Pdis=float(b["dis_max_rated"]),
+               rte=float(b["rte"]) / 100.0, sdr=float(b["sdr"]), soc_target=float(b["soc_target"]) / 100.0,
+               ulsoc=float(b["ulsoc"]) / 100.0, llsoc=float(b["llsoc"]) / 100.0, fixedOM=float(b["fixedOM"]),
+               OMexpenses=float(b["OMexpenses"]))
+    frd = dict(eou=float(fr["eou"]), eod=float(fr["eod"]), regu_price=blk("regu_price"),
+               regd_price=blk("regd_price"), fr_price=blk("fr_price"), combined=flag(fr.get("CombinedMarket", 0)))
+    if flag(fr.get("u_ts_constraints", 0)):
+        frd["regu_max"], frd["regu_min"] = blk("regu_max"), blk("regu_min")
+    if flag(fr.get("d_ts_constraints", 0)):
+        frd["regd_max"], frd["regd_min"] = blk("regd_max"), blk("regd_min")
+    base = -blk("pv_gen") if "pv_gen" in signals else None
+    return market_group(n, dt, bat, blk("da_price"), frd, base=base, ene_min=blk("agg_emin"),
+                        ene_max=blk("agg_emax"), binary_relax=relax and flag(sc.get("binary", 0)), name=name,
+                        tags=[("day", int(r[0]) // n) for r in sel])

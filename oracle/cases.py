@@ -66,3 +66,44 @@ def case_windows(name):
             index=sel,
         ))
     return wins, arr, meta, price
+
+
+def load_market():
+    arr = dict(np.load(os.path.join(GOLDEN, "uc3_market.npz")))
+    with open(os.path.join(GOLDEN, "uc3_market.json")) as f:
+        meta = json.load(f)
+    return arr, meta
+
+
+def market_windows(name, relax=True):
+    """Daily DA + FR window inputs (oracle.window_lp.build) of a Usecase 3 planned golden case (n = 24 steps:
+    storagevet ``optimization_levels`` for an integer n are consecutive blocks of n steps), with the golden
+    dispatch of each window as a solution vector in the build() layout (x_golden) and the golden objective row.
+    Load is not included (incl_site_load = 0); fixed PV generation (curtail = 0) enters the DA net term."""
+    arr, meta = load_market()
+    m = meta[name]
+    p = m["params"]
+    key = lambda k: arr[f"{name}__{k}"]
+    n = int(p["Scenario"]["n"])
+    dt = float(p["Scenario"]["dt"])
+    fr = p["FR"]
+    bat = battery_from_params(p)
+    N = len(key("da_price"))
+    wins = []
+    for d in range(N // n):
+        s = slice(d * n, d * n + n)
+        w = dict(T=n, dt=dt, load=np.zeros(n), gen=key("pv_gen")[s], retail_price=None, da_price=key("da_price")[s],
+                 demand=[], ene_min=key("agg_emin")[s], ene_max=key("agg_emax")[s], bat=bat,
+                 fr=dict(eou=float(fr["eou"]), eod=float(fr["eod"]), regu_price=key("regu_price")[s],
+                         regd_price=key("regd_price")[s], fr_price=key("fr_price")[s],
+                         combined=fr.get("CombinedMarket", "0") not in ("0", "0.0")),
+                 binary_relax=relax and p["Scenario"].get("binary", "0") not in ("0", "0.0"),
+                 golden_objective=key("golden_objective")[d], index=np.arange(d * n, d * n + n))
+        if fr.get("u_ts_constraints", "0") not in ("0", "0.0"):
+            w["fr"]["regu_max"], w["fr"]["regu_min"] = key("regu_max")[s], key("regu_min")[s]
+        if fr.get("d_ts_constraints", "0") not in ("0", "0.0"):
+            w["fr"]["regd_max"], w["fr"]["regd_min"] = key("regd_max")[s], key("regd_min")[s]
+        w["x_golden"] = np.concatenate([key(k)[s] for k in ("golden_ch", "golden_dis", "golden_ene", "golden_up_ch",
+                                                            "golden_up_dis", "golden_down_ch", "golden_down_dis")])
+        wins.append(w)
+    return wins, m["objective_keys"]

@@ -14,8 +14,23 @@ DER / value-stream set:
     ene_0 = target;  ene_{t+1} = ene_t + dt (eta ch_t - dis_t) - dt sdr/100 ene_t;  final step reaches target
     max(llsoc E, a_min_t) <= ene_t <= min(ulsoc E, a_max_t);  0 <= ch <= P_ch;  0 <= dis <= P_dis
   optional (unpinned): curtailable PV 0 <= pv_t <= pv_max_t; LP-relaxed ICE (elec_t, on_t in [0,1]).
+  market services (storagevet MarketServiceUpAndDown / FrequencyRegulation, absent
+  here -- restated from the Usecase 3 goldens, which pin every formula below to 1e-11 at dt = 1):
+    reservation variables up_ch, up_dis, down_ch, down_dis >= 0 ('Regulation Up/Down (Charging/Discharging)')
+    charge option uch = eou up_ch - eod down_ch, discharge option udis = eou up_dis - eod down_dis,
+    energy option uene = dt (rte uch - udis) enters the SOE recurrence:
+      ene_{t+1} = (1 - dt sdr) ene_t + dt rte (ch_t + uch_t) - dt (dis_t + udis_t)
+    ch_t + down_ch_t <= P_ch, dis_t + up_dis_t <= P_dis, up_ch_t <= ch_t, down_dis_t <= dis_t
+    option consistency uene_t <= dt (uch_t + udis_t), i.e. (1 - rte) uch_t + 2 udis_t >= 0: with it the MILP
+      restatement (binary on_c / on_d) reproduces the golden daily objectives to 1e-15 (tests/test_market_oracle.py)
+    optional u/d_ts limits: regu_min <= up_ch + up_dis <= regu_max (and down); CombinedMarket: up = down
+    regup_prof   = -sum p_regu (up_ch + up_dis)          regdown_prof = -sum p_regd (down_ch + down_dis)
+    fr_energy_settlement = sum p_fr dt (eod (down_ch + down_dis) - eou (up_ch + up_dis))
+  binary = 1 windows, opt-in LP relaxation: on_c + on_d <= 1 with ch <= P_ch on_c, dis <= P_dis on_d
+  (ch_min = dis_min = 0) projects to  ch / P_ch + dis / P_dis <= 1.
 
-Variable order: [ch(T), dis(T), ene(T), tau(J), pv(T)?, elec(T)?, on(T)?].  Rows: equalities then >= rows.
+Variable order: [ch(T), dis(T), ene(T), tau(J), pv(T)?, elec(T)?, on(T)?, up_ch, up_dis, down_ch, down_dis (T
+each)?].  Rows: equalities (init, recurrence, final, CombinedMarket) then >= rows (DCM, ICE, FR, relaxation).
 This per-window scipy.sparse restatement is deliberately independent of the product's vectorised
 batch builder (``der-vet_amd/dervet_hip/lp/builder.py``); tests compare the two.
 """
@@ -29,7 +44,10 @@ def build(win):
          T, dt, load (L_t, kW), gen (fixed generation G_t, kW), retail_price (or None), da_price (or None),
          demand: list of (d_j $/kW, bool mask length T), ene_min, ene_max (arrays or None),
          bat: dict(E, Pch, Pdis, rte, sdr, soc_target, ulsoc, llsoc, fixedOM, OMexpenses, hp, name),
-         pv_curtail_max (array or None), ice (dict or None).
+         pv_curtail_max (array or None), ice (dict or None),
+         fr (dict or None): eou, eod, regu_price, regd_price, fr_price [T]; optional regu_max, regu_min, regd_max,
+             regd_min [T] (u/d_ts_constraints), combined (bool),
+         binary_relax (bool): the LP relaxation row ch / P_ch + dis / P_dis <= 1.
     Returns dict(K csr, q, c, c0, l, u, m_eq, funcs{name: (coef, const)}, layout)."""
     T = int(win["T"])
     dt = float(win["dt"])
@@ -50,6 +68,11 @@ def build(win):
         off["elec"] = n
         off["on"] = n + T
         n += 2 * T
+    fr = win.get("fr")
+    if fr is not None:
+        for k in ("uc", "ud", "dc", "dd"):
+            off[k] = n
+            n += T
     hp = float(b.get("hp", 0.0))
     base = np.asarray(win["load"], float) - np.asarray(win.get("gen", np.zeros(T)), float) + hp
 
@@ -69,19 +92,36 @@ def build(win):
     r = 0
     # equality rows: ene_0 = target
     rows.append(r); cols.append(off["ene"]); vals.append(1.0); q.append(target); r += 1
-    # recurrence t = 0..T-2:  ene_{t+1} - (1 - dt sdr) ene_t - dt eta ch_t + dt dis_t = 0
+    # energy-option terms of step t's energy change: dt (eta uch_t - udis_t)
+    def opt_terms(t, sign):
+        if fr is None:
+            return [], []
+        eou, eod = float(fr["eou"]), float(fr["eod"])
+        return ([off["uc"] + t, off["dc"] + t, off["ud"] + t, off["dd"] + t],
+                [sign * dt * eta * eou, -sign * dt * eta * eod, -sign * dt * eou, sign * dt * eod])
+    # recurrence t = 0..T-2:  ene_{t+1} - (1 - dt sdr) ene_t - dt eta ch_t + dt dis_t - dt (eta uch_t - udis_t) = 0
     for t in range(T - 1):
-        rows += [r] * 4
-        cols += [off["ene"] + t + 1, off["ene"] + t, off["ch"] + t, off["dis"] + t]
-        vals += [1.0, -(1.0 - dt * sdr), -dt * eta, dt]
+        oc, ov = opt_terms(t, -1.0)
+        rows += [r] * (4 + len(oc))
+        cols += [off["ene"] + t + 1, off["ene"] + t, off["ch"] + t, off["dis"] + t] + oc
+        vals += [1.0, -(1.0 - dt * sdr), -dt * eta, dt] + ov
         q.append(0.0)
         r += 1
-    # final: (1 - dt sdr) ene_{T-1} + dt eta ch_{T-1} - dt dis_{T-1} = target
-    rows += [r] * 3
-    cols += [off["ene"] + T - 1, off["ch"] + T - 1, off["dis"] + T - 1]
-    vals += [1.0 - dt * sdr, dt * eta, -dt]
+    # final: (1 - dt sdr) ene_{T-1} + dt eta ch_{T-1} - dt dis_{T-1} + dt (eta uch - udis)_{T-1} = target
+    oc, ov = opt_terms(T - 1, 1.0)
+    rows += [r] * (3 + len(oc))
+    cols += [off["ene"] + T - 1, off["ch"] + T - 1, off["dis"] + T - 1] + oc
+    vals += [1.0 - dt * sdr, dt * eta, -dt] + ov
     q.append(target)
     r += 1
+    if fr is not None and fr.get("combined"):
+        # CombinedMarket: up_ch + up_dis - down_ch - down_dis = 0
+        for t in range(T):
+            rows += [r] * 4
+            cols += [off["uc"] + t, off["ud"] + t, off["dc"] + t, off["dd"] + t]
+            vals += [1.0, 1.0, -1.0, -1.0]
+            q.append(0.0)
+            r += 1
     m_eq = r
     # >= rows: tau_j - (ch - dis - pv - elec)_t >= base_t   for t in M_j
     for j, (d, mask) in enumerate(demand):
@@ -99,6 +139,32 @@ def build(win):
         for t in range(T):
             rows += [r, r]; cols += [off["on"] + t, off["elec"] + t]; vals += [cap, -1.0]; q.append(0.0); r += 1
             rows += [r, r]; cols += [off["elec"] + t, off["on"] + t]; vals += [1.0, -pmin]; q.append(0.0); r += 1
+    if fr is not None:
+        def ge_rows(entries, rhs):
+            nonlocal r
+            for t in range(T):
+                for k, v in entries:
+                    rows.append(r); cols.append(off[k] + t); vals.append(v)
+                q.append(float(rhs[t]))
+                r += 1
+        ge_rows([("ch", -1.0), ("dc", -1.0)], np.full(T, -pch))    # ch + down_ch <= P_ch
+        ge_rows([("dis", -1.0), ("ud", -1.0)], np.full(T, -pdis))  # dis + up_dis <= P_dis
+        ge_rows([("ch", 1.0), ("uc", -1.0)], np.zeros(T))          # up_ch <= ch
+        ge_rows([("dis", 1.0), ("dd", -1.0)], np.zeros(T))         # down_dis <= dis
+        eou, eod = float(fr["eou"]), float(fr["eod"])
+        ge_rows([("uc", (1.0 - eta) * eou), ("dc", -(1.0 - eta) * eod), ("ud", 2.0 * eou), ("dd", -2.0 * eod)],
+                np.zeros(T))                                       # (1 - rte) uch + 2 udis >= 0
+        if fr.get("regu_max") is not None:
+            ge_rows([("uc", -1.0), ("ud", -1.0)], -np.asarray(fr["regu_max"], float))
+            ge_rows([("uc", 1.0), ("ud", 1.0)], np.asarray(fr["regu_min"], float))
+        if fr.get("regd_max") is not None:
+            ge_rows([("dc", -1.0), ("dd", -1.0)], -np.asarray(fr["regd_max"], float))
+            ge_rows([("dc", 1.0), ("dd", 1.0)], np.asarray(fr["regd_min"], float))
+    if win.get("binary_relax"):
+        for t in range(T):  # -ch/P_ch - dis/P_dis >= -1
+            rows += [r, r]; cols += [off["ch"] + t, off["dis"] + t]; vals += [-1.0 / pch, -1.0 / pdis]
+            q.append(-1.0)
+            r += 1
     m = r
     K = sp.csr_matrix((vals, (rows, cols)), shape=(m, n))
     K.sum_duplicates()
@@ -141,6 +207,23 @@ def build(win):
         funcs["DCM"] = (coef, 0.0)
     if win.get("retail_price") is not None:
         funcs["retailETS"] = net_term(np.asarray(win["retail_price"], float))
+    if fr is not None:
+        eou, eod = float(fr["eou"]), float(fr["eod"])
+        pu, pd_, pe = (np.asarray(fr[k], float) for k in ("regu_price", "regd_price", "fr_price"))
+        coef = np.zeros(n)
+        coef[off["uc"]:off["uc"] + T] = -pu
+        coef[off["ud"]:off["ud"] + T] = -pu
+        funcs["regup_prof"] = (coef, 0.0)
+        coef = np.zeros(n)
+        coef[off["dc"]:off["dc"] + T] = -pd_
+        coef[off["dd"]:off["dd"] + T] = -pd_
+        funcs["regdown_prof"] = (coef, 0.0)
+        coef = np.zeros(n)
+        for k in ("uc", "ud"):
+            coef[off[k]:off[k] + T] = -pe * dt * eou
+        for k in ("dc", "dd"):
+            coef[off[k]:off[k] + T] = pe * dt * eod
+        funcs["fr_energy_settlement"] = (coef, 0.0)
     name = b.get("name", "es")
     funcs[f"{name} fixed_om"] = (np.zeros(n), float(b.get("fixedOM", 0.0)) * pdis)
     coef = np.zeros(n)
@@ -204,3 +287,33 @@ def primal_residual_rel(lp, x):
     bv = np.maximum(lp["l"] - x, 0) + np.maximum(x - lp["u"], 0)
     return (float(np.sqrt(r @ r + bv @ bv)) / (1.0 + float(np.linalg.norm(lp["q"]))),
             float(max(np.abs(r).max(initial=0), bv.max(initial=0))))
+
+
+def solve_highs_milp(win, gap=1e-10):
+    """The binary = 1 window as the reference solves it (GLPK_MI there, HiGHS MILP here): explicit on_c, on_d in
+    {0, 1} with ch <= P_ch on_c, dis <= P_dis on_d, on_c + on_d <= 1 (ch_min = dis_min = 0).  Returns the
+    objective (with c0) and the solution in the build() layout."""
+    from scipy.optimize import Bounds, LinearConstraint, milp
+    lp = build(dict(win, binary_relax=False))
+    K, q, m_eq, off = lp["K"], lp["q"], lp["m_eq"], lp["layout"]
+    n, T = K.shape[1], lp["T"]
+    N = n + 2 * T
+    A = sp.hstack([K, sp.csr_matrix((K.shape[0], 2 * T))]).tocsr()
+    t = np.arange(T)
+    b = win["bat"]
+    on_rows = sp.csr_matrix((np.concatenate([np.ones(T), np.full(T, -float(b["Pch"])), np.ones(T),
+                                             np.full(T, -float(b["Pdis"]))]),
+                             (np.concatenate([t, t, T + t, T + t]),
+                              np.concatenate([off["ch"] + t, n + t, off["dis"] + t, n + T + t]))), shape=(2 * T, N))
+    excl = sp.csr_matrix((np.ones(2 * T), (np.concatenate([t, t]), np.concatenate([n + t, n + T + t]))), shape=(T, N))
+    cons = [LinearConstraint(A[:m_eq], q[:m_eq], q[:m_eq]), LinearConstraint(on_rows, -np.inf, 0.0),
+            LinearConstraint(excl, -np.inf, 1.0)]
+    if K.shape[0] > m_eq:
+        cons.append(LinearConstraint(A[m_eq:], q[m_eq:], np.inf))
+    c = np.concatenate([lp["c"], np.zeros(2 * T)])
+    bounds = Bounds(np.concatenate([lp["l"], np.zeros(2 * T)]), np.concatenate([lp["u"], np.ones(2 * T)]))
+    res = milp(c, constraints=cons, bounds=bounds, integrality=np.concatenate([np.zeros(n), np.ones(2 * T)]),
+               options={"mip_rel_gap": gap})
+    if res.status != 0:
+        return dict(status=res.status, message=res.message)
+    return dict(status=0, obj=float(res.fun + lp["c0"]), x=res.x[:n], on=res.x[n:])

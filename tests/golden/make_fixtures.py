@@ -12,6 +12,8 @@ Sources (all paths relative to /root/reference):
   * test/test_validation_report_sept1/datasets/tariff_refernce_case_1.csv                        (tariff)
   * data/multi_der_hourly_timeseries.csv, data/hourly_timeseries.csv, data/tariff.csv              (bench inputs)
   * test/datasets/000-004-timeseries_5min_negprices.csv                                           (config-3 input)
+  * test/test_validation_report_sept1/Results/Usecase3/planned/step2/<case>/{timeseries_results,
+    objective_values}uc3.csv + Model_params/Usecase3/planned/*_Step2.csv        (DA + FR market windows)
 
 Usage:  python tests/golden/make_fixtures.py [/root/reference]
 """
@@ -193,7 +195,58 @@ def make_reliability_cases():
     print("wrote reliability cases", sorted(meta))
 
 
+# Market services: Usecase 3 planned, DA + frequency regulation, daily MILP windows.
+# name: (results dir, model params csv)
+MARKET_CASES = {
+    "es": ("Results/Usecase3/planned/step2/es", "Model_params/Usecase3/planned/Model_Parameters_Template_Usecase3_Planned_ES_Step2.csv"),
+    "es+pv": ("Results/Usecase3/planned/step2/es+pv",
+              "Model_params/Usecase3/planned/Model_Parameters_Template_Usecase3_Planned_ES+PV_Step2.csv"),
+    "es+pv+dg": ("Results/Usecase3/planned/step2/es+pv+dg",
+                 "Model_params/Usecase3/planned/Model_Parameters_Template_Usecase3_Planned_ES+PV+DG_Step2.csv"),
+}
+MARKET_COLS = {
+    "da_price": "DA Price Signal ($/kWh)", "fr_price": "FR Energy Settlement Price Signal ($/kWh)",
+    "regu_price": "Regulation Up Price Signal ($/kW)", "regd_price": "Regulation Down Price Signal ($/kW)",
+    "regu_max": "FR Reg Up Max (kW)", "regu_min": "FR Reg Up Min (kW)", "regd_max": "FR Reg Down Max (kW)",
+    "regd_min": "FR Reg Down Min (kW)", "agg_emin": "Aggregate Energy Min (kWh)",
+    "agg_emax": "Aggregate Energy Max (kWh)",
+    "golden_ch": "BATTERY: es Charge (kW)", "golden_dis": "BATTERY: es Discharge (kW)",
+    "golden_ene": "BATTERY: es State of Energy (kWh)", "golden_up_ch": "Regulation Up (Charging) (kW)",
+    "golden_up_dis": "Regulation Up (Discharging) (kW)", "golden_down_ch": "Regulation Down (Charging) (kW)",
+    "golden_down_dis": "Regulation Down (Discharging) (kW)",
+}
+
+
+def make_market_cases():
+    """Inputs (price / limit signals as the results CSV echoes them), golden dispatch and the golden per-day
+    objective rows of the Usecase 3 planned DA + FR runs."""
+    arrays, meta = {}, {}
+    for name, (resdir, mp) in MARKET_CASES.items():
+        _, ts = read_csv_cols(os.path.join(VR, resdir, "timeseries_resultsuc3.csv"))
+        _, ob = read_csv_cols(os.path.join(VR, resdir, "objective_valuesuc3.csv"))
+        params = read_params(os.path.join(VR, mp))
+        for key, col in MARKET_COLS.items():
+            arrays[f"{name}__{key}"] = fcol(ts, col)
+        pv = [k for k in ts if k.startswith("PV: ") and k.endswith("Generation (kW)")]
+        arrays[f"{name}__pv_gen"] = np.sum([fcol(ts, k) for k in pv], axis=0) if pv else np.zeros(len(ts[MARKET_COLS["da_price"]]))
+        keys = [k for k in ob if k != ""]
+        arrays[f"{name}__golden_objective"] = np.stack([fcol(ob, k) for k in keys], axis=1)
+        meta[name] = {"source_results": os.path.join("test/test_validation_report_sept1", resdir),
+                      "objective_keys": keys, "active_tags": sorted(params.keys()),
+                      "params": {t: params[t] for t in ("Scenario", "Battery", "PV", "FR", "DA", "User") if t in params}}
+    np.savez_compressed(os.path.join(HERE, "uc3_market.npz"), **arrays)
+    with open(os.path.join(HERE, "uc3_market.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+    print("wrote market cases", sorted(meta))
+
+
 if __name__ == "__main__":
-    make_golden_cases()
-    make_bench_data()
-    make_reliability_cases()
+    what = sys.argv[2:] or ["golden", "bench", "reliability", "market"]
+    if "golden" in what:
+        make_golden_cases()
+    if "bench" in what:
+        make_bench_data()
+    if "reliability" in what:
+        make_reliability_cases()
+    if "market" in what:
+        make_market_cases()
