@@ -297,11 +297,17 @@ def market_group(T, dt, bat, da_price, fr, base=None, ene_min=None, ene_max=None
     ge([(idis, 1.0), (idd, -1.0)], 0.0)
     ge([(iuc, ((1.0 - eta) * eou)[:, None]), (idc, (-(1.0 - eta) * eod)[:, None]), (iud, 2.0 * eou),
         (idd, -2.0 * eod)], 0.0)
+    # The other rows already imply up_ch + up_dis <= P_ch + P_dis and down_ch + down_dis <= P_ch + P_dis
+    # (up_ch <= ch <= P_ch - down_ch, up_dis <= P_dis - dis; down_ch <= P_ch - ch, down_dis <= dis <= P_dis),
+    # so a u/d_ts maximum above that is clamped to it: the same feasible set, but without the reference's
+    # 9,999,999 kW "no limit" placeholders, which would inflate ||q|| and with it the solver's relative
+    # primal tolerance (1e-6 x 7e7 = 70 kW of allowed infeasibility on a Usecase 3 day).
+    cap = (pch + pdis)[:, None]
     if fr.get("regu_max") is not None:
-        ge([(iuc, -1.0), (iud, -1.0)], -_col(fr["regu_max"], G, T))
+        ge([(iuc, -1.0), (iud, -1.0)], -np.minimum(_col(fr["regu_max"], G, T), cap))
         ge([(iuc, 1.0), (iud, 1.0)], _col(fr["regu_min"], G, T))
     if fr.get("regd_max") is not None:
-        ge([(idc, -1.0), (idd, -1.0)], -_col(fr["regd_max"], G, T))
+        ge([(idc, -1.0), (idd, -1.0)], -np.minimum(_col(fr["regd_max"], G, T), cap))
         ge([(idc, 1.0), (idd, 1.0)], _col(fr["regd_min"], G, T))
     if binary_relax:
         ge([(ich, (-1.0 / pch)[:, None]), (idis, (-1.0 / pdis)[:, None])], -1.0)

@@ -76,7 +76,12 @@ def test_builder_matches_oracle(name):
             K[r, g.indices[g.indptr[r]:g.indptr[r + 1]]] = g.data[k, g.indptr[r]:g.indptr[r + 1]]
         assert g.m_eq == o["m_eq"] and K.shape == o["K"].shape
         assert np.abs(K - o["K"].toarray()).max() <= 1e-14
-        for a, b in ((g.q[k], o["q"]), (g.c[k], o["c"]), (g.l[k], o["l"]), (g.u[k], o["u"])):
+        # u/d_ts maxima above P_ch + P_dis are clamped to it by the builder (an implied bound, same feasible set)
+        T = o["T"]
+        cap = -(o["u"][0] + o["u"][T])
+        qb = np.where(o["q"] < cap, cap, o["q"])
+        qb[:o["m_eq"]] = o["q"][:o["m_eq"]]
+        for a, b in ((g.q[k], qb), (g.c[k], o["c"]), (g.l[k], o["l"]), (g.u[k], o["u"])):
             assert np.array_equal(a, b) or np.abs(a - b).max() <= 1e-12
         assert abs(g.c0[k] - o["c0"]) <= 1e-9
         x = wins[d]["x_golden"]
