@@ -10,6 +10,11 @@ returns every window's {objective, residuals, status, iterations} to all ranks.
 
 A step = one solve of the rank's whole batch, already resident in HBM (setup kernel: transpose +
 scaling + ||K|| estimate; PDHG kernel: the iterations), plus the result all-gather when N > 1.
+Default schedule "seeded" (dervet_hip/sweep.py): the windows of 1 in 32 scenarios (battery-energy order) are
+solved from zero first, then every other window warm from its nearest seed's solution of the same month --
+two solver calls per step, every window solved once per step to the same KKT tolerance; nothing carries over
+between steps (the seed phase starts from zero and the warm phase overwrites every warm start).  After the
+timed steps the same batch is solved once more with every window cold, reported as schedule.cold_*.
 The CPU baseline (rank 0, N=1 only) solves a bounded sample of the same windows with HiGHS on a process
 pool (oracle/cpu_baseline.py) and is also the parity check of the GPU objectives on that sample.
 """
@@ -46,6 +51,11 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--check-every", type=int, default=0, help="restart-check period (0: library default)")
     ap.add_argument("--kkt-every", type=int, default=0, help="KKT check every n restart checks (0: default)")
+    ap.add_argument("--schedule", choices=("seeded", "cold"), default="seeded",
+                    help="seeded: every seed-stride-th scenario (battery-energy order) solved cold, the rest warm "
+                         "from their nearest seed (dervet_hip/sweep.py); cold: every window from zero")
+    ap.add_argument("--seed-stride", type=int, default=32)
+    ap.add_argument("--no-cold-ref", action="store_true", help="skip the untimed all-cold reference solve")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -67,9 +77,15 @@ def main():
     S = args.scenarios
     scen = range(*parallel.weak_shard(S, rank))
     t0 = time.time()
-    groups = scenarios.config4(scen)
-    pb = builder.pack_groups(groups)
-    del groups
+    sweep = None
+    if args.schedule == "seeded":
+        from dervet_hip.sweep import SeededSweep
+        sweep = SeededSweep(scenarios.config4, scen, scenarios.sweep_parameters(scen)["E"], stride=args.seed_stride)
+        pb = sweep.packed
+    else:
+        groups = scenarios.config4(scen)
+        pb = builder.pack_groups(groups)
+        del groups
     dev = pb.to_torch(f"cuda:{local}").alloc_outputs()
     build_s = time.time() - t0
     count = pb.count
@@ -84,10 +100,14 @@ def main():
         torch.cuda.synchronize()
 
     gathered = None
+    phase = {}
 
     def step():
         nonlocal gathered
-        solver.solve_packed(dev)
+        if sweep is not None:
+            phase["timing"], phase["paths"] = sweep.solve(solver, dev)
+        else:
+            solver.solve_packed(dev)
         if dist is not None:
             # the single RCCL all-gather of the results (objective, residuals, status, iterations)
             gathered = parallel.gather_rows(parallel.result_rows(dev.stats, dev.istats))
@@ -111,8 +131,10 @@ def main():
     # ---- per-window results of the last step (this rank), roofline of the PDHG kernel
     ist = dev.istats.cpu().numpy()
     st = dev.stats.cpu().numpy()
-    tm = solver.timing()
+    tm = phase.get("timing") or solver.timing()
     ks = solver.kernel_stats()
+    if sweep is not None:
+        ks.update(phase["paths"])
     kname = ("pdhg_band_kernel (battery-banded)" if ks["band_windows"] == count else
              "pdhg_ell_kernel" if ks["ell_windows"] == count else "mixed band / ELL / generic kernels")
     iters = ist[:, 1].astype(np.float64)
@@ -127,8 +149,32 @@ def main():
         with open(tf) as f:
             tj = json.load(f)
         if tj.get("windows") == count:
-            if tj.get("kernel", "").startswith(kname.split()[0]):
-                traffic = tj.get("hbm_bytes_per_launch")
+            lps = 2 if sweep is not None and count > sweep.n_seed else 1
+            if tj.get("kernel", "").startswith(kname.split()[0]) and tj.get("launches_per_step", 1) == lps:
+                traffic = tj.get("hbm_bytes_per_step", tj.get("hbm_bytes_per_launch"))
+
+    schedule = {"kind": args.schedule}
+    if sweep is not None:
+        ns = sweep.n_seed
+        schedule.update(seed_stride=args.seed_stride, seed_windows=ns, iters_mean_seed=round(float(iters[:ns].mean()), 1),
+                        iters_mean_warm=round(float(iters[ns:].mean()), 1) if count > ns else None,
+                        pdhg_launches_per_step=2 if count > ns else 1)
+    if sweep is not None and not args.no_cold_ref:
+        # the same batch once more with every window started from zero (untimed by the contract; for reference)
+        st_seeded = st[:, 0].copy()
+        solver.set_options(warm_start=0)
+        for _ in range(2):  # the first call also re-sizes the workspace for the whole batch
+            barrier()
+            tc = time.perf_counter()
+            solver.solve_packed(dev)
+            barrier()
+            cold_s = time.perf_counter() - tc
+        ist_c = dev.istats.cpu().numpy()
+        st_c = dev.stats.cpu().numpy()
+        schedule.update(cold_windows_per_s=round(count / cold_s, 1), cold_iters_mean=round(float(ist_c[:, 1].mean()), 1),
+                        cold_optimal_frac=float(np.mean(ist_c[:, 0] == 0)),
+                        max_obj_rel_diff_seeded_vs_cold=float(np.max(np.abs(st_seeded - st_c[:, 0]) /
+                                                                     np.maximum(np.abs(st_c[:, 0]), 1.0))))
 
     cpu = None
     parity = None
@@ -165,6 +211,8 @@ def main():
         "config": {"workload": "config4 sweep: 10,000 scenarios x 12 monthly windows per GPU (battery + PV + "
                                "DCM + retailETS, T=672-744 h)",
                    "scenarios_per_gpu": S, "windows_per_gpu": count, "eps_rel_kkt": 1e-6, **opts,
+                   "schedule": (f"seeded (1 in {args.seed_stride} scenarios cold, the rest warm from the nearest "
+                                f"seed)" if sweep is not None else "cold"),
                    "parallelism": f"dp{world} (independent windows, 1 RCCL all-gather of results)"},
         "scenario_years_per_s": round(value / 12.0, 2),
         "iters_mean": round(float(iters.mean()), 1),
@@ -178,10 +226,15 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 3) if achieved else None,
                      "traffic": traffic,
-                     "kernel": kname + ": 1 launch per step; achieved = sum_w B_iter(w) * iters(w) / kernel time "
+                     "traffic_note": "HBM bytes of one step's PDHG launches (PMC FETCH_SIZE x2 + WRITE_SIZE, "
+                                     "profiles/pdhg_traffic.json)",
+                     "kernel": kname + (": 2 launches per step (seed phase + warm phase)" if sweep is not None and
+                                        count > sweep.n_seed else ": 1 launch per step") +
+                               "; achieved = sum_w B_iter(w) * iters(w) / PDHG kernel time of the step "
                                "(HIP events on the solver stream)",
                      "note": "iterate and scaled K are VGPR/LDS-resident, so algorithmic bytes exceed what HBM "
                              "moves; frac > 1 means the on-chip design beats the HBM roofline"},
+        "schedule": schedule,
         "cpu_baseline": cpu,
         "parity": parity,
         "build_s": round(build_s, 1),

@@ -102,6 +102,12 @@ class BatchSolver:
             msg = self._lib.dvh_last_error(self._h)
             raise SolverError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
 
+    def options(self):
+        """The handle's current dvh_options (a copy)."""
+        o = type(self._opts)()
+        ctypes.pointer(o)[0] = self._opts
+        return o
+
     def set_options(self, **options):
         for k, v in options.items():
             setattr(self._opts, k, v)

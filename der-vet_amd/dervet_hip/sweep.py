@@ -1,0 +1,180 @@
+"""Seeded two-phase schedule for scenario sweeps (BASELINE config 4 / 5; DER-VET's sensitivity loop,
+``dervet/DERVET.py:75``, runs the same windows for many perturbed cases).
+
+A sweep solves the same window (same month, same CSR pattern) for thousands of perturbed scenarios.  Instead
+of starting every PDHG run from zero, the schedule
+
+  1. solves a SEED subset of the scenarios cold (every ``stride``-th scenario in order of a similarity key,
+     the battery energy rating by default), then
+  2. solves every other scenario's window warm, from its nearest seed's solution of the same window
+     (``dvh_options.warm_start``): bounded columns are scaled by the ratio of the two windows' upper bounds
+     (charge / discharge power, energy), and, for the plain battery + DCM shape (x = [ch, dis, ene, tau]),
+     the SOE-row duals by the ratio of the mean energy prices and the DCM-row duals by the ratio of the demand
+     charges.
+
+Every window is still solved to the same relative KKT tolerance and the same statuses; only the starting
+point changes (``scripts/warm_study.py``: 3,351 -> 2,316 mean iterations on config-4 windows started from a
+neighbour).  The two phases are two ``dvh_solve_packed_device`` calls on sub-ranges of ONE packed batch (seed
+windows packed first), and the transfer between them is a device-side gather on the solver's stream.
+"""
+from dataclasses import dataclass
+
+import numpy as np
+
+from .packed import PackedBatch
+
+
+def seed_split(keys, stride):
+    """Scenario positions -> (seed positions, rest positions, partner) with `partner[i]` the index into the
+    seed list of rest position `rest[i]`'s nearest seed in key order.  Seeds are every `stride`-th scenario
+    in key order, starting at stride // 2 so that each seed sits in the middle of its neighbourhood."""
+    keys = np.asarray(keys, np.float64)
+    S = len(keys)
+    stride = max(int(stride), 1)
+    if stride == 1 or S < 2:
+        return np.arange(S), np.zeros(0, np.int64), np.zeros(0, np.int64)
+    order = np.argsort(keys, kind="stable")
+    pos = np.arange(S)
+    seed_pos = np.arange(min(stride // 2, S - 1), S, stride)           # positions in key order
+    is_seed = np.zeros(S, bool)
+    is_seed[seed_pos] = True
+    rest_pos = pos[~is_seed]
+    near = np.clip(np.searchsorted(seed_pos, rest_pos), 0, len(seed_pos) - 1)
+    left = np.clip(near - 1, 0, len(seed_pos) - 1)
+    pick = np.where(np.abs(seed_pos[left] - rest_pos) <= np.abs(seed_pos[near] - rest_pos), left, near)
+    return order[seed_pos], order[rest_pos], pick
+
+
+@dataclass
+class _Transfer:
+    """One rest group <- its seed group (same window id and CSR pattern)."""
+    on_rest: int
+    om_rest: int
+    on_seed: int
+    om_seed: int
+    n: int
+    m: int
+    g_rest: int
+    g_seed: int
+    local: object        # [g_rest] index into the seed group
+    battery_dcm: bool    # x = [ch, dis, ene, tau (1)]: scale the duals too
+    T: int
+
+
+def _window_id(tag):
+    return tag[1] if isinstance(tag, tuple) and len(tag) > 1 else tag
+
+
+def plan(seed_groups, rest_groups, partner_of):
+    """Transfers from the packed seed windows (packed first) to the rest windows (packed after them).
+
+    partner_of: dict rest scenario id -> seed scenario id.  Groups are matched by window id (tag[1]) and must
+    share the CSR pattern."""
+    out = []
+    on = om = 0
+    seed_at = {}
+    for g in seed_groups:
+        seed_at[_window_id(g.tags[0])] = (g, on, om)
+        on += g.G * g.n
+        om += g.G * g.m
+    for g in rest_groups:
+        wid = _window_id(g.tags[0])
+        if wid not in seed_at:
+            raise ValueError(f"no seed group for window {wid!r}")
+        sg, son, som = seed_at[wid]
+        if sg.n != g.n or sg.m != g.m or not np.array_equal(sg.indices, g.indices) or \
+                not np.array_equal(sg.indptr, g.indptr):
+            raise ValueError(f"seed and rest groups of window {wid!r} differ in pattern")
+        col = {t[0]: i for i, t in enumerate(sg.tags)}
+        local = np.array([col[partner_of[t[0]]] for t in g.tags], np.int64)
+        out.append(_Transfer(on, om, son, som, g.n, g.m, g.G, sg.G, local,
+                             g.n == 3 * g.T + 1 and g.J == 1, g.T))
+        on += g.G * g.n
+        om += g.G * g.m
+    return out
+
+
+def transfer(tr_list, x, y, c, u):
+    """Write warm starts for the rest windows into x / y (torch tensors, device or host) from the seeds'
+    solutions already in x / y.  c, u: the packed objective and upper bounds."""
+    import torch
+    for t in tr_list:
+        loc = torch.as_tensor(t.local, device=x.device)
+        Xs = x[t.on_seed:t.on_seed + t.g_seed * t.n].view(t.g_seed, t.n)[loc]
+        Us = u[t.on_seed:t.on_seed + t.g_seed * t.n].view(t.g_seed, t.n)[loc]
+        Ur = u[t.on_rest:t.on_rest + t.g_rest * t.n].view(t.g_rest, t.n)
+        ok = torch.isfinite(Ur) & torch.isfinite(Us) & (Us > 0)
+        ratio = torch.where(ok, Ur / torch.where(ok, Us, torch.ones_like(Us)), torch.ones_like(Us))
+        x[t.on_rest:t.on_rest + t.g_rest * t.n].view(t.g_rest, t.n).copy_(Xs * ratio)
+        Ys = y[t.om_seed:t.om_seed + t.g_seed * t.m].view(t.g_seed, t.m)[loc]
+        if t.battery_dcm:
+            T = t.T
+            Cs = c[t.on_seed:t.on_seed + t.g_seed * t.n].view(t.g_seed, t.n)[loc]
+            Cr = c[t.on_rest:t.on_rest + t.g_rest * t.n].view(t.g_rest, t.n)
+            cd = Cr[:, 3 * T:3 * T + 1] / Cs[:, 3 * T:3 * T + 1].clamp(min=1e-12)
+            cp = Cr[:, :T].abs().mean(1, keepdim=True) / Cs[:, :T].abs().mean(1, keepdim=True).clamp(min=1e-12)
+            Ys = torch.cat([Ys[:, :T + 1] * cp, Ys[:, T + 1:] * cd], dim=1)
+        y[t.om_rest:t.om_rest + t.g_rest * t.m].view(t.g_rest, t.m).copy_(Ys)
+
+
+def sub_batch(pb, a, b):
+    """Windows [a, b) of a device PackedBatch as a batch of its own (same flat arrays; the descriptors'
+    offsets are absolute, per-window arrays are sliced)."""
+    return PackedBatch(desc=pb.desc[a:b], indptr=pb.indptr, indices=pb.indices, data=pb.data, c=pb.c,
+                       c0=pb.c0[a:b], q=pb.q, l=pb.l, u=pb.u, x=pb.x, y=pb.y, stats=pb.stats[a:b],
+                       istats=pb.istats[a:b])
+
+
+class SeededSweep:
+    """Packs a scenario sweep seed-first and solves it in the two phases of the module docstring.
+
+    make_groups(scenario_ids) -> list of WindowGroup (e.g. ``scenarios.config4``); keys: similarity key per
+    scenario (same order as `scenario_ids`)."""
+
+    def __init__(self, make_groups, scenario_ids, keys, stride=8):
+        from .lp import builder
+        ids = np.asarray(list(scenario_ids), np.int64)
+        seed_i, rest_i, pick = seed_split(keys, stride)
+        self.seed_ids, self.rest_ids = ids[seed_i], ids[rest_i]
+        partner_of = {int(r): int(self.seed_ids[p]) for r, p in zip(self.rest_ids, pick)}
+        sg = make_groups(self.seed_ids)
+        rg = make_groups(self.rest_ids) if len(self.rest_ids) else []
+        self.transfers = plan(sg, rg, partner_of)
+        self.n_seed = sum(g.G for g in sg)
+        self.packed = builder.pack_groups(sg + rg)
+        self.tags = [t for g in sg + rg for t in g.tags]
+
+    def solve(self, solver, dev):
+        """dev: this sweep's packed batch on the device (``self.packed.to_torch(..).alloc_outputs()``).
+        Returns the kernel timings {setup_ms, pdhg_ms, total_ms} and the windows per kernel path, summed over
+        the two phases."""
+        import torch
+        cnt = dev.count
+        warm0 = solver.options().warm_start
+        tm = {"total_ms": 0.0, "setup_ms": 0.0, "pdhg_ms": 0.0}
+        paths = {}
+
+        def account():
+            for k, v in solver.timing().items():
+                tm[k] += v
+            for k, v in solver.kernel_stats().items():
+                if k.endswith("_windows"):
+                    paths[k] = paths.get(k, 0) + v
+
+        solver.set_options(warm_start=0)
+        solver.solve_packed(sub_batch(dev, 0, self.n_seed))
+        account()
+        if cnt > self.n_seed:
+            stream = torch.cuda.current_stream(dev.x.device) if dev.x.is_cuda else None
+            if stream is not None:
+                torch.cuda.synchronize(dev.x.device)  # seeds solved (library stream) before the gather reads them
+            transfer(self.transfers, dev.x, dev.y, dev.c, dev.u)
+            if stream is not None:
+                torch.cuda.synchronize(dev.x.device)
+            solver.set_options(warm_start=1)
+            try:
+                solver.solve_packed(sub_batch(dev, self.n_seed, cnt))
+            finally:
+                solver.set_options(warm_start=warm0)
+            account()
+        return tm, paths

@@ -28,7 +28,14 @@ def highs_batch(lps, procs=None):
     if procs <= 1:
         res = [_solve_one(lp) for lp in lps]
     else:
-        with get_context("fork").Pool(procs) as pool:
+        pool = get_context("fork").Pool(procs)
+        try:
             res = pool.map(_solve_one, lps, chunksize=max(1, len(lps) // (4 * procs)))
+            pool.close()  # workers exit on their own (no SIGTERM: a profiler's signal handler in them can hang)
+        except BaseException:
+            pool.terminate()
+            raise
+        finally:
+            pool.join()
     wall = time.perf_counter() - t
     return (np.array([r[0] for r in res]), np.array([r[1] for r in res]), wall, procs)

@@ -1,6 +1,9 @@
 """Turn rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE; one counter per pass) into profiles/pdhg_traffic.json.
 
-Usage: python scripts/pmc_traffic.py <fetch_dir> <write_dir> <windows_per_launch> [out.json]
+Usage: python scripts/pmc_traffic.py <fetch_dir> <write_dir> <windows_per_step> [out.json] [launches_per_step]
+
+With the seeded sweep schedule (bench.py default) one step is two launches of the PDHG kernel (seed phase, warm
+phase); hbm_bytes_per_step sums them (the PMC runs do exactly one step and skip the cold reference solves).
 
 FETCH_SIZE / WRITE_SIZE are in KB (rocprofv3 derived counters).  Per MI355X_MICROARCH.md section HBM: on
 gfx950 FETCH_SIZE reports half of the bytes of wide coalesced reads, so it is doubled; WRITE_SIZE is taken
@@ -39,6 +42,7 @@ def main():
     fdir, wdir, windows = sys.argv[1], sys.argv[2], int(sys.argv[3])
     out = sys.argv[4] if len(sys.argv) > 4 else os.path.join(os.path.dirname(__file__), "..", "profiles",
                                                               "pdhg_traffic.json")
+    lps = int(sys.argv[5]) if len(sys.argv) > 5 else 1
     fetch = read_counter(fdir, "FETCH_SIZE")
     write = read_counter(wdir, "WRITE_SIZE")
     kern = [k for k in fetch if "pdhg_band_kernel" in k] or [k for k in fetch if "pdhg_ell_kernel" in k]
@@ -54,6 +58,8 @@ def main():
         "dispatches_fetch": len(fv), "dispatches_write": len(wv),
         "fetch_size_kb_raw": f_kb, "write_size_kb": w_kb,
         "hbm_bytes_per_launch": 2.0 * f_kb * 1024.0 + w_kb * 1024.0,
+        "launches_per_step": lps,
+        "hbm_bytes_per_step": (2.0 * f_kb * 1024.0 + w_kb * 1024.0) * lps,
         "correction": "FETCH_SIZE x2 (gfx950 wide-read under-count), WRITE_SIZE x1; KB = 1024 B",
         "other_kernels": {re.sub(r"^void |\(.*$", "", k)[:80]: {"fetch_kb": sum(v) / len(v)} for k, v in fetch.items()
                           if k not in kern},

@@ -1,0 +1,96 @@
+"""Seeded two-phase sweep schedule (dervet_hip/sweep.py): host logic on CPU, the schedule itself on cuda:0.
+
+CPU: seed selection / nearest-seed partners, the seed-first packing, and the warm-start transfer (bound-ratio
+scaling of x, price-ratio scaling of the duals) on host tensors against a direct numpy restatement.
+GPU: every window of a small config-4 sweep is optimal, objectives within 1e-5 of HiGHS on a sample and of
+the all-cold solve, and the warm phase needs fewer iterations.
+"""
+import numpy as np
+import pytest
+import torch
+
+from dervet_hip.lp import builder, scenarios
+from dervet_hip.sweep import SeededSweep, seed_split, sub_batch, transfer
+
+
+def test_seed_split_partners_are_nearest_in_key_order():
+    rng = np.random.default_rng(3)
+    keys = rng.uniform(0, 1, 101)
+    seeds, rest, pick = seed_split(keys, 8)
+    assert len(seeds) + len(rest) == 101 and len(set(seeds) | set(rest)) == 101
+    order = np.argsort(keys, kind="stable")
+    pos = np.empty(101, int)
+    pos[order] = np.arange(101)
+    for r, p in zip(rest, pick):
+        d = abs(pos[seeds[p]] - pos[r])
+        assert d == min(abs(pos[s] - pos[r]) for s in seeds)
+    s1, r1, _ = seed_split(keys, 1)
+    assert len(s1) == 101 and len(r1) == 0
+
+
+def test_seeded_packing_and_transfer_on_host():
+    ids = np.arange(12)
+    keys = scenarios.sweep_parameters(ids)["E"]
+    sw = SeededSweep(scenarios.config4, ids, keys, stride=4)
+    assert sw.n_seed == 12 * len(sw.seed_ids) and sw.packed.count == 12 * 12
+    # seeds packed first, every window once
+    assert sorted(sw.tags) == sorted((int(s), w) for s in ids for w in range(12))
+    assert {t[0] for t in sw.tags[:sw.n_seed]} == set(int(s) for s in sw.seed_ids)
+    pb = sw.packed.to_torch("cpu").alloc_outputs()
+    g = torch.Generator().manual_seed(0)
+    pb.x.copy_(torch.randn(pb.x.shape, generator=g, dtype=torch.float64))
+    pb.y.copy_(torch.randn(pb.y.shape, generator=g, dtype=torch.float64))
+    x0, y0 = pb.x.clone(), pb.y.clone()
+    transfer(sw.transfers, pb.x, pb.y, pb.c, pb.u)
+    desc = np.asarray(sw.packed.desc)
+    for tr in sw.transfers:
+        for i in range(tr.g_rest):
+            partner_local = int(tr.local[i])
+            on_r, on_s = tr.on_rest + i * tr.n, tr.on_seed + partner_local * tr.n
+            om_r, om_s = tr.om_rest + i * tr.m, tr.om_seed + partner_local * tr.m
+            u_r, u_s = sw.packed.u[on_r:on_r + tr.n], sw.packed.u[on_s:on_s + tr.n]
+            ok = np.isfinite(u_r) & np.isfinite(u_s) & (u_s > 0)
+            ratio = np.where(ok, u_r / np.where(ok, u_s, 1.0), 1.0)
+            np.testing.assert_allclose(pb.x[on_r:on_r + tr.n].numpy(), x0[on_s:on_s + tr.n].numpy() * ratio,
+                                       rtol=1e-15, atol=0)
+            assert tr.battery_dcm  # config-4 windows: x = [ch, dis, ene, tau]
+            T = tr.T
+            c_r, c_s = sw.packed.c[on_r:on_r + tr.n], sw.packed.c[on_s:on_s + tr.n]
+            cd = c_r[3 * T] / max(c_s[3 * T], 1e-12)
+            cp = np.abs(c_r[:T]).mean() / max(np.abs(c_s[:T]).mean(), 1e-12)
+            ys = y0[om_s:om_s + tr.m].numpy()
+            want = np.concatenate([ys[:T + 1] * cp, ys[T + 1:] * cd])
+            np.testing.assert_allclose(pb.y[om_r:om_r + tr.m].numpy(), want, rtol=1e-14, atol=0)
+    # seed windows untouched
+    ns_n = int(desc[sw.n_seed, 6])
+    assert torch.equal(pb.x[:ns_n], x0[:ns_n])
+    # sub-batch views keep absolute offsets and slice the per-window arrays
+    sb = sub_batch(pb, sw.n_seed, pb.count)
+    assert sb.count == pb.count - sw.n_seed and int(sb.desc[0, 6]) == ns_n
+    assert sb.c0.shape[0] == sb.count and sb.stats.shape[0] == sb.count
+
+
+@pytest.mark.gpu
+def test_seeded_sweep_on_gpu_matches_cold_and_highs():
+    from dervet_hip import BatchSolver
+    from oracle import window_lp
+    ids = np.arange(64)
+    sw = SeededSweep(scenarios.config4, ids, scenarios.sweep_parameters(ids)["E"], stride=8)
+    dev = sw.packed.to_torch("cuda:0").alloc_outputs()
+    with BatchSolver(0) as s:
+        _, paths = sw.solve(s, dev)
+        assert s.options().warm_start == 0  # restored
+        st, ist = dev.stats.cpu().numpy(), dev.istats.cpu().numpy()
+        assert (ist[:, 0] == 0).all() and sum(paths.values()) == sw.packed.count
+        cold = builder.pack_groups(scenarios.config4(ids)).to_torch("cuda:0").alloc_outputs()
+        s.solve_packed(cold)
+        cst, cist = cold.stats.cpu().numpy(), cold.istats.cpu().numpy()
+    ctags = [t for g in scenarios.config4(ids) for t in g.tags]
+    cobj = {t: cst[k, 0] for k, t in enumerate(ctags)}
+    rel = [abs(st[k, 0] - cobj[t]) / max(abs(cobj[t]), 1.0) for k, t in enumerate(sw.tags)]
+    assert max(rel) <= 2e-5
+    assert ist[sw.n_seed:, 1].mean() < 0.85 * cist[:, 1].mean()
+    for k in range(0, sw.packed.count, 97):
+        h = window_lp.solve_highs(window_lp.from_packed_window(sw.packed.window(k)))
+        assert abs(st[k, 0] - h["obj"]) <= 1e-5 * max(abs(h["obj"]), 1.0), (k, st[k, 0], h["obj"])
+        assert st[k, 1] <= 1e-6
