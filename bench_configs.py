@@ -1,0 +1,137 @@
+#!/usr/bin/env python3
+"""Per-config measurement of the batched window-LP solver on one MI355X: every BASELINE.json config, one JSON
+line each (bench.py is the headline line, config 4 at full size; this script covers the other four and a
+config-4 slice for comparison).
+
+  config 1  Model_Parameters_Template_DER.csv: template battery, DA energy time shift, 12 monthly windows
+            (literal template) and the DA + retailETS variant
+  config 2  battery + PV + DCM + retailETS on data/multi_der_hourly_timeseries.csv, 3 opt years = 36 windows
+  config 3  5-minute annual window (T = 105,120): the grid-wide large-LP path, with and without retail + DCM
+  config 4  --c4-scenarios scenarios x 12 monthly windows, seeded and cold schedules
+  config 5  battery + PV + LP-relaxed ICE + 4-h reliability min-SOE, --c5-scenarios scenarios x 12 monthly windows
+            per opt year; the 20-year horizon is 20 independent year batches of the same shape (the horizon's
+            windows do not couple), so one year batch resident in HBM is the timed unit
+
+For every config: windows, wall time of a solve with the batch resident in HBM (best of --reps after one
+warm-up), windows/s, iterations, kernel path, and parity on a sample against HiGHS on the restated LP
+(oracle/window_lp.py; objective rel error, and the primal residual recomputed from the returned x).
+Usage: python bench_configs.py [--only 1,2,3,4,5] [--c4-scenarios 2000] [--c5-scenarios 1000]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "der-vet_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def _parity(pb, st, xs, sample, procs):
+    from oracle import cpu_baseline, window_lp
+    idx = np.unique(np.linspace(0, pb.count - 1, min(sample, pb.count)).astype(np.int64))
+    lps = [window_lp.from_packed_window(pb.window(int(k))) for k in idx]
+    objs, sts, wall, used = cpu_baseline.highs_batch(lps, procs)
+    rel, pres = [], []
+    for j, k in enumerate(idx):
+        if sts[j] == 0:
+            rel.append(abs(st[k, 0] - objs[j]) / max(abs(objs[j]), 1.0))
+        d = pb.desc[k]
+        x = xs[int(d[6]):int(d[6]) + int(d[0])]
+        pres.append(window_lp.primal_residual_rel(lps[j], x)[0])
+    return {"sample_windows": int(len(idx)), "highs_optimal": int((sts == 0).sum()),
+            "max_obj_rel_err_vs_highs": float(max(rel)) if rel else None,
+            "max_primal_res_rel": float(max(pres)),
+            "highs_windows_per_s": round(len(idx) / wall, 2), "highs_procs": used}
+
+
+def run(name, note, pb, solver, reps, sample, procs, sweep=None):
+    dev = pb.to_torch("cuda:0").alloc_outputs()
+    best, tm, paths = None, None, None
+    for r in range(reps + 1):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        if sweep is not None:
+            tm_, paths_ = sweep.solve(solver, dev)
+        else:
+            solver.solve_packed(dev)
+            tm_, paths_ = solver.timing(), solver.kernel_stats()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t
+        if r > 0 and (best is None or el < best):
+            best, tm, paths = el, tm_, paths_
+    ist = dev.istats.cpu().numpy()
+    st = dev.stats.cpu().numpy()
+    xs = dev.x.cpu().numpy()
+    d = np.asarray(pb.desc)
+    line = {"config": name, "workload": note, "windows": pb.count, "n_max": int(d[:, 0].max()), "m_max": int(d[:, 1].max()),
+            "schedule": "seeded" if sweep is not None else "cold",
+            "wall_ms": round(best * 1e3, 2), "windows_per_s": round(pb.count / best, 1),
+            "kernel_ms": {k: round(v, 2) for k, v in tm.items()},
+            "iters_mean": round(float(ist[:, 1].mean()), 1), "iters_max": int(ist[:, 1].max()),
+            "optimal": int((ist[:, 0] == 0).sum()),
+            "kernel_path": {k: v for k, v in paths.items() if k.endswith("_windows")},
+            "parity": _parity(pb, st, xs, sample, procs) if sample > 0 else None}
+    print(json.dumps(line), flush=True)
+    del dev
+    return line
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="1,2,3,4,5")
+    ap.add_argument("--c4-scenarios", type=int, default=2000)
+    ap.add_argument("--c5-scenarios", type=int, default=1000)
+    ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--sample", type=int, default=48)
+    ap.add_argument("--procs", type=int, default=16)
+    args = ap.parse_args()
+    if not torch.cuda.is_available():
+        raise SystemExit("bench_configs.py needs a GPU (the solver has no CPU fallback)")
+    from dervet_hip import BatchSolver
+    from dervet_hip.lp import builder, scenarios
+    from dervet_hip.sweep import SeededSweep
+    only = {int(v) for v in args.only.split(",")}
+    s = BatchSolver(0)
+    P = lambda groups: builder.pack_groups(groups)  # noqa: E731
+    if 1 in only:
+        run("config1", "template battery, DA time shift, 12 monthly windows (Model_Parameters_Template_DER.csv)",
+            P(scenarios.config1()), s, args.reps, 12, args.procs)
+        run("config1+retail", "template battery, DA + retailETS (data/tariff.csv, site load), 12 monthly windows",
+            P(scenarios.config1(with_retail=True)), s, args.reps, 12, args.procs)
+    if 2 in only:
+        run("config2", "battery + PV + DCM + retailETS, 3 opt years x 12 monthly windows",
+            P(scenarios.config2()), s, args.reps, 36, args.procs)
+    if 3 in only:
+        ri = scenarios.reference_inputs()
+        T = len(ri["fivemin_da_price"])
+        g = scenarios.windows_by_period(2019, 1.0 / 12, np.zeros((1, T)), None, scenarios.template_battery(),
+                                        da_price=ri["fivemin_da_price"][None, :], n="year")
+        run("config3", "5-min annual window (T = 105,120), template battery, DA", P(g), s, args.reps, 1, 1)
+        g = scenarios.windows_by_period(2019, 1.0 / 12, ri["fivemin_site_load"][None, :], None,
+                                        scenarios.template_battery(), da_price=ri["fivemin_da_price"][None, :],
+                                        tariff_def=scenarios.tariff(), n="year")
+        run("config3+dcm", "5-min annual window, DA + retailETS + 12 monthly DCM charges", P(g), s, args.reps, 0, 1)
+    if 4 in only:
+        ids = range(args.c4_scenarios)
+        run("config4-slice", f"{args.c4_scenarios} scenarios x 12 monthly windows (bench.py runs 10,000)",
+            P(scenarios.config4(ids)), s, args.reps, args.sample, args.procs)
+        sw = SeededSweep(scenarios.config4, ids, scenarios.sweep_parameters(ids)["E"], stride=32)
+        run("config4-slice", f"{args.c4_scenarios} scenarios x 12 monthly windows, seeded schedule",
+            sw.packed, s, args.reps, args.sample, args.procs, sweep=sw)
+    if 5 in only:
+        ids = range(args.c5_scenarios)
+        mk = lambda v: scenarios.config5(v, years=1)  # noqa: E731
+        run("config5", f"{args.c5_scenarios} scenarios x 12 monthly windows of one opt year (x 20 years = 20 such "
+                       f"batches)", P(mk(ids)), s, args.reps, args.sample, args.procs)
+        sw = SeededSweep(mk, ids, scenarios.sweep_parameters(ids)["E"], stride=32)
+        run("config5", f"{args.c5_scenarios} scenarios x 12 monthly windows of one opt year, seeded schedule",
+            sw.packed, s, args.reps, args.sample, args.procs, sweep=sw)
+
+
+if __name__ == "__main__":
+    main()

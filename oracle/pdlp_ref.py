@@ -111,8 +111,12 @@ def solve(lp, opts=None, trace=None):
                     pres_rel=np.linalg.norm(r) / (1 + q_norm), dres_rel=np.linalg.norm(rd) / (1 + c_norm),
                     gap_rel=abs(pobj - dobj) / (1 + abs(pobj) + abs(dobj)))
 
-    x = np.clip(np.zeros(n), lt, ut)
-    y = np.zeros(m)
+    # warm start (dvh_options.warm_start): unscaled x0 / y0 moved into the scaled space; optional w0
+    x = np.clip(np.asarray(o["x0"], float) / Dc if o.get("x0") is not None else np.zeros(n), lt, ut)
+    y = np.asarray(o["y0"], float) / Dr if o.get("y0") is not None else np.zeros(m)
+    y[m_eq:] = np.maximum(y[m_eq:], 0.0)
+    if o.get("w0"):
+        w = float(o["w0"])
     xa, ya = x.copy(), y.copy()
     k = 0
     r0 = None
@@ -160,4 +164,4 @@ def solve(lp, opts=None, trace=None):
     xs, ys = (x, y) if status == OPTIMAL else last
     info = kkt(xs, ys)
     xo = Dc * xs
-    return dict(x=xo, y=Dr * ys, obj=float(c @ xo + c0), status=status, iters=it, kkt=info)
+    return dict(x=xo, y=Dr * ys, obj=float(c @ xo + c0), status=status, iters=it, kkt=info, w=w)
