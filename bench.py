@@ -73,13 +73,13 @@ def main():
     from dervet_hip.lp import builder, scenarios
 
     from dervet_hip import parallel
+    from dervet_hip.sweep import SeededSweep, WARM_OPTIONS
 
     S = args.scenarios
     scen = range(*parallel.weak_shard(S, rank))
     t0 = time.time()
     sweep = None
     if args.schedule == "seeded":
-        from dervet_hip.sweep import SeededSweep
         sweep = SeededSweep(scenarios.config4, scen, scenarios.sweep_parameters(scen)["E"], stride=args.seed_stride)
         pb = sweep.packed
     else:
@@ -212,7 +212,7 @@ def main():
                                "DCM + retailETS, T=672-744 h)",
                    "scenarios_per_gpu": S, "windows_per_gpu": count, "eps_rel_kkt": 1e-6, **opts,
                    "schedule": (f"seeded (1 in {args.seed_stride} scenarios cold, the rest warm from the nearest "
-                                f"seed)" if sweep is not None else "cold"),
+                                f"seed; warm phase {WARM_OPTIONS})" if sweep is not None else "cold"),
                    "parallelism": f"dp{world} (independent windows, 1 RCCL all-gather of results)"},
         "scenario_years_per_s": round(value / 12.0, 2),
         "iters_mean": round(float(iters.mean()), 1),

@@ -1,0 +1,55 @@
+"""Warm-phase parameter sweep (dev helper): the seeded config-4 schedule with different dvh_options for the warm
+phase only.  Prints warm-phase iterations and kernel time per variant.
+
+Usage: python scripts/warm_params.py <scenarios>
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "der-vet_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from dervet_hip import BatchSolver  # noqa: E402
+from dervet_hip.lp import scenarios  # noqa: E402
+from dervet_hip.sweep import SeededSweep  # noqa: E402
+
+VARIANTS = [
+    {},
+    {"check_every": 64},
+    {"check_every": 64, "restart_artificial": 0.2},
+    {"check_every": 64, "kkt_every": 2},
+    {"check_every": 64, "kkt_every": 3, "restart_artificial": 0.2},
+    {"check_every": 48},
+    {"check_every": 48, "restart_artificial": 0.2},
+    {"check_every": 96, "kkt_every": 2},
+    {"check_every": 128, "kkt_every": 1},
+    {"restart_artificial": 0.3},
+]
+
+
+def main():
+    S = int(sys.argv[1]) if len(sys.argv) > 1 else 4000
+    ids = np.arange(S)
+    sw = SeededSweep(scenarios.config4, ids, scenarios.sweep_parameters(ids)["E"], stride=32)
+    dev = sw.packed.to_torch("cuda:0").alloc_outputs()
+    s = BatchSolver(0)
+    ns = sw.n_seed
+    base = None
+    for v in VARIANTS:
+        tms = []
+        for rep in range(2):
+            tm, _ = sw.solve(s, dev, warm_options=v)
+            tms.append(tm["pdhg_ms"])
+        ist = dev.istats.cpu().numpy()
+        obj = dev.stats.cpu().numpy()[:, 0]
+        if base is None:
+            base = obj.copy()
+        rel = np.abs(obj - base) / np.maximum(np.abs(base), 1.0)
+        print(f"{str(v):40s} pdhg {min(tms):7.1f} ms  warm iters mean {ist[ns:, 1].mean():7.1f}  p99 "
+              f"{np.percentile(ist[ns:, 1], 99):.0f}  optimal {(ist[:, 0] == 0).sum()}/{len(ist)}  "
+              f"max obj diff vs default {rel.max():.1e}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
