@@ -63,11 +63,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (the solver has no CPU fallback)")
+    local = local % torch.cuda.device_count()  # one rank per GPU; wraps only in a several-ranks-per-GPU rehearsal
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # RCCL over xGMI; DVH_BENCH_BACKEND=gloo only to rehearse several ranks on one GPU (RCCL refuses that)
+        backend = os.environ.get("DVH_BENCH_BACKEND", "nccl")
+        dist.init_process_group(backend, **({"device_id": torch.device("cuda", local)} if backend == "nccl" else {}))
 
     from dervet_hip import BatchSolver
     from dervet_hip.lp import builder, scenarios
@@ -208,7 +211,7 @@ def main():
         "dtype": "f64",
         "data": "synthetic: config-4 generator (PCG64 seeds 20250217+s) over data/multi_der_hourly_timeseries.csv "
                 "and data/tariff.csv",
-        "config": {"workload": "config4 sweep: 10,000 scenarios x 12 monthly windows per GPU (battery + PV + "
+        "config": {"workload": f"config4 sweep: {S:,} scenarios x 12 monthly windows per GPU (battery + PV + "
                                "DCM + retailETS, T=672-744 h)",
                    "scenarios_per_gpu": S, "windows_per_gpu": count, "eps_rel_kkt": 1e-6, **opts,
                    "schedule": (f"seeded (1 in {args.seed_stride} scenarios cold, the rest warm from the nearest "
