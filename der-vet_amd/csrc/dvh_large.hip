@@ -70,6 +70,7 @@ struct LgArgs {
   LgState* st;
   double eps, rho, b_suff, b_nec, b_art, theta, step_safety;
   int chk, kkt_every, max_iters;
+  int warm;              // 1: start from the unscaled x / y already in the output buffers (dvh_options.warm_start)
   // outputs
   double* ox; double* oy; double* ostats; int32_t* oist;
 };
@@ -291,16 +292,18 @@ __global__ __launch_bounds__(1024) void lg_pow_norm(LgArgs a, int nblk) {
 __global__ __launch_bounds__(LB) void lg_start(LgArgs a) {
   const int t = blockIdx.x * LB + threadIdx.x;
   if (t < a.n) {
-    const double x0 = fmin(fmax(0.0, a.ls[t]), a.us[t]);
+    const double x0 = fmin(fmax(a.warm ? a.ox[t] / a.dc[t] : 0.0, a.ls[t]), a.us[t]);
     a.x[t] = x0;
     a.xa[t] = x0;
     a.xo[t] = x0;
     a.xb[t] = x0;
   }
   if (t < a.m) {
-    a.y[t] = 0.0;
-    a.ya[t] = 0.0;
-    a.yo[t] = 0.0;
+    double y0 = a.warm ? a.oy[t] / a.dr[t] : 0.0;
+    if (t >= a.meq) y0 = fmax(y0, 0.0);  // >= rows: dual feasibility of the start
+    a.y[t] = y0;
+    a.ya[t] = y0;
+    a.yo[t] = y0;
   }
   if (t == 0) {
     LgState* st = a.st;
@@ -766,6 +769,7 @@ hipError_t large_solve(LargeSolver* ls, const Batch& b, int k, const int64_t* d,
   a.chk = std::max(1, std::min(o.check_every, o.max_iters));
   a.kkt_every = std::max(1, o.kkt_every);
   a.max_iters = o.max_iters;
+  a.warm = o.warm ? 1 : 0;
   a.ox = b.x + on; a.oy = b.y + om; a.ostats = b.stats + 4 * (int64_t)k; a.oist = b.istats + 2 * (int64_t)k;
   {
     double c0 = 0.0;

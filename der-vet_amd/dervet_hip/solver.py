@@ -68,10 +68,23 @@ class SolverError(RuntimeError):
     pass
 
 
+def _init_torch_first():
+    """Let PyTorch (device memory, streams, torch.distributed in this package) create its HIP context before the
+    library's first HIP call: on the GPU box, torch.cuda.is_available() reported no device when libdervet_hip
+    had initialised HIP first in the process."""
+    try:
+        import torch
+    except ImportError:
+        return
+    if torch.cuda.is_available():
+        torch.cuda.init()
+
+
 class BatchSolver:
     """One GPU, one HIP stream.  Options are dvh_options fields (eps, max_iters, ...)."""
 
     def __init__(self, device=0, **options):
+        _init_torch_first()
         self._lib = _lib.load()
         self._opts = _lib.default_options(**options)
         h = ctypes.c_void_p()
