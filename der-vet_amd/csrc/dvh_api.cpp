@@ -493,7 +493,7 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
     DVH_HIP(h, hipEventCreate(&e2));
     h->chunk_events.push_back({e0, e1, e2});
     DVH_HIP(h, hipEventRecord(e0, s));
-    DVH_HIP(h, dvh::launch_setup(b, w, c.ch, o, c.mn, s));
+    DVH_HIP(h, dvh::launch_setup(b, w, c.ch, o, c.mn, c.mm, s));
     DVH_HIP(h, hipEventRecord(e1, s));
     // ELL widths from the setup statistics (one small D2H per chunk)
     scal.resize((size_t)c.ch.count * dvh::kScal);

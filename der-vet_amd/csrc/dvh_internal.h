@@ -72,7 +72,7 @@ struct Chunk {
 };
 
 // Launchers (dvh_kernels.hip).  Return hipError_t.
-hipError_t launch_setup(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n,
+hipError_t launch_setup(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n, int max_m,
                         hipStream_t s);
 // Solve kernel selection is made from the chunk maxima; returns hipErrorInvalidValue when no
 // instantiation covers the sizes (the caller reports DVH_ERR_UNSUPPORTED).
@@ -90,7 +90,7 @@ hipError_t launch_pdhg_ell(const Batch& b, const Work& w, const Chunk& ch, const
 // or null for the whole chunk.
 hipError_t launch_pdhg_band(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, hipStream_t s, bool ice,
                             const int32_t* list, int nlist);
-size_t setup_lds_bytes(int max_n);
+size_t setup_lds_bytes(int max_n, int max_m);
 // Power iteration for ||Kt||_2 of the listed windows (generic path; the ELL kernel does its own on chip).
 hipError_t launch_power(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, const int32_t* list, int nlist,
                         hipStream_t s);

@@ -98,8 +98,8 @@ __global__ __launch_bounds__(kSetupB) void setup_kernel(const Batch b, const Wor
   double* KV = w.kval + W.wz;
   int32_t* rowof = w.rowof + W.wz;
   int32_t* perm = w.perm + W.wz;
-  double* Dr = w.dr + W.wm;
-  double* Dc = w.dc + W.wn;
+  double* gDr = w.dr + W.wm;
+  double* gDc = w.dc + W.wn;
   double* tmpr = w.tmpr + W.wm;
   double* tmpc = w.tmpc + W.wn;
   int32_t* longk = w.longk + (int64_t)kl * kLMax;
@@ -212,7 +212,11 @@ __global__ __launch_bounds__(kSetupB) void setup_kernel(const Batch b, const Wor
     }
     return;
   }
-  // 5. Ruiz (inf-norm) passes, then one Pock-Chambolle (alpha = 1) pass
+  // 5. Ruiz (inf-norm) passes, then one Pock-Chambolle (alpha = 1) pass.  Dr / Dc live in LDS from here on
+  //    (the transpose cursors are dead): the row / column passes gather Dc[Kc[p]] and Dr[Ti[p]] from LDS
+  //    instead of a dependent global load; copied to the workspace at the end.
+  double* Dr = reinterpret_cast<double*>(smem);
+  double* Dc = Dr + m;
   for (int j = tid; j < n; j += kSetupB) Dc[j] = 1.0;
   for (int i = tid; i < m; i += kSetupB) Dr[i] = 1.0;
   __syncthreads();
@@ -255,6 +259,8 @@ __global__ __launch_bounds__(kSetupB) void setup_kernel(const Batch b, const Wor
     nrm[1] += qi * d * qi * d;
     nrm[3] += qi * qi;
   }
+  for (int j = tid; j < n; j += kSetupB) gDc[j] = Dc[j];
+  for (int i = tid; i < m; i += kSetupB) gDr[i] = Dr[i];
   block_sum<kSetupB, 4>(nrm, red);
   // 8. row-length statistics for the ELL fast path: max length among rows with <= kEllMax entries and
   //    the number of longer rows, for K and K^T
@@ -1606,12 +1612,15 @@ hipError_t ell_dispatch_xy(int max_n, int max_m, const Batch& b, const Work& w, 
 }  // namespace
 
 int setup_segments(int max_n) { return max_n <= 8000 ? 4 : 1; }
-size_t setup_lds_bytes(int max_n) {
-  return align16(sizeof(int32_t) * (size_t)setup_segments(max_n) * ((size_t)max_n + 1));
+size_t setup_lds_bytes(int max_n, int max_m) {
+  // transpose cursors, later reused for Dr / Dc
+  return align16(std::max(sizeof(int32_t) * (size_t)setup_segments(max_n) * ((size_t)max_n + 1),
+                          sizeof(double) * ((size_t)max_n + (size_t)max_m)));
 }
 
-hipError_t launch_setup(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n, hipStream_t s) {
-  const size_t lds = setup_lds_bytes(max_n);
+hipError_t launch_setup(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n, int max_m,
+                        hipStream_t s) {
+  const size_t lds = setup_lds_bytes(max_n, max_m);
   Opts o2 = o;
   o2.setup_segments = setup_segments(max_n);
   hipError_t e = hipFuncSetAttribute((const void*)setup_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
