@@ -83,7 +83,9 @@ def main():
     t0 = time.time()
     sweep = None
     if args.schedule == "seeded":
-        sweep = SeededSweep(scenarios.config4, scen, scenarios.sweep_parameters(scen)["E"], stride=args.seed_stride)
+        P = scenarios.sweep_parameters(scen)
+        sweep = SeededSweep(scenarios.config4, scen, P["E"], stride=args.seed_stride,
+                            features=scenarios.sweep_features(P))
         pb = sweep.packed
     else:
         groups = scenarios.config4(scen)
@@ -215,7 +217,7 @@ def main():
                                "DCM + retailETS, T=672-744 h)",
                    "scenarios_per_gpu": S, "windows_per_gpu": count, "eps_rel_kkt": 1e-6, **opts,
                    "schedule": (f"seeded (1 in {args.seed_stride} scenarios cold, the rest warm from the nearest "
-                                f"seed; warm phase {WARM_OPTIONS})" if sweep is not None else "cold"),
+                                f"seed in (log E/load, duration, PV/load); warm phase {WARM_OPTIONS})" if sweep is not None else "cold"),
                    "parallelism": f"dp{world} (independent windows, 1 RCCL all-gather of results)"},
         "scenario_years_per_s": round(value / 12.0, 2),
         "iters_mean": round(float(iters.mean()), 1),

@@ -148,7 +148,8 @@ def main():
         ids = range(args.c4_scenarios)
         run("config4-slice", f"{args.c4_scenarios} scenarios x 12 monthly windows (bench.py runs 10,000)",
             P(scenarios.config4(ids)), s, args.reps, args.sample, args.procs)
-        sw = SeededSweep(scenarios.config4, ids, scenarios.sweep_parameters(ids)["E"], stride=32)
+        P4 = scenarios.sweep_parameters(ids)
+        sw = SeededSweep(scenarios.config4, ids, P4["E"], stride=32, features=scenarios.sweep_features(P4))
         run("config4-slice", f"{args.c4_scenarios} scenarios x 12 monthly windows, seeded schedule",
             sw.packed, s, args.reps, args.sample, args.procs, sweep=sw)
     if 5 in only:
@@ -156,7 +157,8 @@ def main():
         mk = lambda v: scenarios.config5(v, years=1)  # noqa: E731
         run("config5", f"{args.c5_scenarios} scenarios x 12 monthly windows of one opt year (x 20 years = 20 such "
                        f"batches)", P(mk(ids)), s, args.reps, args.sample, args.procs)
-        sw = SeededSweep(mk, ids, scenarios.sweep_parameters(ids)["E"], stride=32)
+        P5 = scenarios.sweep_parameters(ids)
+        sw = SeededSweep(mk, ids, P5["E"], stride=32, features=scenarios.sweep_features(P5))
         run("config5", f"{args.c5_scenarios} scenarios x 12 monthly windows of one opt year, seeded schedule",
             sw.packed, s, args.reps, args.sample, args.procs, sweep=sw)
 

@@ -138,6 +138,13 @@ def sweep_parameters(scenarios):
     return out
 
 
+def sweep_features(P):
+    """Similarity features of sweep scenarios (for dervet_hip.sweep's nearest-seed choice): battery energy
+    relative to load (log), battery duration, PV rating relative to load.  GPU study on 48,000 config-4 windows
+    (profiles/r01i_seeded_features*.log): warm windows 2,152 -> 2,023 iterations vs battery energy alone."""
+    return np.stack([np.log(P["E"] / P["load_scale"]), P["duration"], P["pv_rated"] / P["load_scale"]], axis=1)
+
+
 def config4(scenarios):
     """Synthetic sweep windows for the given scenario ids (12 monthly windows each)."""
     from scipy.signal import lfilter

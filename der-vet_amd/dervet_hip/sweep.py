@@ -24,10 +24,12 @@ import numpy as np
 from .packed import PackedBatch
 
 
-def seed_split(keys, stride):
+def seed_split(keys, stride, features=None):
     """Scenario positions -> (seed positions, rest positions, partner) with `partner[i]` the index into the
     seed list of rest position `rest[i]`'s nearest seed in key order.  Seeds are every `stride`-th scenario
-    in key order, starting at stride // 2 so that each seed sits in the middle of its neighbourhood."""
+    in key order, starting at stride // 2 so that each seed sits in the middle of its neighbourhood.
+    features [S, d] (optional): the partner is instead the nearest seed in these features (each standardised
+    to unit variance)."""
     keys = np.asarray(keys, np.float64)
     S = len(keys)
     stride = max(int(stride), 1)
@@ -42,7 +44,16 @@ def seed_split(keys, stride):
     near = np.clip(np.searchsorted(seed_pos, rest_pos), 0, len(seed_pos) - 1)
     left = np.clip(near - 1, 0, len(seed_pos) - 1)
     pick = np.where(np.abs(seed_pos[left] - rest_pos) <= np.abs(seed_pos[near] - rest_pos), left, near)
-    return order[seed_pos], order[rest_pos], pick
+    seeds, rest = order[seed_pos], order[rest_pos]
+    if features is not None:
+        f = np.asarray(features, np.float64).reshape(S, -1)
+        f = (f - f.mean(0)) / np.where(f.std(0) > 0, f.std(0), 1.0)
+        pick = np.empty(len(rest), np.int64)
+        fs = f[seeds]
+        for a in range(0, len(rest), 4096):  # blocked nearest-seed search
+            d = ((f[rest[a:a + 4096], None, :] - fs[None, :, :]) ** 2).sum(-1)
+            pick[a:a + 4096] = d.argmin(1)
+    return seeds, rest, pick
 
 
 # dvh_options for the warm phase: restart checks every 64 iterations, KKT every 2nd check (the cold default is
@@ -137,10 +148,10 @@ class SeededSweep:
     make_groups(scenario_ids) -> list of WindowGroup (e.g. ``scenarios.config4``); keys: similarity key per
     scenario (same order as `scenario_ids`)."""
 
-    def __init__(self, make_groups, scenario_ids, keys, stride=8):
+    def __init__(self, make_groups, scenario_ids, keys, stride=8, features=None):
         from .lp import builder
         ids = np.asarray(list(scenario_ids), np.int64)
-        seed_i, rest_i, pick = seed_split(keys, stride)
+        seed_i, rest_i, pick = seed_split(keys, stride, features)
         self.seed_ids, self.rest_ids = ids[seed_i], ids[rest_i]
         partner_of = {int(r): int(self.seed_ids[p]) for r, p in zip(self.rest_ids, pick)}
         sg = make_groups(self.seed_ids)

@@ -39,8 +39,23 @@ def main():
     print(f"cold: wall {cold_wall * 1e3:.1f} ms  setup {tm['setup_ms']:.1f}  pdhg {tm['pdhg_ms']:.1f}  "
           f"iters mean {ist[:, 1].mean():.1f}", flush=True)
     del dev
-    for stride in strides:
-        sw = SeededSweep(scenarios.config4, ids, keys, stride=stride)
+    P = scenarios.sweep_parameters(ids)
+    feats = {
+        "E": None,
+        "E/load,dur,rte,pv/load,dem/price": np.stack([np.log(P["E"] / P["load_scale"]), P["duration"], P["rte"],
+                                                      P["pv_rated"] / P["load_scale"],
+                                                      P["demand"] / P["price_scale"]], 1),
+        "E/load,dur,pv/load": np.stack([np.log(P["E"] / P["load_scale"]), P["duration"],
+                                        P["pv_rated"] / P["load_scale"]], 1),
+        "E/load,dur,pv/load,rte": np.stack([np.log(P["E"] / P["load_scale"]), P["duration"],
+                                            P["pv_rated"] / P["load_scale"], P["rte"]], 1),
+        "E/load,pv/load": np.stack([np.log(P["E"] / P["load_scale"]), P["pv_rated"] / P["load_scale"]], 1),
+    }
+    if os.environ.get("FEATS"):
+        feats = {k: v for k, v in feats.items() if k in os.environ["FEATS"].split(";")}
+    for stride, (fname, fv) in [(st, kv) for st in strides for kv in feats.items()]:
+        print(f"features: {fname}", flush=True)
+        sw = SeededSweep(scenarios.config4, ids, keys, stride=stride, features=fv)
         d2 = sw.packed.to_torch("cuda:0").alloc_outputs()
         sw.solve(s, d2)
         torch.cuda.synchronize()

@@ -94,3 +94,14 @@ def test_seeded_sweep_on_gpu_matches_cold_and_highs():
         h = window_lp.solve_highs(window_lp.from_packed_window(sw.packed.window(k)))
         assert abs(st[k, 0] - h["obj"]) <= 1e-5 * max(abs(h["obj"]), 1.0), (k, st[k, 0], h["obj"])
         assert st[k, 1] <= 1e-6
+
+
+def test_seed_split_feature_partners_are_nearest_in_standardised_features():
+    rng = np.random.default_rng(5)
+    keys = rng.uniform(0, 1, 300)
+    feats = np.stack([rng.normal(0, 10, 300), rng.normal(0, 0.1, 300)], 1)
+    seeds, rest, pick = seed_split(keys, 16, feats)
+    f = (feats - feats.mean(0)) / feats.std(0)
+    for r, p in zip(rest, pick):
+        d = ((f[seeds] - f[r]) ** 2).sum(1)
+        assert d[p] == d.min()
