@@ -81,7 +81,8 @@ def run(name, note, pb, solver, reps, sample, procs, sweep=None):
     return line
 
 
-def stitched(long, subs, solver, reps):
+def stitched(long, subs, solver, reps, name="config3",
+             note="5-min annual window, DA, started from its 365 daily windows (one batched solve)"):
     """Config 3 started from its 365 daily windows (dervet_hip/stitch.py): wall time of the whole call
     (daily batch + stitch + long window, host buffers in and out)."""
     from dervet_hip.stitch import solve_stitched
@@ -96,8 +97,7 @@ def stitched(long, subs, solver, reps):
     res, tm = keep
     lp = window_lp.from_packed_window(__import__("dervet_hip.lp.builder", fromlist=["x"]).pack_groups([long]).window(0))
     h = window_lp.solve_highs(lp)
-    line = {"config": "config3", "workload": "5-min annual window, DA, started from its 365 daily windows "
-                                             "(one batched solve) -- host buffers in / out",
+    line = {"config": name, "workload": note + " -- host buffers in / out", "sub_windows": len(subs),
             "schedule": "stitched", "windows": 1, "wall_ms": round(best * 1e3, 2),
             "windows_per_s": round(1.0 / best, 2), "kernel_ms": {k: round(v, 2) for k, v in tm.items()},
             "iters": res.iters, "status": res.status_name,
@@ -144,6 +144,13 @@ def main():
                                         scenarios.template_battery(), da_price=ri["fivemin_da_price"][None, :],
                                         tariff_def=scenarios.tariff(), n="year")
         run("config3+dcm", "5-min annual window, DA + retailETS + 12 monthly DCM charges", P(g), s, args.reps, 0, 1)
+        for sub in (288,):  # measured: slower than cold for this variant; monthly subs: 2.9 s
+            stitched(g[0], scenarios.windows_by_period(2019, 1.0 / 12, ri["fivemin_site_load"][None, :], None,
+                                                       scenarios.template_battery(),
+                                                       da_price=ri["fivemin_da_price"][None, :],
+                                                       tariff_def=scenarios.tariff(), n=sub), s, args.reps,
+                     name="config3+dcm", note=f"5-min annual window, DA + retailETS + 12 monthly DCM, started from "
+                                              f"its {'daily' if sub == 288 else 'monthly'} windows")
     if 4 in only:
         ids = range(args.c4_scenarios)
         run("config4-slice", f"{args.c4_scenarios} scenarios x 12 monthly windows (bench.py runs 10,000)",

@@ -24,12 +24,13 @@ import numpy as np
 from .packed import PackedBatch
 
 
-def seed_split(keys, stride, features=None):
+def seed_split(keys, stride, features=None, cover=False):
     """Scenario positions -> (seed positions, rest positions, partner) with `partner[i]` the index into the
     seed list of rest position `rest[i]`'s nearest seed in key order.  Seeds are every `stride`-th scenario
     in key order, starting at stride // 2 so that each seed sits in the middle of its neighbourhood.
     features [S, d] (optional): the partner is instead the nearest seed in these features (each standardised
-    to unit variance)."""
+    to unit variance); with cover=True the seeds themselves are chosen by greedy farthest-point sampling in
+    those features."""
     keys = np.asarray(keys, np.float64)
     S = len(keys)
     stride = max(int(stride), 1)
@@ -48,6 +49,18 @@ def seed_split(keys, stride, features=None):
     if features is not None:
         f = np.asarray(features, np.float64).reshape(S, -1)
         f = (f - f.mean(0)) / np.where(f.std(0) > 0, f.std(0), 1.0)
+        if cover:  # greedy farthest-point seeds in feature space (same count), starting at the key-order seed
+            ns = len(seeds)
+            sel = [int(seeds[0])]
+            dmin = ((f - f[sel[0]]) ** 2).sum(1)
+            for _ in range(ns - 1):
+                j = int(dmin.argmax())
+                sel.append(j)
+                dmin = np.minimum(dmin, ((f - f[j]) ** 2).sum(1))
+            seeds = np.array(sel, np.int64)
+            mask = np.ones(S, bool)
+            mask[seeds] = False
+            rest = np.nonzero(mask)[0]
         pick = np.empty(len(rest), np.int64)
         fs = f[seeds]
         for a in range(0, len(rest), 4096):  # blocked nearest-seed search
@@ -148,10 +161,10 @@ class SeededSweep:
     make_groups(scenario_ids) -> list of WindowGroup (e.g. ``scenarios.config4``); keys: similarity key per
     scenario (same order as `scenario_ids`)."""
 
-    def __init__(self, make_groups, scenario_ids, keys, stride=8, features=None):
+    def __init__(self, make_groups, scenario_ids, keys, stride=8, features=None, cover=False):
         from .lp import builder
         ids = np.asarray(list(scenario_ids), np.int64)
-        seed_i, rest_i, pick = seed_split(keys, stride, features)
+        seed_i, rest_i, pick = seed_split(keys, stride, features, cover)
         self.seed_ids, self.rest_ids = ids[seed_i], ids[rest_i]
         partner_of = {int(r): int(self.seed_ids[p]) for r, p in zip(self.rest_ids, pick)}
         sg = make_groups(self.seed_ids)

@@ -55,7 +55,8 @@ def main():
         feats = {k: v for k, v in feats.items() if k in os.environ["FEATS"].split(";")}
     for stride, (fname, fv) in [(st, kv) for st in strides for kv in feats.items()]:
         print(f"features: {fname}", flush=True)
-        sw = SeededSweep(scenarios.config4, ids, keys, stride=stride, features=fv)
+        sw = SeededSweep(scenarios.config4, ids, keys, stride=stride, features=fv,
+                         cover=bool(int(os.environ.get("COVER", "0"))))
         d2 = sw.packed.to_torch("cuda:0").alloc_outputs()
         sw.solve(s, d2)
         torch.cuda.synchronize()
