@@ -234,9 +234,20 @@ __global__ __launch_bounds__(kSetupB) void setup_kernel(const Batch b, const Wor
       rows_reduce<true>(Tp, n, longt, nlt, fc, gc);
     }
     __syncthreads();
-    for (int j = tid; j < n; j += kSetupB) Dc[j] *= tmpc[j];
-    for (int i = tid; i < m; i += kSetupB) Dr[i] *= tmpr[i];
-    __syncthreads();
+    int changed = 0;
+    for (int j = tid; j < n; j += kSetupB) {
+      const double t = tmpc[j];
+      changed |= t != 1.0;
+      Dc[j] *= t;
+    }
+    for (int i = tid; i < m; i += kSetupB) {
+      const double t = tmpr[i];
+      changed |= t != 1.0;
+      Dr[i] *= t;
+    }
+    // A Ruiz pass whose factors are all exactly 1 left Dr / Dc unchanged, so every further Ruiz pass would
+    // repeat it bit for bit: skip to the Pock-Chambolle pass (same result, fewer passes).
+    if (__syncthreads_or(changed) == 0 && !pc) pass = o.ruiz_iters - 1;
   }
   // 6. scaled data
   for (int p = tid; p < nnz; p += kSetupB) {

@@ -15,23 +15,20 @@ from dervet_hip.lp import scenarios  # noqa: E402
 from dervet_hip.sweep import SeededSweep  # noqa: E402
 
 VARIANTS = [
-    {},
-    {"check_every": 64},
-    {"check_every": 64, "restart_artificial": 0.2},
     {"check_every": 64, "kkt_every": 2},
-    {"check_every": 64, "kkt_every": 3, "restart_artificial": 0.2},
-    {"check_every": 48},
-    {"check_every": 48, "restart_artificial": 0.2},
-    {"check_every": 96, "kkt_every": 2},
-    {"check_every": 128, "kkt_every": 1},
-    {"restart_artificial": 0.3},
+    {"check_every": 64, "kkt_every": 2, "power_iters": 48},
+    {"check_every": 64, "kkt_every": 2, "power_iters": 32},
+    {"check_every": 64, "kkt_every": 2, "power_iters": 16},
+    {"check_every": 64, "kkt_every": 2, "ruiz_iters": 5},
+    {"check_every": 64, "kkt_every": 2, "restart_sufficient": 0.15},
 ]
 
 
 def main():
     S = int(sys.argv[1]) if len(sys.argv) > 1 else 4000
     ids = np.arange(S)
-    sw = SeededSweep(scenarios.config4, ids, scenarios.sweep_parameters(ids)["E"], stride=32)
+    P = scenarios.sweep_parameters(ids)
+    sw = SeededSweep(scenarios.config4, ids, P["E"], stride=32, features=scenarios.sweep_features(P))
     dev = sw.packed.to_torch("cuda:0").alloc_outputs()
     s = BatchSolver(0)
     ns = sw.n_seed
