@@ -32,6 +32,9 @@ import torch  # noqa: E402
 
 METRIC = "dispatch LP windows/sec (whole node, 8760h monthly windows); % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# VALU issue peak: 256 CUs x 4 SIMDs x 2.4 GHz, one wave instruction per 2 cycles per SIMD (MI355X_MICROARCH.md:
+# "issues each VALU instruction over 2 cycles"); FP64 FMA / ADD / MUL issue at half that (78.6 TF FP64 vector)
+VALU_PEAK_WAVE_INSTS = 256 * 4 * 2.4e9 / 2
 
 
 def alg_bytes_per_iter(desc):
@@ -158,6 +161,26 @@ def main():
             if tj.get("kernel", "").startswith(kname.split()[0]) and tj.get("launches_per_step", 1) == lps:
                 traffic = tj.get("hbm_bytes_per_step", tj.get("hbm_bytes_per_launch"))
 
+    # the kernel's actual bound: VALU issue (PMC SQ_INSTS_VALU of one step's PDHG launches, profiles/pdhg_valu.json)
+    compute = None
+    vf = os.path.join(ROOT, "profiles", "pdhg_valu.json")
+    if os.path.exists(vf) and achieved:
+        with open(vf) as f:
+            vj = json.load(f)
+        lps = 2 if sweep is not None and count > sweep.n_seed else 1
+        if vj.get("windows") == count and vj.get("dispatches_per_step") == lps:
+            cps = vj["counters_per_step"]
+            valu = cps.get("SQ_INSTS_VALU")
+            if valu:
+                compute = {"bound": "valu", "achieved": valu / pdhg_s, "peak": VALU_PEAK_WAVE_INSTS,
+                           "unit": "VALU wave-instructions/s", "frac": round(valu / pdhg_s / VALU_PEAK_WAVE_INSTS, 3),
+                           "valu_per_window_iteration": round(valu / float(iters.sum()), 1),
+                           "salu_per_window_iteration": round(cps.get("SQ_INSTS_SALU", 0.0) / float(iters.sum()), 1),
+                           "lds_per_window_iteration": round(cps.get("SQ_INSTS_LDS", 0.0) / float(iters.sum()), 1),
+                           "note": "PMC pass over one step (profiles/pdhg_valu.json, same schedule and batch); peak = "
+                                   "one VALU wave-instruction per 2 cycles per SIMD at 2.4 GHz; FP64 FMA / ADD / MUL "
+                                   "issue at half that rate"}
+
     schedule = {"kind": args.schedule}
     if sweep is not None:
         ns = sweep.n_seed
@@ -239,6 +262,7 @@ def main():
                                "(HIP events on the solver stream)",
                      "note": "iterate and scaled K are VGPR/LDS-resident, so algorithmic bytes exceed what HBM "
                              "moves; frac > 1 means the on-chip design beats the HBM roofline"},
+        "compute": compute,
         "schedule": schedule,
         "cpu_baseline": cpu,
         "parity": parity,
