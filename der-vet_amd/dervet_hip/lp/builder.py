@@ -229,7 +229,7 @@ def _assemble(G, m, blocks):
 
 
 def market_group(T, dt, bat, da_price, fr, base=None, ene_min=None, ene_max=None, binary_relax=False, name="es",
-                 tags=None):
+                 tags=None, reserves=None):
     """G windows of battery dispatch with the DA energy term and frequency-regulation reservations (storagevet
     MarketServiceUpAndDown / FrequencyRegulation + EnergyStorage).  Formulation and
     row order as oracle/window_lp.py (pinned to the Usecase 3 goldens: with binaries the restatement reproduces
@@ -244,7 +244,17 @@ def market_group(T, dt, bat, da_price, fr, base=None, ene_min=None, ene_max=None
 
     da_price [G, T]; base [G, T] = load - fixed generation (kW) of the DA net term (zeros: incl_site_load = 0);
     fr: dict eou, eod (scalars), regu_price, regd_price, fr_price [G, T], optional regu_max, regu_min, regd_max,
-    regd_min [G, T], combined (bool)."""
+    regd_min [G, T], combined (bool).
+
+    reserves (optional, parity unpinned): upward-only reserve services (spinning / non-spinning reserve, storagevet
+    MarketServiceUp via SpinningReserve / NonspinningReserve, registered at dervet/MicrogridScenario.py:93-94; the
+    reference ships no golden result with them active), a list of dicts key ('SR' / 'NSR'), price [G, T] ($/kW),
+    duration (h, template column SR/NSR duration), optional max / min [G, T] (ts_constraints).  Each adds
+    x blocks [ch_less, dis_more] (T each, >= 0) after the FR blocks; ch_less joins the "ch - up_ch >= 0" row and
+    dis_more the "P_dis - dis - up_dis >= 0" row (one shared headroom for every upward service); with a duration
+    > 0 one more >= row per step, ene - sum_k duration_k dis_more_k >= lower SOE bound (the energy held back to
+    sustain the extra discharge); objective key '<key>' = -price (ch_less + dis_more), per kW like regup_prof.
+    Without reserves the LP is exactly the pinned DA + FR window."""
     da_price = np.atleast_2d(np.asarray(da_price, np.float64))
     G = da_price.shape[0]
     base = np.zeros((G, T)) if base is None else _col(base, G, T)
@@ -255,7 +265,9 @@ def market_group(T, dt, bat, da_price, fr, base=None, ene_min=None, ene_max=None
     eou, eod = float(fr["eou"]), float(fr["eod"])
     combined = bool(fr.get("combined", False))
     ich, idis, iene, iuc, iud, idc, idd = (k * T for k in range(7))
-    n = 7 * T
+    res = list(reserves or [])
+    ires = [((7 + 2 * k) * T, (8 + 2 * k) * T) for k in range(len(res))]  # (ch_less, dis_more) offsets
+    n = (7 + 2 * len(res)) * T
     t = np.arange(T)
     tt = t[:-1]
     one = np.ones((G, 1))
@@ -292,8 +304,8 @@ def market_group(T, dt, bat, da_price, fr, base=None, ene_min=None, ene_max=None
         m += T
 
     ge([(ich, -1.0), (idc, -1.0)], -pch[:, None])
-    ge([(idis, -1.0), (iud, -1.0)], -pdis[:, None])
-    ge([(ich, 1.0), (iuc, -1.0)], 0.0)
+    ge([(idis, -1.0), (iud, -1.0)] + [(idm, -1.0) for _, idm in ires], -pdis[:, None])
+    ge([(ich, 1.0), (iuc, -1.0)] + [(icl, -1.0) for icl, _ in ires], 0.0)
     ge([(idis, 1.0), (idd, -1.0)], 0.0)
     ge([(iuc, ((1.0 - eta) * eou)[:, None]), (idc, (-(1.0 - eta) * eod)[:, None]), (iud, 2.0 * eou),
         (idd, -2.0 * eod)], 0.0)
@@ -311,6 +323,19 @@ def market_group(T, dt, bat, da_price, fr, base=None, ene_min=None, ene_max=None
         ge([(idc, 1.0), (idd, 1.0)], _col(fr["regd_min"], G, T))
     if binary_relax:
         ge([(ich, (-1.0 / pch)[:, None]), (idis, (-1.0 / pdis)[:, None])], -1.0)
+    lo = (_col(bat.get("llsoc", 0.0), G) * E)[:, None] * np.ones((1, T))
+    hi = (_col(bat.get("ulsoc", 1.0), G) * E)[:, None] * np.ones((1, T))
+    if ene_min is not None:
+        lo = np.maximum(lo, _col(ene_min, G, T))
+    if ene_max is not None:
+        hi = np.minimum(hi, _col(ene_max, G, T))
+    for rv, (icl, idm) in zip(res, ires):  # reserve participation limits (ts_constraints), clamped as FR's
+        if rv.get("max") is not None:
+            ge([(icl, -1.0), (idm, -1.0)], -np.minimum(_col(rv["max"], G, T), cap))
+            ge([(icl, 1.0), (idm, 1.0)], _col(rv["min"], G, T))
+    dur = [float(rv.get("duration", 0.0)) for rv in res]
+    if any(d > 0.0 for d in dur):
+        ge([(iene, 1.0)] + [(idm, -d) for d, (_, idm) in zip(dur, ires) if d > 0.0], lo)
     indptr, indices, data = _assemble(G, m, blocks)
     q = np.concatenate(q_eq + q_ge, axis=1)
 
@@ -318,12 +343,6 @@ def market_group(T, dt, bat, da_price, fr, base=None, ene_min=None, ene_max=None
     u = np.full((G, n), np.inf)
     u[:, ich:ich + T] = pch[:, None]
     u[:, idis:idis + T] = pdis[:, None]
-    lo = (_col(bat.get("llsoc", 0.0), G) * E)[:, None] * np.ones((1, T))
-    hi = (_col(bat.get("ulsoc", 1.0), G) * E)[:, None] * np.ones((1, T))
-    if ene_min is not None:
-        lo = np.maximum(lo, _col(ene_min, G, T))
-    if ene_max is not None:
-        hi = np.minimum(hi, _col(ene_max, G, T))
     l[:, iene:iene + T] = lo
     u[:, iene:iene + T] = hi
 
@@ -347,6 +366,12 @@ def market_group(T, dt, bat, da_price, fr, base=None, ene_min=None, ene_max=None
     coef[:, idc:idc + T] = pe * dt * eod
     coef[:, idd:idd + T] = pe * dt * eod
     terms["fr_energy_settlement"] = (coef, np.zeros(G))
+    for rv, (icl, idm) in zip(res, ires):
+        coef = np.zeros((G, n))
+        pr = _col(rv["price"], G, T)
+        coef[:, icl:icl + T] = -pr
+        coef[:, idm:idm + T] = -pr
+        terms[str(rv["key"])] = (coef, np.zeros(G))
     terms[f"{name} fixed_om"] = (np.zeros((G, n)), _col(bat.get("fixedOM", 0.0), G) * pdis)
     coef = np.zeros((G, n))
     coef[:, idis:idis + T] = (_col(bat.get("OMexpenses", 0.0), G) / 1000.0 * dt)[:, None]

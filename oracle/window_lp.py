@@ -28,6 +28,11 @@ DER / value-stream set:
     fr_energy_settlement = sum p_fr dt (eod (down_ch + down_dis) - eou (up_ch + up_dis))
   binary = 1 windows, opt-in LP relaxation: on_c + on_d <= 1 with ch <= P_ch on_c, dis <= P_dis on_d
   (ch_min = dis_min = 0) projects to  ch / P_ch + dis / P_dis <= 1.
+  upward reserves (PARITY UNPINNED: storagevet MarketServiceUp / SpinningReserve / NonspinningReserve, registered at
+  dervet/MicrogridScenario.py:93-94, are absent and no reference result has SR / NSR active): per service k
+  ch_less_k, dis_more_k >= 0;  up_ch + sum_k ch_less_k <= ch;  dis + up_dis + sum_k dis_more_k <= P_dis;
+  ts_constraints min_k <= ch_less_k + dis_more_k <= max_k;  duration d_k > 0: ene_t - sum_k d_k dis_more_k >= lower
+  SOE bound;  objective key k = -sum price_k (ch_less_k + dis_more_k).
 
 Variable order: [ch(T), dis(T), ene(T), tau(J), pv(T)?, elec(T)?, on(T)?, up_ch, up_dis, down_ch, down_dis (T
 each)?].  Rows: equalities (init, recurrence, final, CombinedMarket) then >= rows (DCM, ICE, FR, relaxation).
@@ -73,6 +78,11 @@ def build(win):
         for k in ("uc", "ud", "dc", "dd"):
             off[k] = n
             n += T
+    reserves = list(win.get("reserves") or [])
+    assert not reserves or fr is not None, "reserves ride on the market window (fr)"
+    for i in range(len(reserves)):
+        off[f"cl{i}"], off[f"dm{i}"] = n, n + T
+        n += 2 * T
     hp = float(b.get("hp", 0.0))
     base = np.asarray(win["load"], float) - np.asarray(win.get("gen", np.zeros(T)), float) + hp
 
@@ -148,8 +158,10 @@ def build(win):
                 q.append(float(rhs[t]))
                 r += 1
         ge_rows([("ch", -1.0), ("dc", -1.0)], np.full(T, -pch))    # ch + down_ch <= P_ch
-        ge_rows([("dis", -1.0), ("ud", -1.0)], np.full(T, -pdis))  # dis + up_dis <= P_dis
-        ge_rows([("ch", 1.0), ("uc", -1.0)], np.zeros(T))          # up_ch <= ch
+        ge_rows([("dis", -1.0), ("ud", -1.0)] + [(f"dm{i}", -1.0) for i in range(len(reserves))],
+                np.full(T, -pdis))                                 # dis + up_dis + sum dis_more <= P_dis
+        ge_rows([("ch", 1.0), ("uc", -1.0)] + [(f"cl{i}", -1.0) for i in range(len(reserves))],
+                np.zeros(T))                                       # up_ch + sum ch_less <= ch
         ge_rows([("dis", 1.0), ("dd", -1.0)], np.zeros(T))         # down_dis <= dis
         eou, eod = float(fr["eou"]), float(fr["eod"])
         ge_rows([("uc", (1.0 - eta) * eou), ("dc", -(1.0 - eta) * eod), ("ud", 2.0 * eou), ("dd", -2.0 * eod)],
@@ -165,6 +177,19 @@ def build(win):
             rows += [r, r]; cols += [off["ch"] + t, off["dis"] + t]; vals += [-1.0 / pch, -1.0 / pdis]
             q.append(-1.0)
             r += 1
+    elo = np.full(T, float(b.get("llsoc", 0.0)) * E)
+    ehi = np.full(T, float(b.get("ulsoc", 1.0)) * E)
+    if win.get("ene_min") is not None:
+        elo = np.maximum(elo, np.asarray(win["ene_min"], float))
+    if win.get("ene_max") is not None:
+        ehi = np.minimum(ehi, np.asarray(win["ene_max"], float))
+    for i, rv in enumerate(reserves):
+        if rv.get("max") is not None:
+            ge_rows([(f"cl{i}", -1.0), (f"dm{i}", -1.0)], -np.asarray(rv["max"], float))
+            ge_rows([(f"cl{i}", 1.0), (f"dm{i}", 1.0)], np.asarray(rv["min"], float))
+    if any(float(rv.get("duration", 0.0)) > 0.0 for rv in reserves):
+        ge_rows([("ene", 1.0)] + [(f"dm{i}", -float(rv["duration"])) for i, rv in enumerate(reserves)
+                                  if float(rv.get("duration", 0.0)) > 0.0], elo)
     m = r
     K = sp.csr_matrix((vals, (rows, cols)), shape=(m, n))
     K.sum_duplicates()
@@ -173,12 +198,6 @@ def build(win):
     hi = np.full(n, np.inf)
     hi[off["ch"]:off["ch"] + T] = pch
     hi[off["dis"]:off["dis"] + T] = pdis
-    elo = np.full(T, float(b.get("llsoc", 0.0)) * E)
-    ehi = np.full(T, float(b.get("ulsoc", 1.0)) * E)
-    if win.get("ene_min") is not None:
-        elo = np.maximum(elo, np.asarray(win["ene_min"], float))
-    if win.get("ene_max") is not None:
-        ehi = np.minimum(ehi, np.asarray(win["ene_max"], float))
     lo[off["ene"]:off["ene"] + T] = elo
     hi[off["ene"]:off["ene"] + T] = ehi
     lo[off["tau"]:off["tau"] + J] = -np.inf
@@ -224,6 +243,11 @@ def build(win):
         for k in ("dc", "dd"):
             coef[off[k]:off[k] + T] = pe * dt * eod
         funcs["fr_energy_settlement"] = (coef, 0.0)
+    for i, rv in enumerate(reserves):
+        coef = np.zeros(n)
+        coef[off[f"cl{i}"]:off[f"cl{i}"] + T] = -np.asarray(rv["price"], float)
+        coef[off[f"dm{i}"]:off[f"dm{i}"] + T] = -np.asarray(rv["price"], float)
+        funcs[str(rv["key"])] = (coef, 0.0)
     name = b.get("name", "es")
     funcs[f"{name} fixed_om"] = (np.zeros(n), float(b.get("fixedOM", 0.0)) * pdis)
     coef = np.zeros(n)
