@@ -11,11 +11,14 @@ config-4 slice for comparison).
   config 5  battery + PV + LP-relaxed ICE + 4-h reliability min-SOE, --c5-scenarios scenarios x 12 monthly windows
             per opt year; the 20-year horizon is 20 independent year batches of the same shape (the horizon's
             windows do not couple), so one year batch resident in HBM is the timed unit
+  market    (`--only 6`) Usecase 3 daily DA + FR windows of the three golden cases (3 x 365), and
+            the same days with load following + spinning / non-spinning reserve added (synthetic LF / SR / NSR
+            prices from the fixture's Reg Up / Down prices; parity unpinned beyond HiGHS on the same LP)
 
 For every config: windows, wall time of a solve with the batch resident in HBM (best of --reps after one
 warm-up), windows/s, iterations, kernel path, and parity on a sample against HiGHS on the restated LP
 (oracle/window_lp.py; objective rel error, and the primal residual recomputed from the returned x).
-Usage: python bench_configs.py [--only 1,2,3,4,5] [--c4-scenarios 2000] [--c5-scenarios 1000]
+Usage: python bench_configs.py [--only 1,2,3,4,5,6] [--c4-scenarios 2000] [--c5-scenarios 1000]
 """
 import argparse
 import json
@@ -159,6 +162,31 @@ def main():
         sw = SeededSweep(scenarios.config4, ids, P4["E"], stride=32, features=scenarios.sweep_features(P4))
         run("config4-slice", f"{args.c4_scenarios} scenarios x 12 monthly windows, seeded schedule",
             sw.packed, s, args.reps, args.sample, args.procs, sweep=sw)
+    if 6 in only:
+        import json as _json
+        gold = os.path.join(ROOT, "tests", "golden")
+        arr = dict(np.load(os.path.join(gold, "uc3_market.npz")))
+        with open(os.path.join(gold, "uc3_market.json")) as f:
+            meta = _json.load(f)
+        names = ("es", "es+pv", "es+pv+dg")
+        sigs = {nm: {k.split("__", 1)[1]: v for k, v in arr.items() if k.startswith(nm + "__")} for nm in names}
+        run("market-uc3", "Usecase 3 daily DA + FR windows, 3 golden cases x 365 days (LP relaxation of binary = 1)",
+            P([scenarios.market_days(sigs[nm], meta[nm]["params"]) for nm in names]), s, args.reps, args.sample,
+            args.procs)
+        groups = []
+        for nm in names:
+            sg, pdis = sigs[nm], float(meta[nm]["params"]["Battery"]["dis_max_rated"])
+            N = len(sg["da_price"])
+            h = np.arange(N)
+            res = [dict(key="SR", price=0.6 * sg["regu_price"], duration=0.5, max=np.full(N, 0.5 * pdis),
+                        min=np.zeros(N)), dict(key="NSR", price=0.3 * sg["regu_price"], duration=1.0)]
+            lf = dict(eou=0.2 + 0.05 * np.sin(h / 7.0), eod=0.2 + 0.05 * np.cos(h / 5.0),
+                      up_price=0.8 * sg["regu_price"], down_price=0.8 * sg["regd_price"], energy_price=sg["da_price"],
+                      up_max=np.full(N, 0.25 * pdis), up_min=np.zeros(N), down_max=np.full(N, 0.25 * pdis),
+                      down_min=np.zeros(N), combined=False)
+            groups.append(scenarios.market_days(sg, meta[nm]["params"], reserves=res, lf=lf))
+        run("market-uc3+lf+sr+nsr", "the same 3 x 365 days with load following + SR + NSR (synthetic prices)",
+            P(groups), s, args.reps, args.sample, args.procs)
     if 5 in only:
         ids = range(args.c5_scenarios)
         mk = lambda v: scenarios.config5(v, years=1)  # noqa: E731

@@ -229,7 +229,7 @@ def _assemble(G, m, blocks):
 
 
 def market_group(T, dt, bat, da_price, fr, base=None, ene_min=None, ene_max=None, binary_relax=False, name="es",
-                 tags=None, reserves=None):
+                 tags=None, reserves=None, lf=None):
     """G windows of battery dispatch with the DA energy term and frequency-regulation reservations (storagevet
     MarketServiceUpAndDown / FrequencyRegulation + EnergyStorage).  Formulation and
     row order as oracle/window_lp.py (pinned to the Usecase 3 goldens: with binaries the restatement reproduces
@@ -254,7 +254,13 @@ def market_group(T, dt, bat, da_price, fr, base=None, ene_min=None, ene_max=None
     dis_more the "P_dis - dis - up_dis >= 0" row (one shared headroom for every upward service); with a duration
     > 0 one more >= row per step, ene - sum_k duration_k dis_more_k >= lower SOE bound (the energy held back to
     sustain the extra discharge); objective key '<key>' = -price (ch_less + dis_more), per kW like regup_prof.
-    Without reserves the LP is exactly the pinned DA + FR window."""
+    lf (optional, parity unpinned): load following (storagevet LoadFollowing, a MarketServiceUpAndDown like FR;
+    dervet/MicrogridScenario.py:92), dict eou, eod ([G, T] or scalar: template columns "LF Energy Option Up / Down
+    (kWh/kW-hr)"), up_price, down_price, energy_price [G, T], optional up_max, up_min, down_max, down_min [G, T],
+    combined.  x blocks [lf_up_ch, lf_up_dis, lf_down_ch, lf_down_dis] after the reserve blocks; its options join
+    FR's in the SOE recurrence, the four headroom rows and the option-consistency row; keys 'lf_up_prof',
+    'lf_down_prof', 'lf_energy_settlement' as FR's.
+    Without reserves / lf the LP is exactly the pinned DA + FR window."""
     da_price = np.atleast_2d(np.asarray(da_price, np.float64))
     G = da_price.shape[0]
     base = np.zeros((G, T)) if base is None else _col(base, G, T)
@@ -268,6 +274,11 @@ def market_group(T, dt, bat, da_price, fr, base=None, ene_min=None, ene_max=None
     res = list(reserves or [])
     ires = [((7 + 2 * k) * T, (8 + 2 * k) * T) for k in range(len(res))]  # (ch_less, dis_more) offsets
     n = (7 + 2 * len(res)) * T
+    luc = lud = ldc = ldd = -1  # load-following blocks (lf)
+    if lf is not None:
+        luc, lud, ldc, ldd = (n + k * T for k in range(4))
+        n += 4 * T
+        LEU, LED = _col(lf["eou"], G, T), _col(lf["eod"], G, T)
     t = np.arange(T)
     tt = t[:-1]
     one = np.ones((G, 1))
@@ -280,16 +291,29 @@ def market_group(T, dt, bat, da_price, fr, base=None, ene_min=None, ene_max=None
                    (idis + tt, dt * one), (iuc + tt, -dt * eou * eta[:, None]), (idc + tt, dt * eod * eta[:, None]),
                    (iud + tt, dt * eou * one), (idd + tt, -dt * eod * one)):
         blocks.append((r, c0_, v * np.ones((1, len(tt)))))
+    if lf is not None:
+        for c0_, v in ((luc + tt, -dt * LEU[:, tt] * eta[:, None]), (ldc + tt, dt * LED[:, tt] * eta[:, None]),
+                       (lud + tt, dt * LEU[:, tt]), (ldd + tt, -dt * LED[:, tt])):
+            blocks.append((r, c0_, v))
     # final row: (1 - dt sdr) ene + dt eta ch - dt dis + dt (eta uch - udis) = target   (step T-1)
     k = T - 1
     for c0_, v in ((iene + k, 1.0 - dt * sdr), (ich + k, dt * eta), (idis + k, -dt * np.ones(G)),
                    (iuc + k, dt * eou * eta), (idc + k, -dt * eod * eta), (iud + k, -dt * eou * np.ones(G)),
                    (idd + k, dt * eod * np.ones(G))):
         blocks.append(([T], [c0_], np.asarray(v).reshape(G, 1)))
+    if lf is not None:
+        for c0_, v in ((luc + k, dt * LEU[:, k] * eta), (ldc + k, -dt * LED[:, k] * eta), (lud + k, -dt * LEU[:, k]),
+                       (ldd + k, dt * LED[:, k])):
+            blocks.append(([T], [c0_], np.asarray(v).reshape(G, 1)))
     m = T + 1
     q_eq = [target[:, None], np.zeros((G, T - 1)), target[:, None]]
     if combined:
         for c0_, v in ((iuc, 1.0), (iud, 1.0), (idc, -1.0), (idd, -1.0)):
+            blocks.append((m + t, c0_ + t, np.full((G, T), v)))
+        q_eq.append(np.zeros((G, T)))
+        m += T
+    if lf is not None and lf.get("combined"):
+        for c0_, v in ((luc, 1.0), (lud, 1.0), (ldc, -1.0), (ldd, -1.0)):
             blocks.append((m + t, c0_ + t, np.full((G, T), v)))
         q_eq.append(np.zeros((G, T)))
         m += T
@@ -303,12 +327,14 @@ def market_group(T, dt, bat, da_price, fr, base=None, ene_min=None, ene_max=None
         q_ge.append(np.broadcast_to(np.asarray(rhs, np.float64), (G, T)))
         m += T
 
-    ge([(ich, -1.0), (idc, -1.0)], -pch[:, None])
-    ge([(idis, -1.0), (iud, -1.0)] + [(idm, -1.0) for _, idm in ires], -pdis[:, None])
-    ge([(ich, 1.0), (iuc, -1.0)] + [(icl, -1.0) for icl, _ in ires], 0.0)
-    ge([(idis, 1.0), (idd, -1.0)], 0.0)
+    xl = (lambda e: [e]) if lf is not None else (lambda e: [])  # LF's entries in the shared rows
+    ge([(ich, -1.0), (idc, -1.0)] + xl((ldc, -1.0)), -pch[:, None])
+    ge([(idis, -1.0), (iud, -1.0)] + xl((lud, -1.0)) + [(idm, -1.0) for _, idm in ires], -pdis[:, None])
+    ge([(ich, 1.0), (iuc, -1.0)] + xl((luc, -1.0)) + [(icl, -1.0) for icl, _ in ires], 0.0)
+    ge([(idis, 1.0), (idd, -1.0)] + xl((ldd, -1.0)), 0.0)
     ge([(iuc, ((1.0 - eta) * eou)[:, None]), (idc, (-(1.0 - eta) * eod)[:, None]), (iud, 2.0 * eou),
-        (idd, -2.0 * eod)], 0.0)
+        (idd, -2.0 * eod)] + ([(luc, (1.0 - eta)[:, None] * LEU), (ldc, -(1.0 - eta)[:, None] * LED),
+                                (lud, 2.0 * LEU), (ldd, -2.0 * LED)] if lf is not None else []), 0.0)
     # The other rows already imply up_ch + up_dis <= P_ch + P_dis and down_ch + down_dis <= P_ch + P_dis
     # (up_ch <= ch <= P_ch - down_ch, up_dis <= P_dis - dis; down_ch <= P_ch - ch, down_dis <= dis <= P_dis),
     # so a u/d_ts maximum above that is clamped to it: the same feasible set, but without the reference's
@@ -333,6 +359,13 @@ def market_group(T, dt, bat, da_price, fr, base=None, ene_min=None, ene_max=None
         if rv.get("max") is not None:
             ge([(icl, -1.0), (idm, -1.0)], -np.minimum(_col(rv["max"], G, T), cap))
             ge([(icl, 1.0), (idm, 1.0)], _col(rv["min"], G, T))
+    if lf is not None:
+        if lf.get("up_max") is not None:
+            ge([(luc, -1.0), (lud, -1.0)], -np.minimum(_col(lf["up_max"], G, T), cap))
+            ge([(luc, 1.0), (lud, 1.0)], _col(lf["up_min"], G, T))
+        if lf.get("down_max") is not None:
+            ge([(ldc, -1.0), (ldd, -1.0)], -np.minimum(_col(lf["down_max"], G, T), cap))
+            ge([(ldc, 1.0), (ldd, 1.0)], _col(lf["down_min"], G, T))
     dur = [float(rv.get("duration", 0.0)) for rv in res]
     if any(d > 0.0 for d in dur):
         ge([(iene, 1.0)] + [(idm, -d) for d, (_, idm) in zip(dur, ires) if d > 0.0], lo)
@@ -372,6 +405,19 @@ def market_group(T, dt, bat, da_price, fr, base=None, ene_min=None, ene_max=None
         coef[:, icl:icl + T] = -pr
         coef[:, idm:idm + T] = -pr
         terms[str(rv["key"])] = (coef, np.zeros(G))
+    if lf is not None:
+        pu, pd_, pe = (_col(lf[k], G, T) for k in ("up_price", "down_price", "energy_price"))
+        for key, blocks_, pr in (("lf_up_prof", (luc, lud), pu), ("lf_down_prof", (ldc, ldd), pd_)):
+            coef = np.zeros((G, n))
+            for b0 in blocks_:
+                coef[:, b0:b0 + T] = -pr
+            terms[key] = (coef, np.zeros(G))
+        coef = np.zeros((G, n))
+        coef[:, luc:luc + T] = -pe * dt * LEU
+        coef[:, lud:lud + T] = -pe * dt * LEU
+        coef[:, ldc:ldc + T] = pe * dt * LED
+        coef[:, ldd:ldd + T] = pe * dt * LED
+        terms["lf_energy_settlement"] = (coef, np.zeros(G))
     terms[f"{name} fixed_om"] = (np.zeros((G, n)), _col(bat.get("fixedOM", 0.0), G) * pdis)
     coef = np.zeros((G, n))
     coef[:, idis:idis + T] = (_col(bat.get("OMexpenses", 0.0), G) / 1000.0 * dt)[:, None]

@@ -208,14 +208,16 @@ def config5(scenarios, years=20, start_year=2017):
     return groups
 
 
-def market_days(signals, params, relax=True, days=None, name="es", reserves=None):
+def market_days(signals, params, relax=True, days=None, name="es", reserves=None, lf=None):
     """Daily DA + frequency-regulation windows (Usecase 3 style) as one
     market_group.  signals: dict of [N] arrays da_price, regu_price, regd_price, fr_price, agg_emin, agg_emax,
     pv_gen (fixed PV, curtail = 0), regu_max/min, regd_max/min; params: model parameters (Tag -> Key -> value
     strings, as the reference's model-parameter CSV).  Windows are consecutive blocks of n steps
     (``optimization_levels`` for an integer n); ``relax`` applies the opt-in LP relaxation to binary = 1.
     reserves (optional, parity unpinned): upward reserve services as builder.market_group takes them, with
-    full-length [N] price / max / min series (template columns "SR Price ($/kW)", "SR Max (kW)", ...)."""
+    full-length [N] price / max / min series (template columns "SR Price ($/kW)", "SR Max (kW)", ...).
+    lf (optional, parity unpinned): load following as builder.market_group takes it, with full-length [N] series
+    (eou / eod may be scalars; combined a bool)."""
     from .builder import market_group
     sc, b, fr = params["Scenario"], params["Battery"], params["FR"]
     n, dt = int(sc["n"]), float(sc["dt"])
@@ -243,6 +245,10 @@ def market_days(signals, params, relax=True, days=None, name="es", reserves=None
         if r.get("max") is not None:
             d["max"], d["min"] = np.asarray(r["max"], np.float64)[sel], np.asarray(r["min"], np.float64)[sel]
         rv.append(d)
+    lfd = None
+    if lf is not None:
+        cut = lambda v: np.asarray(v, np.float64)[sel] if np.ndim(v) else float(v)
+        lfd = {k: (cut(v) if v is not None and k != "combined" else v) for k, v in lf.items()}
     return market_group(n, dt, bat, blk("da_price"), frd, base=base, ene_min=blk("agg_emin"),
                         ene_max=blk("agg_emax"), binary_relax=relax and flag(sc.get("binary", 0)), name=name,
-                        tags=[("day", int(r[0]) // n) for r in sel], reserves=rv)
+                        tags=[("day", int(r[0]) // n) for r in sel], reserves=rv, lf=lfd)

@@ -33,6 +33,10 @@ DER / value-stream set:
   ch_less_k, dis_more_k >= 0;  up_ch + sum_k ch_less_k <= ch;  dis + up_dis + sum_k dis_more_k <= P_dis;
   ts_constraints min_k <= ch_less_k + dis_more_k <= max_k;  duration d_k > 0: ene_t - sum_k d_k dis_more_k >= lower
   SOE bound;  objective key k = -sum price_k (ch_less_k + dis_more_k).
+  load following (PARITY UNPINNED: storagevet LoadFollowing, a MarketServiceUpAndDown like FR, registered at
+  dervet/MicrogridScenario.py:92; no reference result has LF active): its own up_ch, up_dis, down_ch, down_dis
+  with per-step energy options eou_t, eod_t, restated exactly as FR's above and sharing FR's rows (SOE recurrence,
+  the four headroom rows, option consistency); keys lf_up_prof, lf_down_prof, lf_energy_settlement.
 
 Variable order: [ch(T), dis(T), ene(T), tau(J), pv(T)?, elec(T)?, on(T)?, up_ch, up_dis, down_ch, down_dis (T
 each)?].  Rows: equalities (init, recurrence, final, CombinedMarket) then >= rows (DCM, ICE, FR, relaxation).
@@ -83,6 +87,13 @@ def build(win):
     for i in range(len(reserves)):
         off[f"cl{i}"], off[f"dm{i}"] = n, n + T
         n += 2 * T
+    lf = win.get("lf")
+    assert lf is None or fr is not None, "load following rides on the market window (fr)"
+    if lf is not None:
+        for k in ("luc", "lud", "ldc", "ldd"):
+            off[k] = n
+            n += T
+        leu, led = (np.broadcast_to(np.asarray(lf[k], float), (T,)) for k in ("eou", "eod"))
     hp = float(b.get("hp", 0.0))
     base = np.asarray(win["load"], float) - np.asarray(win.get("gen", np.zeros(T)), float) + hp
 
@@ -107,8 +118,12 @@ def build(win):
         if fr is None:
             return [], []
         eou, eod = float(fr["eou"]), float(fr["eod"])
-        return ([off["uc"] + t, off["dc"] + t, off["ud"] + t, off["dd"] + t],
-                [sign * dt * eta * eou, -sign * dt * eta * eod, -sign * dt * eou, sign * dt * eod])
+        oc = [off["uc"] + t, off["dc"] + t, off["ud"] + t, off["dd"] + t]
+        ov = [sign * dt * eta * eou, -sign * dt * eta * eod, -sign * dt * eou, sign * dt * eod]
+        if lf is not None:
+            oc += [off["luc"] + t, off["ldc"] + t, off["lud"] + t, off["ldd"] + t]
+            ov += [sign * dt * eta * leu[t], -sign * dt * eta * led[t], -sign * dt * leu[t], sign * dt * led[t]]
+        return oc, ov
     # recurrence t = 0..T-2:  ene_{t+1} - (1 - dt sdr) ene_t - dt eta ch_t + dt dis_t - dt (eta uch_t - udis_t) = 0
     for t in range(T - 1):
         oc, ov = opt_terms(t, -1.0)
@@ -129,6 +144,13 @@ def build(win):
         for t in range(T):
             rows += [r] * 4
             cols += [off["uc"] + t, off["ud"] + t, off["dc"] + t, off["dd"] + t]
+            vals += [1.0, 1.0, -1.0, -1.0]
+            q.append(0.0)
+            r += 1
+    if lf is not None and lf.get("combined"):
+        for t in range(T):
+            rows += [r] * 4
+            cols += [off["luc"] + t, off["lud"] + t, off["ldc"] + t, off["ldd"] + t]
             vals += [1.0, 1.0, -1.0, -1.0]
             q.append(0.0)
             r += 1
@@ -154,17 +176,20 @@ def build(win):
             nonlocal r
             for t in range(T):
                 for k, v in entries:
-                    rows.append(r); cols.append(off[k] + t); vals.append(v)
+                    rows.append(r); cols.append(off[k] + t); vals.append(v if np.isscalar(v) else v[t])
                 q.append(float(rhs[t]))
                 r += 1
-        ge_rows([("ch", -1.0), ("dc", -1.0)], np.full(T, -pch))    # ch + down_ch <= P_ch
-        ge_rows([("dis", -1.0), ("ud", -1.0)] + [(f"dm{i}", -1.0) for i in range(len(reserves))],
-                np.full(T, -pdis))                                 # dis + up_dis + sum dis_more <= P_dis
-        ge_rows([("ch", 1.0), ("uc", -1.0)] + [(f"cl{i}", -1.0) for i in range(len(reserves))],
-                np.zeros(T))                                       # up_ch + sum ch_less <= ch
-        ge_rows([("dis", 1.0), ("dd", -1.0)], np.zeros(T))         # down_dis <= dis
+        L = (lambda e: [e]) if lf is not None else (lambda e: [])
+        ge_rows([("ch", -1.0), ("dc", -1.0)] + L(("ldc", -1.0)), np.full(T, -pch))  # ch + down_ch's <= P_ch
+        ge_rows([("dis", -1.0), ("ud", -1.0)] + L(("lud", -1.0)) + [(f"dm{i}", -1.0) for i in range(len(reserves))],
+                np.full(T, -pdis))                                 # dis + up_dis's + sum dis_more <= P_dis
+        ge_rows([("ch", 1.0), ("uc", -1.0)] + L(("luc", -1.0)) + [(f"cl{i}", -1.0) for i in range(len(reserves))],
+                np.zeros(T))                                       # up_ch's + sum ch_less <= ch
+        ge_rows([("dis", 1.0), ("dd", -1.0)] + L(("ldd", -1.0)), np.zeros(T))  # down_dis's <= dis
         eou, eod = float(fr["eou"]), float(fr["eod"])
-        ge_rows([("uc", (1.0 - eta) * eou), ("dc", -(1.0 - eta) * eod), ("ud", 2.0 * eou), ("dd", -2.0 * eod)],
+        ge_rows([("uc", (1.0 - eta) * eou), ("dc", -(1.0 - eta) * eod), ("ud", 2.0 * eou), ("dd", -2.0 * eod)] +
+                ([("luc", (1.0 - eta) * leu), ("ldc", -(1.0 - eta) * led), ("lud", 2.0 * leu),
+                  ("ldd", -2.0 * led)] if lf is not None else []),
                 np.zeros(T))                                       # (1 - rte) uch + 2 udis >= 0
         if fr.get("regu_max") is not None:
             ge_rows([("uc", -1.0), ("ud", -1.0)], -np.asarray(fr["regu_max"], float))
@@ -187,6 +212,11 @@ def build(win):
         if rv.get("max") is not None:
             ge_rows([(f"cl{i}", -1.0), (f"dm{i}", -1.0)], -np.asarray(rv["max"], float))
             ge_rows([(f"cl{i}", 1.0), (f"dm{i}", 1.0)], np.asarray(rv["min"], float))
+    if lf is not None:
+        for a, b_, lim in (("luc", "lud", "up"), ("ldc", "ldd", "down")):
+            if lf.get(f"{lim}_max") is not None:
+                ge_rows([(a, -1.0), (b_, -1.0)], -np.asarray(lf[f"{lim}_max"], float))
+                ge_rows([(a, 1.0), (b_, 1.0)], np.asarray(lf[f"{lim}_min"], float))
     if any(float(rv.get("duration", 0.0)) > 0.0 for rv in reserves):
         ge_rows([("ene", 1.0)] + [(f"dm{i}", -float(rv["duration"])) for i, rv in enumerate(reserves)
                                   if float(rv.get("duration", 0.0)) > 0.0], elo)
@@ -248,6 +278,19 @@ def build(win):
         coef[off[f"cl{i}"]:off[f"cl{i}"] + T] = -np.asarray(rv["price"], float)
         coef[off[f"dm{i}"]:off[f"dm{i}"] + T] = -np.asarray(rv["price"], float)
         funcs[str(rv["key"])] = (coef, 0.0)
+    if lf is not None:
+        pu, pd_, pe = (np.asarray(lf[k], float) for k in ("up_price", "down_price", "energy_price"))
+        for key, ks, pr in (("lf_up_prof", ("luc", "lud"), pu), ("lf_down_prof", ("ldc", "ldd"), pd_)):
+            coef = np.zeros(n)
+            for k in ks:
+                coef[off[k]:off[k] + T] = -pr
+            funcs[key] = (coef, 0.0)
+        coef = np.zeros(n)
+        for k in ("luc", "lud"):
+            coef[off[k]:off[k] + T] = -pe * dt * leu
+        for k in ("ldc", "ldd"):
+            coef[off[k]:off[k] + T] = pe * dt * led
+        funcs["lf_energy_settlement"] = (coef, 0.0)
     name = b.get("name", "es")
     funcs[f"{name} fixed_om"] = (np.zeros(n), float(b.get("fixedOM", 0.0)) * pdis)
     coef = np.zeros(n)

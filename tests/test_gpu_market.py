@@ -99,3 +99,23 @@ def test_reserve_windows_match_highs(gpu_solver):
         assert abs(r.obj - h["obj"]) <= OBJ_TOL * max(abs(h["obj"]), 1.0), (d, r.obj, h["obj"])
         terms = sum(coef[k] @ r.x + const[k] for coef, const in g.terms.values())
         assert abs(terms - r.obj) <= 1e-9 * max(abs(r.obj), 1.0)
+
+
+@pytest.mark.parametrize("combined", [False, True])
+def test_load_following_windows_match_highs(gpu_solver, combined):
+    """Market days with FR + load following + SR / NSR (parity unpinned: tests/test_market_reserves.py) on the
+    GPU: objective within 1e-5 of HiGHS on the same LP and primal residual <= 1e-6."""
+    from test_market_reserves import _lf, reserve_series, sp_csr
+    sig, meta = _signals("es")
+    pdis = float(meta["params"]["Battery"]["dis_max_rated"])
+    days = list(range(3, 365, 20))
+    g = scenarios.market_days(sig, meta["params"], days=days, reserves=reserve_series(sig, pdis),
+                              lf=_lf(sig, pdis, combined=combined))
+    res = gpu_solver.solve(builder.group_window_lps(g))
+    for k, (d, r) in enumerate(zip(days, res)):
+        o = dict(K=sp_csr(g, k), q=g.q[k], c=g.c[k], c0=float(g.c0[k]), l=g.l[k], u=g.u[k], m_eq=g.m_eq)
+        h = window_lp.solve_highs(o)
+        assert h["status"] == 0 and r.status == 0, (d, r.status_name, r.iters)
+        pres, _ = window_lp.primal_residual_rel(o, r.x)
+        assert pres <= PRES_TOL, (d, pres)
+        assert abs(r.obj - h["obj"]) <= OBJ_TOL * max(abs(h["obj"]), 1.0), (d, r.obj, h["obj"])

@@ -116,3 +116,72 @@ def test_no_reserves_is_the_pinned_market_lp():
     c = scenarios.market_days(sig, meta["params"], days=DAYS, reserves=None)
     for f in ("indptr", "indices", "data", "q", "c", "l", "u"):
         assert np.array_equal(getattr(a, f), getattr(c, f))
+
+
+def lf_series(sig, scale=1.0, limits=True, combined=False):
+    """Load following over the whole fixture year: prices from the Reg Up / Down prices, energy settled at the
+    DA price, per-step energy options around 0.2 kWh/kW-h, participation limited to P_dis / 4 when ``limits``."""
+    N = len(sig["da_price"])
+    h = np.arange(N)
+    d = dict(eou=0.2 + 0.05 * np.sin(h / 7.0), eod=0.2 + 0.05 * np.cos(h / 5.0),
+             up_price=scale * 0.8 * sig["regu_price"], down_price=scale * 0.8 * sig["regd_price"],
+             energy_price=sig["da_price"], combined=combined)
+    return d, limits
+
+
+def _lf(sig, pdis, **kw):
+    d, limits = lf_series(sig, **kw)
+    if limits:
+        N = len(sig["da_price"])
+        d["up_max"] = d["down_max"] = np.full(N, 0.25 * pdis)
+        d["up_min"] = d["down_min"] = np.zeros(N)
+    return d
+
+
+@pytest.mark.parametrize("name,combined", [("es", False), ("es+pv+dg", True)])
+def test_load_following_builder_matches_oracle(name, combined):
+    sig, meta = _signals(name)
+    pdis = float(meta["params"]["Battery"]["dis_max_rated"])
+    res = reserve_series(sig, pdis)
+    lf = _lf(sig, pdis, combined=combined)
+    g = scenarios.market_days(sig, meta["params"], days=DAYS, reserves=res, lf=lf)
+    wins, _ = cases.market_windows(name)
+    T = g.T
+    assert g.n == 15 * T and {"lf_up_prof", "lf_down_prof", "lf_energy_settlement", "SR"} <= set(g.terms)
+    for k, d in enumerate(DAYS):
+        w = _oracle_window(wins[d], res, T)
+        s = slice(d * T, d * T + T)
+        w["lf"] = {key: (v[s] if np.ndim(v) else v) for key, v in lf.items()}
+        o = window_lp.build(w)
+        K = np.zeros((g.m, g.n))
+        for r in range(g.m):
+            K[r, g.indices[g.indptr[r]:g.indptr[r + 1]]] = g.data[k, g.indptr[r]:g.indptr[r + 1]]
+        assert g.m_eq == o["m_eq"] and K.shape == o["K"].shape
+        assert np.abs(K - o["K"].toarray()).max() <= 1e-14
+        for a, b in ((g.c[k], o["c"]), (g.l[k], o["l"]), (g.u[k], o["u"])):
+            assert np.array_equal(a, b) or np.abs(a - b).max() <= 1e-12
+        hb = window_lp.solve_highs(dict(K=sp_csr(g, k), q=g.q[k], c=g.c[k], c0=float(g.c0[k]), l=g.l[k],
+                                        u=g.u[k], m_eq=g.m_eq))
+        ho = window_lp.solve_highs(o)
+        assert hb["status"] == ho["status"] == 0
+        assert abs(hb["obj"] - ho["obj"]) <= 1e-7 * max(abs(ho["obj"]), 1.0), (d, hb["obj"], ho["obj"])
+
+
+def test_load_following_properties():
+    """LF is optional participation: the optimum with it never exceeds the optimum without it (LF = 0 is
+    feasible), and raising its capacity prices never raises the optimum.  (Zero-priced LF can still lower the
+    optimum: FR's pinned energy-option form, which LF shares, credits up_ch with stored energy and energy revenue
+    at once, so there is no "unchanged at price 0" identity to test.)"""
+    sig, meta = _signals("es+pv+dg")
+    pdis = float(meta["params"]["Battery"]["dis_max_rated"])
+    base = scenarios.market_days(sig, meta["params"], days=DAYS)
+    cheap = scenarios.market_days(sig, meta["params"], days=DAYS, lf=_lf(sig, pdis, scale=0.5))
+    paid = scenarios.market_days(sig, meta["params"], days=DAYS, lf=_lf(sig, pdis))
+    for k, d in enumerate(DAYS):
+        lp = lambda g: dict(K=sp_csr(g, k), q=g.q[k], c=g.c[k], c0=float(g.c0[k]), l=g.l[k], u=g.u[k],
+                            m_eq=g.m_eq)
+        h0, hc, hp = (window_lp.solve_highs(lp(g)) for g in (base, cheap, paid))
+        assert h0["status"] == hc["status"] == hp["status"] == 0
+        tol = 1e-7 * max(abs(h0["obj"]), 1.0)
+        assert hc["obj"] <= h0["obj"] + tol, (d, hc["obj"], h0["obj"])
+        assert hp["obj"] <= hc["obj"] + tol, (d, hp["obj"], hc["obj"])
