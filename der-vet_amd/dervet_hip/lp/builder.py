@@ -259,7 +259,8 @@ def market_group(T, dt, bat, da_price, fr, base=None, ene_min=None, ene_max=None
     (kWh/kW-hr)"), up_price, down_price, energy_price [G, T], optional up_max, up_min, down_max, down_min [G, T],
     combined.  x blocks [lf_up_ch, lf_up_dis, lf_down_ch, lf_down_dis] after the reserve blocks; its options join
     FR's in the SOE recurrence, the four headroom rows and the option-consistency row; keys 'lf_up_prof',
-    'lf_down_prof', 'lf_energy_settlement' as FR's.
+    'lf_down_prof', 'lf_energy_settlement' as FR's.  With lf the options enter through two free columns (uch, udis)
+    appended last, each defined by one equality row per step (see ``agg`` below).
     Without reserves / lf the LP is exactly the pinned DA + FR window."""
     da_price = np.atleast_2d(np.asarray(da_price, np.float64))
     G = da_price.shape[0]
@@ -279,6 +280,15 @@ def market_group(T, dt, bat, da_price, fr, base=None, ene_min=None, ene_max=None
         luc, lud, ldc, ldd = (n + k * T for k in range(4))
         n += 4 * T
         LEU, LED = _col(lf["eou"], G, T), _col(lf["eod"], G, T)
+    # With LF the options of both services enter the SOE rows through two free aggregate columns
+    # uch = sum eou up_ch - eod down_ch, udis = sum eou up_dis - eod down_dis (one equality row each per step):
+    # the same LP projected onto the original columns, with 6-entry SOE rows instead of 12, so each ene column
+    # sits in short rows only (the small-window ELL kernel's shape) -- without LF the pinned FR form is kept.
+    agg = lf is not None
+    iuh = iudh = -1
+    if agg:
+        iuh, iudh = n, n + T
+        n += 2 * T
     t = np.arange(T)
     tt = t[:-1]
     one = np.ones((G, 1))
@@ -287,24 +297,19 @@ def market_group(T, dt, bat, da_price, fr, base=None, ene_min=None, ene_max=None
     # SOE rows 1..T-1 (step t = row - 1): ene_{t+1} - (1 - dt sdr) ene_t - dt eta ch_t + dt dis_t
     #   - dt eta eou up_ch_t + dt eta eod down_ch_t + dt eou up_dis_t - dt eod down_dis_t = 0
     r = 1 + tt
+    opt = ((iuh + tt, -dt * eta[:, None]), (iudh + tt, dt * one)) if agg else (
+        (iuc + tt, -dt * eou * eta[:, None]), (idc + tt, dt * eod * eta[:, None]), (iud + tt, dt * eou * one),
+        (idd + tt, -dt * eod * one))
     for c0_, v in ((iene + tt + 1, one), (iene + tt, -(1.0 - dt * sdr)[:, None]), (ich + tt, -dt * eta[:, None]),
-                   (idis + tt, dt * one), (iuc + tt, -dt * eou * eta[:, None]), (idc + tt, dt * eod * eta[:, None]),
-                   (iud + tt, dt * eou * one), (idd + tt, -dt * eod * one)):
+                   (idis + tt, dt * one)) + opt:
         blocks.append((r, c0_, v * np.ones((1, len(tt)))))
-    if lf is not None:
-        for c0_, v in ((luc + tt, -dt * LEU[:, tt] * eta[:, None]), (ldc + tt, dt * LED[:, tt] * eta[:, None]),
-                       (lud + tt, dt * LEU[:, tt]), (ldd + tt, -dt * LED[:, tt])):
-            blocks.append((r, c0_, v))
     # final row: (1 - dt sdr) ene + dt eta ch - dt dis + dt (eta uch - udis) = target   (step T-1)
     k = T - 1
-    for c0_, v in ((iene + k, 1.0 - dt * sdr), (ich + k, dt * eta), (idis + k, -dt * np.ones(G)),
-                   (iuc + k, dt * eou * eta), (idc + k, -dt * eod * eta), (iud + k, -dt * eou * np.ones(G)),
-                   (idd + k, dt * eod * np.ones(G))):
+    opt = ((iuh + k, dt * eta), (iudh + k, -dt * np.ones(G))) if agg else (
+        (iuc + k, dt * eou * eta), (idc + k, -dt * eod * eta), (iud + k, -dt * eou * np.ones(G)),
+        (idd + k, dt * eod * np.ones(G)))
+    for c0_, v in ((iene + k, 1.0 - dt * sdr), (ich + k, dt * eta), (idis + k, -dt * np.ones(G))) + opt:
         blocks.append(([T], [c0_], np.asarray(v).reshape(G, 1)))
-    if lf is not None:
-        for c0_, v in ((luc + k, dt * LEU[:, k] * eta), (ldc + k, -dt * LED[:, k] * eta), (lud + k, -dt * LEU[:, k]),
-                       (ldd + k, dt * LED[:, k])):
-            blocks.append(([T], [c0_], np.asarray(v).reshape(G, 1)))
     m = T + 1
     q_eq = [target[:, None], np.zeros((G, T - 1)), target[:, None]]
     if combined:
@@ -317,6 +322,13 @@ def market_group(T, dt, bat, da_price, fr, base=None, ene_min=None, ene_max=None
             blocks.append((m + t, c0_ + t, np.full((G, T), v)))
         q_eq.append(np.zeros((G, T)))
         m += T
+    if agg:  # uch - sum(eou up_ch - eod down_ch) = 0, udis - sum(eou up_dis - eod down_dis) = 0
+        for ia, (u_, d_), (lu_, ld_) in ((iuh, (iuc, idc), (luc, ldc)), (iudh, (iud, idd), (lud, ldd))):
+            for c0_, v in ((ia, np.ones((G, 1))), (u_, np.full((G, 1), -eou)), (d_, np.full((G, 1), eod)),
+                           (lu_, -LEU), (ld_, LED)):
+                blocks.append((m + t, c0_ + t, np.broadcast_to(v, (G, T))))
+            q_eq.append(np.zeros((G, T)))
+            m += T
     m_eq = m
     q_ge = []
 
@@ -332,9 +344,11 @@ def market_group(T, dt, bat, da_price, fr, base=None, ene_min=None, ene_max=None
     ge([(idis, -1.0), (iud, -1.0)] + xl((lud, -1.0)) + [(idm, -1.0) for _, idm in ires], -pdis[:, None])
     ge([(ich, 1.0), (iuc, -1.0)] + xl((luc, -1.0)) + [(icl, -1.0) for icl, _ in ires], 0.0)
     ge([(idis, 1.0), (idd, -1.0)] + xl((ldd, -1.0)), 0.0)
-    ge([(iuc, ((1.0 - eta) * eou)[:, None]), (idc, (-(1.0 - eta) * eod)[:, None]), (iud, 2.0 * eou),
-        (idd, -2.0 * eod)] + ([(luc, (1.0 - eta)[:, None] * LEU), (ldc, -(1.0 - eta)[:, None] * LED),
-                                (lud, 2.0 * LEU), (ldd, -2.0 * LED)] if lf is not None else []), 0.0)
+    if agg:
+        ge([(iuh, (1.0 - eta)[:, None]), (iudh, 2.0)], 0.0)
+    else:
+        ge([(iuc, ((1.0 - eta) * eou)[:, None]), (idc, (-(1.0 - eta) * eod)[:, None]), (iud, 2.0 * eou),
+            (idd, -2.0 * eod)], 0.0)
     # The other rows already imply up_ch + up_dis <= P_ch + P_dis and down_ch + down_dis <= P_ch + P_dis
     # (up_ch <= ch <= P_ch - down_ch, up_dis <= P_dis - dis; down_ch <= P_ch - ch, down_dis <= dis <= P_dis),
     # so a u/d_ts maximum above that is clamped to it: the same feasible set, but without the reference's
@@ -376,6 +390,8 @@ def market_group(T, dt, bat, da_price, fr, base=None, ene_min=None, ene_max=None
     u = np.full((G, n), np.inf)
     u[:, ich:ich + T] = pch[:, None]
     u[:, idis:idis + T] = pdis[:, None]
+    if agg:
+        l[:, iuh:iuh + 2 * T] = -np.inf
     l[:, iene:iene + T] = lo
     u[:, iene:iene + T] = hi
 

@@ -147,24 +147,27 @@ def test_load_following_builder_matches_oracle(name, combined):
     g = scenarios.market_days(sig, meta["params"], days=DAYS, reserves=res, lf=lf)
     wins, _ = cases.market_windows(name)
     T = g.T
-    assert g.n == 15 * T and {"lf_up_prof", "lf_down_prof", "lf_energy_settlement", "SR"} <= set(g.terms)
+    # the builder carries the options through two free aggregate columns (uch, udis) after the oracle's 15 blocks
+    assert g.n == 17 * T and {"lf_up_prof", "lf_down_prof", "lf_energy_settlement", "SR"} <= set(g.terms)
+    n0 = 15 * T
     for k, d in enumerate(DAYS):
         w = _oracle_window(wins[d], res, T)
         s = slice(d * T, d * T + T)
         w["lf"] = {key: (v[s] if np.ndim(v) else v) for key, v in lf.items()}
         o = window_lp.build(w)
-        K = np.zeros((g.m, g.n))
-        for r in range(g.m):
-            K[r, g.indices[g.indptr[r]:g.indptr[r + 1]]] = g.data[k, g.indptr[r]:g.indptr[r + 1]]
-        assert g.m_eq == o["m_eq"] and K.shape == o["K"].shape
-        assert np.abs(K - o["K"].toarray()).max() <= 1e-14
-        for a, b in ((g.c[k], o["c"]), (g.l[k], o["l"]), (g.u[k], o["u"])):
+        assert o["K"].shape[1] == n0
+        for a, b in ((g.c[k][:n0], o["c"]), (g.l[k][:n0], o["l"]), (g.u[k][:n0], o["u"])):
             assert np.array_equal(a, b) or np.abs(a - b).max() <= 1e-12
+        assert not np.any(g.c[k][n0:]) and np.all(np.isneginf(g.l[k][n0:])) and np.all(np.isposinf(g.u[k][n0:]))
         hb = window_lp.solve_highs(dict(K=sp_csr(g, k), q=g.q[k], c=g.c[k], c0=float(g.c0[k]), l=g.l[k],
                                         u=g.u[k], m_eq=g.m_eq))
         ho = window_lp.solve_highs(o)
         assert hb["status"] == ho["status"] == 0
         assert abs(hb["obj"] - ho["obj"]) <= 1e-7 * max(abs(ho["obj"]), 1.0), (d, hb["obj"], ho["obj"])
+        # the builder's optimum, restricted to the oracle's columns, is feasible and optimal for the oracle's LP
+        xb = hb["x"][:n0]
+        assert window_lp.primal_residual_rel(o, xb)[0] <= 1e-8
+        assert abs(o["c"] @ xb + o["c0"] - ho["obj"]) <= 1e-7 * max(abs(ho["obj"]), 1.0)
 
 
 def test_load_following_properties():
