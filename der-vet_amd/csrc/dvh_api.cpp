@@ -104,10 +104,12 @@ void dvh_default_options(dvh_options* o) {
   o->restart_artificial = 0.1;
   o->primal_weight_theta = 1.0;
   o->verbose = 0;
+  o->eps_obj = 1e-6;
 }
 
 static std::string check_options(const dvh_options* o) {
   if (!(o->eps > 0.0)) return "eps must be > 0";
+  if (!(o->eps_obj >= 0.0)) return "eps_obj must be >= 0";
   if (o->max_iters <= 0) return "max_iters must be > 0";
   if (o->check_every <= 0) return "check_every must be > 0";
   if (o->kkt_every <= 0) return "kkt_every must be > 0";
@@ -394,6 +396,7 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
   const int count = bt->count;
   dvh::Opts o;
   o.eps = h->opts.eps;
+  o.eps_obj = h->opts.eps_obj;
   o.step_safety = h->opts.step_safety;
   o.rho = h->opts.reflection;
   o.b_suff = h->opts.restart_sufficient;

@@ -53,10 +53,13 @@ __device__ __noinline__ ColKkt col_kkt_fn(double kt, double cj, double loj, doub
   const double rd = rc - lam;
   return {rd * rd, cj * xj, (fl ? loj * d * fmax(lam, 0.0) : 0.0) + (fh ? hij * d * fmin(lam, 0.0) : 0.0)};
 }
-__device__ __noinline__ double row_kkt_fn(double kv, double qi, double dr, int ge) {
+struct RowKkt {
+  double rp2, y2;
+};
+__device__ __noinline__ RowKkt row_kkt_fn(double kv, double qi, double yi, double dr, int ge) {
   double r = (qi - kv) / dr;
   if (ge) r = fmax(r, 0.0);
-  return r * r;
+  return {r * r, (yi * dr) * (yi * dr)};
 }
 
 template <int B, bool ICE>
@@ -582,8 +585,10 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
         acc[8] += r.bt;
       };
       auto row_kkt = [&](int i, double kv, double qi, double yi, bool ge) {
-        acc[4] += row_kkt_fn(kv, qi, drv[opaque(i)], ge);
+        const RowKkt r = row_kkt_fn(kv, qi, yi, drv[opaque(i)], ge);
+        acc[4] += r.rp2;
         acc[7] += qi * yi;
+        acc[9] += r.y2;
       };
       double kt[NC];
       ktr(yp, YS[tid], kt);
@@ -624,7 +629,7 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
         fin[2] = dres;
         fin[3] = gap;
       }
-      if (pres <= o.eps && dres <= o.eps && gap <= o.eps) {
+      if (kkt_done(o, pres, dres, gap, pobj, dobj, acc[4], acc[9])) {
         status = kOptimal;
         break;
       }

@@ -17,6 +17,7 @@ constexpr int kSmallMax = 4096;     // windows with n or m above this go to the 
 // Kernel-side copy of dvh_options (POD, passed by value).
 struct Opts {
   double eps, step_safety, rho, b_suff, b_nec, b_art, theta;
+  double eps_obj;      // objective-error termination (dvh_options.eps_obj; 0 = off)
   int max_iters, check_every, kkt_every, ruiz_iters, power_iters;
   int setup_segments;  // set by launch_setup
   int small_max;       // setup skips (scal[6] = 2) windows with n or m above this

@@ -665,10 +665,12 @@ __global__ __launch_bounds__(B) void pdhg_kernel(const Batch b, const Work w, co
       acc[8] += (fl ? loj * d * fmax(lam, 0.0) : 0.0) + (fh ? hij * d * fmin(lam, 0.0) : 0.0);
     };
     auto row_kkt = [&](int i, double kx, double qi, double yi) {
-      double r = (qi - kx) / drv[i];
+      const double d = drv[i];
+      double r = (qi - kx) / d;
       if (i >= meq) r = fmax(r, 0.0);
       acc[4] += r * r;
       acc[7] += qi * yi;
+      acc[9] += (yi * d) * (yi * d);
     };
 #pragma unroll
     for (int s = 0; s < XS; ++s) {
@@ -710,7 +712,7 @@ __global__ __launch_bounds__(B) void pdhg_kernel(const Batch b, const Work w, co
       fin[1] = pres;
       fin[2] = dres;
       fin[3] = gap;
-      if (pres <= o.eps && dres <= o.eps && gap <= o.eps) {
+      if (kkt_done(o, pres, dres, gap, pobj, dobj, acc[4], acc[9])) {
         status = kOptimal;
         break;
       }
@@ -1432,10 +1434,12 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(WPE))) void p
         acc[8] += (fl ? loj * d * fmax(lam, 0.0) : 0.0) + (fh ? hij * d * fmin(lam, 0.0) : 0.0);
       };
       auto row_kkt = [&](int i, double kv, double qi, double yi2) {
-        double r = (qi - kv) / drv[opaque(i)];
+        const double d = drv[opaque(i)];
+        double r = (qi - kv) / d;
         if (i >= meq) r = fmax(r, 0.0);
         acc[4] += r * r;
         acc[7] += qi * yi2;
+        acc[9] += (yi2 * d) * (yi2 * d);
       };
 #pragma unroll
       for (int s = 0; s < XS; ++s)
@@ -1479,7 +1483,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(WPE))) void p
         fin[2] = dres;
         fin[3] = gap;
       }
-      if (pres <= o.eps && dres <= o.eps && gap <= o.eps) {
+      if (kkt_done(o, pres, dres, gap, pobj, dobj, acc[4], acc[9])) {
         status = kOptimal;
         break;
       }
@@ -1694,8 +1698,11 @@ static bool small_enabled() { return small_variant() >= 0; }
 
 hipError_t launch_pdhg_ell(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n, int max_m,
                            int wx, int wy, hipStream_t s, int* variant_out, const int32_t* list, int nlist) {
-  if (max_n <= 384 && max_m <= 512 && wx <= 6 && wy <= 8 && small_enabled())
-    return small_dispatch(max_n, max_m, wx, wy, b, w, ch, o, s, variant_out, list, nlist);
+  if (max_n <= 384 && max_m <= 512 && wx <= 6 && wy <= 8 && small_enabled()) {
+    const hipError_t e = small_dispatch(max_n, max_m, wx, wy, b, w, ch, o, s, variant_out, list, nlist);
+    if (e != hipErrorInvalidValue) return e;
+    (void)hipGetLastError();  // no small variant covers the shape (e.g. DVH_SMALL forcing one): the 512-thread kernels
+  }
   if (wx <= 2 && wy <= 4) return ell_dispatch_xy<2, 4>(max_n, max_m, b, w, ch, o, s, variant_out, list, nlist);
   if (wx <= 4 && wy <= 8) return ell_dispatch_xy<4, 8>(max_n, max_m, b, w, ch, o, s, variant_out, list, nlist);
   return hipErrorInvalidValue;

@@ -68,7 +68,7 @@ struct LgArgs {
   double* part;          // [(nbc + nlc + nbr + nlr) * kPart]
   const double* hinv;
   LgState* st;
-  double eps, rho, b_suff, b_nec, b_art, theta, step_safety;
+  double eps, rho, b_suff, b_nec, b_art, theta, step_safety, eps_obj;
   int chk, kkt_every, max_iters;
   int warm;              // 1: start from the unscaled x / y already in the output buffers (dvh_options.warm_start)
   // outputs
@@ -427,12 +427,14 @@ __global__ __launch_bounds__(LB) void lg_kkt_rows(LgArgs a) {
   const LgState* st = a.st;
   if (st->status >= 0 || !is_kkt_check(a, st)) return;
   const int pb = a.nbc + a.nlc + blockIdx.x;
-  double v[2] = {0.0, 0.0};
+  double v[3] = {0.0, 0.0, 0.0};
   auto acc = [&](int r, double kxs) {
     double res = a.q[r] - kxs / a.dr[r];
     if (r >= a.meq) res = fmax(res, 0.0);
+    const double yu = a.dr[r] * a.yo[r];
     v[0] += res * res;
-    v[1] += a.q[r] * (a.dr[r] * a.yo[r]);
+    v[1] += a.q[r] * yu;
+    v[2] += yu * yu;
   };
   if ((int)blockIdx.x < a.nbr) {
     const int r = blockIdx.x * LB + threadIdx.x;
@@ -441,7 +443,7 @@ __global__ __launch_bounds__(LB) void lg_kkt_rows(LgArgs a) {
       for (int e = 0; e < a.wr; ++e) kx += a.kv[(size_t)e * a.m + r] * a.xo[a.ki[(size_t)e * a.m + r]];
       acc(r, kx);
     }
-    lg_block_sum<2>(v);
+    lg_block_sum<3>(v);
   } else {
     const int L = blockIdx.x - a.nbr;
     double s[1] = {0.0};
@@ -452,6 +454,7 @@ __global__ __launch_bounds__(LB) void lg_kkt_rows(LgArgs a) {
   if (threadIdx.x == 0) {
     a.part[(size_t)pb * kPart + 2] = v[0];
     a.part[(size_t)pb * kPart + 3] = v[1];
+    a.part[(size_t)pb * kPart + 4] = v[2];
   }
 }
 
@@ -498,12 +501,12 @@ __global__ __launch_bounds__(1024) void lg_check(LgArgs a) {
   if (st->status >= 0) return;
   const int ncb = a.nbc + a.nlc, nrb = a.nbr + a.nlr;
   const bool kkt = is_kkt_check(a, st);
-  double cm[2], rm[2], ck[3] = {0.0, 0.0, 0.0}, rk[2] = {0.0, 0.0};
+  double cm[2], rm[2], ck[3] = {0.0, 0.0, 0.0}, rk[3] = {0.0, 0.0, 0.0};
   lg_reduce_parts<2>(a.part, 0, ncb, 0, cm);
   lg_reduce_parts<2>(a.part, ncb, nrb, 0, rm);
   if (kkt) {
     lg_reduce_parts<3>(a.part, 0, ncb, 2, ck);
-    lg_reduce_parts<2>(a.part, ncb, nrb, 2, rk);
+    lg_reduce_parts<3>(a.part, ncb, nrb, 2, rk);
   }
   if (threadIdx.x != 0) return;
   const int after = st->it + a.chk;
@@ -518,7 +521,8 @@ __global__ __launch_bounds__(1024) void lg_check(LgArgs a) {
     st->dres = sqrt(ck[0]) / (1.0 + st->nc);
     st->gap = fabs(pobj - dobj) / (1.0 + fabs(pobj) + fabs(dobj));
     st->pobj = pobj;
-    if (st->pres <= a.eps && st->dres <= a.eps && st->gap <= a.eps) {
+    const bool obj_ok = !(a.eps_obj > 0.0) || fabs(pobj - dobj) + sqrt(rk[0] * rk[2]) <= a.eps_obj * (1.0 + fabs(pobj));
+    if (st->pres <= a.eps && st->dres <= a.eps && st->gap <= a.eps && obj_ok) {
       st->status = kOptimal;
       return;
     }
@@ -764,7 +768,7 @@ hipError_t large_solve(LargeSolver* ls, const Batch& b, int k, const int64_t* d,
   a.part = db + o_part;
   a.hinv = hinv;
   a.st = ls->st.as<LgState>();
-  a.eps = o.eps; a.rho = o.rho; a.b_suff = o.b_suff; a.b_nec = o.b_nec; a.b_art = o.b_art; a.theta = o.theta;
+  a.eps = o.eps; a.eps_obj = o.eps_obj; a.rho = o.rho; a.b_suff = o.b_suff; a.b_nec = o.b_nec; a.b_art = o.b_art; a.theta = o.theta;
   a.step_safety = o.step_safety;
   a.chk = std::max(1, std::min(o.check_every, o.max_iters));
   a.kkt_every = std::max(1, o.kkt_every);

@@ -13,35 +13,37 @@ Reference loop (dervet/MicrogridScenario.py:281-320, serial over windows):
 per-window ``solve_optimization`` by ONE ``BatchSolver.solve`` over every LP window:
 
   1. set up every window with the unchanged ``set_up_optimization`` and export it immediately
-     (``CvxpyExporter``: cvxpy ``get_problem_data`` -> canonical LP), keeping that window's DER
-     ``variables_dict`` objects (CVXPY variables are re-created per window, ElectricVehicles.py:96-122);
+     (``CvxpyExporter``: cvxpy ``get_problem_data(ECOS)`` -> ``export.ecos_to_window``: presolve + band
+     canonicalisation), keeping that window's DER ``variables_dict`` objects (CVXPY variables are re-created per
+     window, ElectricVehicles.py:96-122);
   2. solve all exported windows in one batch on the GPU;
-  3. per window, in order: re-point each DER's ``variables_dict``, write the solution into the CVXPY
-     variables, and call the unchanged ``save_optimization_results``.
+  3. per window, in order: re-point each DER's ``variables_dict``, hand the solution to CVXPY exactly as ECOS's
+     would arrive (``ExportedWindow.ecos_solution`` -> ``Problem.unpack_results``), and call the unchanged
+     ``save_optimization_results``.  Statuses map to ECOS exit flags (infeasible 1, unbounded 2, iteration limit
+     10 = optimal_inaccurate); a numerical failure, on which CVXPY would raise SolverError, skips
+     ``unpack_results`` and is saved with its error message (errors travel as ``cvx_error_msg``,
+     MicrogridScenario.py:319-320); the loop goes on either way.
 
 Windows that are not LPs (binary / integer variables: MILP, ESSSizing.py:82-138) are solved by the
 reference ``solve_optimization`` in their place in the order.  Scenarios whose windows are coupled through
-saved results (battery degradation, Battery.py:87-110; sizing, MicrogridScenario.py:361-363) run the
-reference loop unchanged.  ``DERVET.solve`` hard-codes ``MicrogridScenario`` (dervet/DERVET.py:76), so
-``install`` patches that name with the batched subclass.
+saved results (battery degradation, Battery.py:87-110; sizing, MicrogridScenario.py:361-363) cannot batch their
+own windows; ``batched_cases_loop`` batches them ACROSS scenarios instead: window k of every case in one GPU
+call, saved before any case sets up window k + 1 (the serial case loop of dervet/DERVET.py:75-83, in lockstep).
+``DERVET.solve`` hard-codes ``MicrogridScenario`` (dervet/DERVET.py:76), so ``install`` patches that name with
+the batched subclass.
 """
-import numpy as np
-
 from . import _lib
-from .solver import BatchSolver, WindowLP
+from .export import ExportError, ecos_to_window
+from .solver import BatchSolver
 
 STATUS_TO_CVXPY = _lib.STATUS_NAMES  # DVH status -> cvxpy status string read by save_optimization_results
 
 
 class CvxpyExporter:
-    """(functions, constraints) of one window -> WindowLP via CVXPY's ECOS canonicalisation.
-
-    ECOS data: min c'x + offset  s.t.  A x = b,  G x + s = h,  s in K.  An LP window has a purely
-    nonnegative cone (dims.q / dims.e empty), i.e.  G x <= h  ->  K_I = -G, q_I = -h.
-    """
+    """(functions, constraints) of one window -> ExportedWindow via CVXPY's ECOS canonicalisation."""
 
     def __init__(self):
-        import cvxpy as cvx  # noqa: F401  (absent in this container; the native builder is used there)
+        import cvxpy as cvx  # noqa: F401  (absent in this container; tests drive ecos_to_window directly)
         self.cvx = cvx
 
     def export(self, functions, constraints):
@@ -50,32 +52,33 @@ class CvxpyExporter:
         if any(v.attributes.get("boolean") or v.attributes.get("integer") for v in prob.variables()):
             return None  # MILP: stays on the reference path
         data, chain, inverse = prob.get_problem_data(cvx.ECOS)
-        dims = data["dims"]
-        if getattr(dims, "soc", None) or getattr(dims, "exp", 0):
-            return None
-        import scipy.sparse as sp
-        A = sp.csr_matrix(data["A"]) if data.get("A") is not None else sp.csr_matrix((0, len(data["c"])))
-        G = sp.csr_matrix(data["G"]) if data.get("G") is not None else sp.csr_matrix((0, len(data["c"])))
-        K = sp.vstack([A, -G]).tocsr()
-        q = np.concatenate([np.asarray(data.get("b", np.zeros(A.shape[0])), float).ravel(),
-                            -np.asarray(data["h"], float).ravel()])
-        n = len(data["c"])
-        lp = WindowLP.from_csr(K, q, np.asarray(data["c"], float), np.full(n, -np.inf), np.full(n, np.inf),
-                               A.shape[0], float(data.get("offset", 0.0)))
-        return _CvxpyWindow(prob, chain, inverse, lp, A.shape[0])
+        try:
+            ew = ecos_to_window(data)
+        except ExportError:
+            return None  # not an LP the solver takes (cones, infeasible presolve): the reference solve
+        return CvxpyWindow(ew, prob, chain, inverse)
 
 
-class _CvxpyWindow:
-    def __init__(self, prob, chain, inverse, lp, m_eq):
-        self.prob, self.chain, self.inverse, self.lp, self.m_eq = prob, chain, inverse, lp, m_eq
+class CvxpyWindow:
+    """An exported window and the CVXPY objects its solution goes back into."""
+
+    def __init__(self, ew, prob=None, chain=None, inverse=None):
+        self.ew, self.prob, self.chain, self.inverse = ew, prob, chain, inverse
+
+    @property
+    def lp(self):
+        return self.ew.lp
 
     def unpack(self, res):
-        """Write a WindowResult into the CVXPY variables (same path ECOS results take)."""
-        y = res.y
-        sol = {"x": res.x, "y": y[:self.m_eq], "z": -y[self.m_eq:],
-               "info": {"exitFlag": 0 if res.status == 0 else -1, "pcost": res.obj, "iter": res.iters}}
-        self.prob.unpack_results(sol, self.chain, self.inverse)
-        return self.prob
+        """-> (problem, cvx_error_msg), as the reference's solve would leave them: the result goes through CVXPY's
+        own ECOS inversion (``unpack_results``) -- optimal / optimal_inaccurate write the variables, infeasible /
+        unbounded set the status and value as an ECOS result would -- except a numerical failure, for which
+        CVXPY would raise SolverError inside ``prob.solve``: the problem stays unsolved and the message is the
+        window's cvx_error_msg (MicrogridScenario.py:319-320)."""
+        if res.status == _lib.NUMERICAL:
+            return self.prob, f"dervet_hip: window solve status {res.status_name} (solver error)"
+        self.prob.unpack_results(self.ew.ecos_solution(res), self.chain, self.inverse)
+        return self.prob, None
 
 
 def windows_are_independent(scenario):
@@ -89,10 +92,10 @@ def windows_are_independent(scenario):
     return True
 
 
-def batched_optimize_problem_loop(scenario, solver=None, exporter=None, **kwargs):
-    """Batched ``MicrogridScenario.optimize_problem_loop`` (dervet/MicrogridScenario.py:281-320)."""
+def _preamble(scenario):
+    """MicrogridScenario.optimize_problem_loop :289-307 in effect; returns (alpha, ignore_der_costs) or None when
+    the optimizer is off."""
     sa, poi = scenario.service_agg, scenario.poi
-    # ---- preamble, verbatim in effect (:289-307)
     scenario.system_requirements = sa.identify_system_requirements(poi.der_list, scenario.opt_years,
                                                                    scenario.frequency)
     alpha = 1
@@ -103,9 +106,55 @@ def batched_optimize_problem_loop(scenario, solver=None, exporter=None, **kwargs
     if sa.post_facto_reliability_only_and_user_defined_constraints():
         sa.value_streams["Reliability"].use_user_const = True
     if not scenario.opt_engine:
-        return
-    ignore = sa.post_facto_reliability_only()
-    if not windows_are_independent(scenario):
+        return None
+    return alpha, sa.post_facto_reliability_only()
+
+
+def _setup_export(scenario, opt_period, alpha, ignore, exporter):
+    """set_up_optimization of one window + its export; None for a window with nothing to optimize (:316-318)."""
+    functions, constraints, sub_index = scenario.set_up_optimization(opt_period, annuity_scalar=alpha,
+                                                                     ignore_der_costs=ignore)
+    if not len(constraints) and not len(functions.values()):
+        return None
+    saved_vars = {der: getattr(der, "variables_dict", None) for der in getattr(scenario.poi, "active_ders", [])}
+    return (opt_period, sub_index, functions, constraints, saved_vars, exporter.export(functions, constraints))
+
+
+def _solve_plans(plans, solver):
+    """One batched solve over the LP windows of `plans` (list of plan tuples); returns {index: WindowResult}."""
+    lp_idx = [i for i, p in enumerate(plans) if p[5] is not None]
+    if not lp_idx:
+        return {}
+    own = solver is None
+    solver = solver or BatchSolver(0)
+    try:
+        res = solver.solve([plans[i][5].lp for i in lp_idx])
+    finally:
+        if own:
+            solver.close()
+    return dict(zip(lp_idx, res))
+
+
+def _save(scenario, plan, r):
+    opt_period, sub_index, functions, constraints, saved_vars, win = plan
+    for der, vd in saved_vars.items():
+        if vd is not None:
+            der.variables_dict = vd
+    if win is None:  # MILP / non-LP window: the reference solve, in place
+        prob, obj, err = scenario.solve_optimization(functions, constraints)
+    else:
+        prob, err = win.unpack(r)
+        obj = functions
+    scenario.save_optimization_results(opt_period, sub_index, prob, obj, err)
+
+
+def batched_optimize_problem_loop(scenario, solver=None, exporter=None, **kwargs):
+    """Batched ``MicrogridScenario.optimize_problem_loop`` (dervet/MicrogridScenario.py:281-320)."""
+    pre = _preamble(scenario)
+    if pre is None:
+        return None
+    alpha, ignore = pre
+    if not windows_are_independent(scenario):  # coupled windows: the reference loop, unchanged
         for opt_period in scenario.optimization_levels.predictive.unique():
             functions, constraints, sub_index = scenario.set_up_optimization(opt_period, annuity_scalar=alpha,
                                                                              ignore_der_costs=ignore)
@@ -113,44 +162,67 @@ def batched_optimize_problem_loop(scenario, solver=None, exporter=None, **kwargs
                 continue
             prob, obj, err = scenario.solve_optimization(functions, constraints)
             scenario.save_optimization_results(opt_period, sub_index, prob, obj, err)
-        return
+        return None
     exporter = exporter or CvxpyExporter()
-    # ---- 1. set up + export every window
-    plan = []
-    for opt_period in scenario.optimization_levels.predictive.unique():
-        functions, constraints, sub_index = scenario.set_up_optimization(opt_period, annuity_scalar=alpha,
-                                                                         ignore_der_costs=ignore)
-        if not len(constraints) and not len(functions.values()):
-            continue
-        saved_vars = {der: getattr(der, "variables_dict", None) for der in getattr(poi, "active_ders", [])}
-        win = exporter.export(functions, constraints)
-        plan.append((opt_period, sub_index, functions, constraints, saved_vars, win))
-    # ---- 2. one batched GPU solve for the LP windows
-    lp_idx = [i for i, p in enumerate(plan) if p[5] is not None]
-    results = {}
-    if lp_idx:
-        own = solver is None
-        solver = solver or BatchSolver(0)
-        try:
-            res = solver.solve([plan[i][5].lp for i in lp_idx])
-        finally:
-            if own:
-                solver.close()
-        results = dict(zip(lp_idx, res))
-    # ---- 3. write back and save, window by window, in the reference order
-    for i, (opt_period, sub_index, functions, constraints, saved_vars, win) in enumerate(plan):
-        for der, vd in saved_vars.items():
-            if vd is not None:
-                der.variables_dict = vd
-        if win is None:  # MILP / non-LP window: the reference solve, in place
-            prob, obj, err = scenario.solve_optimization(functions, constraints)
-        else:
-            r = results[i]
-            prob = win.unpack(r)
-            obj = functions
-            err = None if r.status == _lib.OPTIMAL else f"dervet_hip: window solve status {r.status_name}"
-        scenario.save_optimization_results(opt_period, sub_index, prob, obj, err)
+    plan = [p for p in (_setup_export(scenario, w, alpha, ignore, exporter)
+                        for w in scenario.optimization_levels.predictive.unique()) if p is not None]
+    results = _solve_plans(plan, solver)
+    for i, p in enumerate(plan):
+        _save(scenario, p, results.get(i))
     return plan
+
+
+def batched_cases_loop(scenarios, solver=None, exporter=None):
+    """The optimize_problem_loop of several cases (dervet/DERVET.py:75-83) batched on the GPU.
+
+    Independent cases (``windows_are_independent``) put all their windows into one batch.  Coupled cases
+    (degradation / sizing) advance in lockstep: window position k of every coupled case is set up, solved in one
+    batch and saved (so each case's degradation update runs) before any coupled case sets up position k + 1.
+    Returns the plans per case, in case order."""
+    exporter = exporter or CvxpyExporter()
+    own = solver is None
+    solver = solver or BatchSolver(0)
+    try:
+        live, indep, coupled = [], [], []
+        for s in scenarios:
+            pre = _preamble(s)
+            if pre is None:
+                live.append(None)
+                continue
+            live.append(pre)
+            (indep if windows_are_independent(s) else coupled).append(len(live) - 1)
+        plans = {i: [] for i in range(len(scenarios))}
+        # every window of every independent case: one batch
+        flat = []
+        for i in indep:
+            s = scenarios[i]
+            alpha, ignore = live[i]
+            for w in s.optimization_levels.predictive.unique():
+                p = _setup_export(s, w, alpha, ignore, exporter)
+                if p is not None:
+                    flat.append((i, p))
+        res = _solve_plans([p for _, p in flat], solver)
+        for k, (i, p) in enumerate(flat):
+            _save(scenarios[i], p, res.get(k))
+            plans[i].append(p)
+        # coupled cases: window position by window position across the cases
+        periods = {i: list(scenarios[i].optimization_levels.predictive.unique()) for i in coupled}
+        for pos in range(max((len(v) for v in periods.values()), default=0)):
+            step = []
+            for i in coupled:
+                if pos < len(periods[i]):
+                    alpha, ignore = live[i]
+                    p = _setup_export(scenarios[i], periods[i][pos], alpha, ignore, exporter)
+                    if p is not None:
+                        step.append((i, p))
+            res = _solve_plans([p for _, p in step], solver)
+            for k, (i, p) in enumerate(step):
+                _save(scenarios[i], p, res.get(k))
+                plans[i].append(p)
+        return [plans[i] for i in range(len(scenarios))]
+    finally:
+        if own:
+            solver.close()
 
 
 def make_batched_scenario_class(base, solver_factory=None):

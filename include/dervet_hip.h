@@ -67,7 +67,11 @@ typedef struct dvh_options {
   int32_t kkt_every;          /* termination (KKT) check every kkt_every restart checks, default 4 */
   int32_t warm_start;         /* 1: start each window from the x / y already in the output buffers     */
                               /*    (unscaled, e.g. a similar window's solution); 0: x = proj(0), y = 0 */
-  int32_t reserved[5];
+  int32_t pad0;
+  double eps_obj;             /* objective-error termination (0 = off), default 1e-6: besides the KKT test, */
+                              /* |pobj - dobj| + ||y||_2 ||r_p||_2 <= eps_obj (1 + |pobj|) (unscaled), an    */
+                              /* estimate of |pobj - opt| (gap + the dual-weighted primal residual)          */
+  int32_t reserved[2];
 } dvh_options;
 
 typedef struct dvh_lp {

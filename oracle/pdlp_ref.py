@@ -28,7 +28,7 @@ OPTIMAL, PRIMAL_INFEASIBLE, DUAL_INFEASIBLE, ITER_LIMIT, NUMERICAL = 0, 1, 2, 3,
 
 # defaults mirror dvh_default_options (der-vet_amd/csrc/dvh_api.cpp)
 DEFAULTS = dict(eps=1e-6, max_iters=100000, check_every=32, kkt_every=4, ruiz_iters=10, power_iters=64,
-                step_safety=0.998, rho=1.0, b_suff=0.2, b_nec=0.8, b_art=0.1, theta=1.0)
+                step_safety=0.998, rho=1.0, b_suff=0.2, b_nec=0.8, b_art=0.1, theta=1.0, eps_obj=1e-6)
 
 
 def precondition(K, ruiz_iters):
@@ -108,8 +108,15 @@ def solve(lp, opts=None, trace=None):
         dobj = q @ y + np.sum(np.where(finite_l, l, 0) * np.maximum(lam, 0)) + \
             np.sum(np.where(finite_u, u, 0) * np.minimum(lam, 0)) + c0
         return dict(pres=np.linalg.norm(r), dres=np.linalg.norm(rd), pobj=pobj, dobj=dobj,
+                    xnorm=np.linalg.norm(x), ynorm=np.linalg.norm(y),
                     pres_rel=np.linalg.norm(r) / (1 + q_norm), dres_rel=np.linalg.norm(rd) / (1 + c_norm),
                     gap_rel=abs(pobj - dobj) / (1 + abs(pobj) + abs(dobj)))
+
+    def obj_ok(i):
+        # objective-error estimate (eps_obj > 0): |pobj - dobj| + ||y||_2 ||r_p||_2 <= eps_obj (1 + |pobj|)
+        if not o["eps_obj"] > 0.0:
+            return True
+        return abs(i["pobj"] - i["dobj"]) + i["ynorm"] * i["pres"] <= o["eps_obj"] * (1.0 + abs(i["pobj"]))
 
     # warm start (dvh_options.warm_start): unscaled x0 / y0 moved into the scaled space; optional w0
     x = np.clip(np.asarray(o["x0"], float) / Dc if o.get("x0") is not None else np.zeros(n), lt, ut)
@@ -137,7 +144,8 @@ def solve(lp, opts=None, trace=None):
                 last = (xp, yp)
                 if trace is not None:
                     trace.append((it, k, w, r, info["pres_rel"], info["dres_rel"], info["gap_rel"]))
-                if info["pres_rel"] <= o["eps"] and info["dres_rel"] <= o["eps"] and info["gap_rel"] <= o["eps"]:
+                if info["pres_rel"] <= o["eps"] and info["dres_rel"] <= o["eps"] and info["gap_rel"] <= o["eps"] \
+                        and obj_ok(info):
                     x, y = xp, yp
                     status = OPTIMAL
                     break

@@ -1,16 +1,21 @@
 """Drop-in window loop (dervet_hip.dropin) exercised with fakes of the reference objects it touches.
 
-storagevet / cvxpy are absent, so the scenario, POI, service aggregator, DERs and
-the exporter are fakes with the reference's method names; the solver is a CPU stand-in that answers with
-HiGHS (it replaces only the GPU call, to check the loop's ordering, write-back and fallback logic).
+storagevet / cvxpy are absent, so the scenario, POI, service aggregator and DERs are fakes
+with the reference's method names.  The export is the real one: each window is written in the form CVXPY 1.0.31
+hands ECOS (tests/ecos_forms.py) and goes through dervet_hip.export; results come back through a restatement of
+CVXPY's ECOS inversion (ecos_forms.FakeProblem).  The solver is a CPU stand-in that answers with HiGHS on the
+exported LP (it replaces only the GPU call, to check the loop's ordering, write-back and fallback logic; the GPU
+run of the same loop is tests/test_gpu_export.py).
 """
 import types
 
 import numpy as np
 import pandas as pd
 import pytest
+import scipy.sparse as sp
 
-from dervet_hip import WindowResult, dropin
+import ecos_forms
+from dervet_hip import WindowResult, dropin, export
 from dervet_hip.lp import builder, scenarios
 from oracle import window_lp
 
@@ -36,12 +41,20 @@ class FakeSA:
         return False
 
 
+_LPS = {}
+
+
+def _config4_lps(scen):
+    if scen not in _LPS:
+        _LPS[scen] = [lp for g in scenarios.config4([scen]) for lp in builder.group_window_lps(g)]
+    return _LPS[scen]
+
+
 class FakeScenario:
     """Windows are config-4 window LPs; set_up_optimization re-creates the DER variables per window."""
 
-    def __init__(self, n_windows=6, empty=(), milp=(), degrade=False):
-        groups = scenarios.config4([0])
-        self.lps = [lp for g in groups for lp in builder.group_window_lps(g)][:n_windows]
+    def __init__(self, n_windows=6, empty=(), milp=(), degrade=False, scen=0, journal=None):
+        self.lps = _config4_lps(scen)[:n_windows]
         self.optimization_levels = pd.DataFrame({"predictive": np.arange(n_windows)})
         self.ders = [FakeDER("es", degrade)]
         self.poi = types.SimpleNamespace(der_list=self.ders, active_ders=self.ders, is_sizing_optimization=False)
@@ -51,9 +64,12 @@ class FakeScenario:
         self.opt_engine = True
         self.empty, self.milp = set(empty), set(milp)
         self.saved, self.reference_solves, self.log = [], [], []
+        self.journal = journal if journal is not None else []
+        self.scen = scen
 
     def set_up_optimization(self, opt_period, annuity_scalar=1, ignore_der_costs=False):
         self.log.append(("setup", int(opt_period)))
+        self.journal.append((self.scen, "setup", int(opt_period)))
         for der in self.ders:
             der.variables_dict = {"window": int(opt_period)}
         if opt_period in self.empty:
@@ -62,23 +78,24 @@ class FakeScenario:
 
     def solve_optimization(self, functions, constraints):
         self.reference_solves.append(functions["lp"])
-        lp = functions["lp"]
-        h = _highs(lp)
+        h = _highs(functions["lp"])
         return types.SimpleNamespace(status="optimal", value=h.obj, x=h.x), functions, None
 
     def save_optimization_results(self, opt_window_num, sub_index, prob, obj_expression, cvx_error_msg):
         self.log.append(("save", int(opt_window_num)))
+        self.journal.append((self.scen, "save", int(opt_window_num)))
         self.saved.append((int(opt_window_num), prob, cvx_error_msg, dict(self.ders[0].variables_dict)))
 
 
 def _highs(lp):
-    import scipy.sparse as sp
     K = sp.csr_matrix((lp.data, lp.indices, lp.indptr), shape=(lp.m, lp.n))
     h = window_lp.solve_highs(dict(K=K, q=lp.q, c=lp.c, c0=lp.c0, l=lp.l, u=lp.u, m_eq=lp.m_eq))
     return WindowResult(h["x"], h["y"], h["obj"], 0, 0, 0.0, 0.0, 0.0)
 
 
 class FakeExporter:
+    """Writes the window in CVXPY's ECOS form and exports it with dervet_hip.export (MILP windows: None)."""
+
     def __init__(self, milp):
         self.milp = milp
 
@@ -86,9 +103,9 @@ class FakeExporter:
         lp = functions["lp"]
         if any(lp is m for m in self.milp):
             return None
-        win = types.SimpleNamespace(lp=lp)
-        win.unpack = lambda r: types.SimpleNamespace(status=r.status_name, value=r.obj, x=r.x)
-        return win
+        olp, dt, eta, sdr, target = ecos_forms.oracle_lp_of(lp)
+        data, col = ecos_forms.ecos_form(olp, dt, eta, sdr, target, seed=len(lp.c))
+        return dropin.CvxpyWindow(export.ecos_to_window(data), ecos_forms.FakeProblem(data, col))
 
 
 class CpuStandInSolver:
@@ -113,6 +130,13 @@ def test_batched_loop_orders_saves_and_repoints_variables():
     assert all(s[3]["window"] == s[0] for s in sc.saved)
     assert all(s[2] is None for s in sc.saved)
     assert len(plan) == 5
+    # the values arrive through the ECOS inversion: status and objective as the reference's solve leaves them
+    for w, prob, err, _ in sc.saved:
+        assert prob.status == "optimal"
+        assert prob.value == pytest.approx(_highs(sc.lps[w]).obj, rel=1e-9)
+        # the primal x in ECOS order is the window's solution (builder layout through the export's column map)
+        lp = sc.lps[w]
+        assert lp.c @ prob.x[prob.col] + lp.c0 == pytest.approx(prob.value, rel=1e-12)
 
 
 def test_milp_windows_fall_back_in_place():
@@ -133,17 +157,50 @@ def test_coupled_windows_run_the_reference_loop():
     assert [k for k, _ in sc.log] == ["setup", "save"] * 3
 
 
-def test_nonoptimal_status_becomes_error_message():
-    sc = FakeScenario(n_windows=2)
+def test_statuses_reach_save_as_the_reference_solve_leaves_them():
+    """a non-optimal window must not abort the loop.  Iteration limit -> optimal_inaccurate with the
+    solution; infeasible -> status 'infeasible' (no error, as CVXPY reports it); numerical failure -> CVXPY would
+    raise SolverError: the problem stays unsolved and the message is the window's cvx_error_msg."""
+    sc = FakeScenario(n_windows=4)
 
-    class Bad(CpuStandInSolver):
+    class Mixed(CpuStandInSolver):
         def solve(self, lps):
             out = super().solve(lps)
-            out[1].status = 3  # ITER_LIMIT
+            out[1].status = 3   # ITER_LIMIT
+            out[2].status = 1   # PRIMAL_INFEASIBLE
+            out[3].status = 4   # NUMERICAL
             return out
 
-    dropin.batched_optimize_problem_loop(sc, solver=Bad(), exporter=FakeExporter([]))
-    assert sc.saved[0][2] is None and "optimal_inaccurate" in sc.saved[1][2]
+    dropin.batched_optimize_problem_loop(sc, solver=Mixed(), exporter=FakeExporter([]))
+    st = {w: (prob.status, err) for w, prob, err, _ in sc.saved}
+    assert st[0] == ("optimal", None)
+    assert st[1] == ("optimal_inaccurate", None)
+    assert st[2] == ("infeasible", None)
+    assert st[3][0] is None and "solver error" in st[3][1]
+    assert [w for w, *_ in sc.saved] == [0, 1, 2, 3]
+
+
+def test_cases_loop_batches_independent_cases_and_steps_coupled_ones_in_lockstep():
+    journal = []
+    cases_ = [FakeScenario(n_windows=3, scen=0, journal=journal),
+              FakeScenario(n_windows=3, scen=1, degrade=True, journal=journal),
+              FakeScenario(n_windows=2, scen=2, degrade=True, journal=journal),
+              FakeScenario(n_windows=2, scen=3, journal=journal)]
+    solver = CpuStandInSolver()
+    plans = dropin.batched_cases_loop(cases_, solver=solver, exporter=FakeExporter([]))
+    # independent cases: all 5 windows in one call; coupled: one call per window position (2, 2, 1 windows)
+    assert solver.calls == [5, 2, 2, 1]
+    assert [len(p) for p in plans] == [3, 3, 2, 2]
+    # lockstep: a coupled case's window k is saved before any coupled case sets up window k + 1
+    coupled = [e for e in journal if e[0] in (1, 2)]
+    for k in (1, 2):
+        first_setup_k = min(i for i, e in enumerate(coupled) if e[1] == "setup" and e[2] == k)
+        last_save_prev = max(i for i, e in enumerate(coupled) if e[1] == "save" and e[2] == k - 1)
+        assert last_save_prev < first_setup_k
+    for c in cases_:
+        assert [w for w, *_ in c.saved] == list(range(len(c.lps)))
+        for w, prob, err, _ in c.saved:
+            assert err is None and prob.value == pytest.approx(_highs(c.lps[w]).obj, rel=1e-9)
 
 
 def test_opt_engine_off_returns_before_any_window():

@@ -1,0 +1,80 @@
+"""GPU half of the drop-in export round trip: CVXPY-shaped ECOS data of the golden windows
+-> dervet_hip.export (presolve + band canonicalisation) -> the HIP solver through the C ABI -> the ECOS solution
+dict -> CVXPY's ECOS inversion (restated in tests/ecos_forms.py) -> the golden per-window objectives."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+import ecos_forms
+from dervet_hip import BatchSolver, dropin, export
+from oracle import cases, window_lp
+
+pytestmark = pytest.mark.gpu
+
+
+def _windows(name):
+    wins, arr, _, _ = cases.case_windows(name)
+    out = []
+    for i, w in enumerate(wins):
+        olp = window_lp.build(w)
+        b = w["bat"]
+        data, col = ecos_forms.ecos_form(olp, w["dt"], b["rte"], b["sdr"] / 100.0, b["soc_target"] * b["E"], seed=7 + i,
+                                         pins="rows" if i % 2 else "bounds")
+        out.append((data, col, export.ecos_to_window(data), float(arr["golden_objective"][i].sum())))
+    return out
+
+
+@pytest.mark.parametrize("name", ["es", "es+pv+dg"])
+def test_exported_golden_windows_run_on_the_band_kernel(name):
+    ws = _windows(name)
+    with BatchSolver(0) as s:
+        res = s.solve([ew.lp for _, _, ew, _ in ws])
+        ks = s.kernel_stats()
+    assert ks["band_windows"] == len(ws), ks
+    for (data, col, ew, gold), r in zip(ws, res):
+        assert r.status == 0
+        sol = ew.ecos_solution(r)
+        inv = ecos_forms.invert(sol, data["offset"])
+        assert inv["status"] == "optimal"
+        assert abs(inv["value"] - gold) <= 1e-5 * abs(gold)
+        # primal feasibility of the ECOS form within the solver's relative tolerance, ECOS dual signs
+        A, G, b, h = data["A"], data["G"], data["b"], data["h"]
+        x, y, z = sol["x"], sol["y"], sol["z"]
+        pres = np.sqrt(np.sum((A @ x - b) ** 2) + np.sum(np.maximum(G @ x - h, 0) ** 2)) / (
+            1 + np.linalg.norm(np.concatenate([b, h])))
+        assert pres <= 1e-6
+        assert z.min() >= 0.0
+        stat = np.linalg.norm(data["c"] + A.T @ y + G.T @ z) / (1 + np.linalg.norm(data["c"]))
+        assert stat <= 1e-5
+        assert abs(sol["info"]["dcost"] + data["offset"] - gold) <= 1e-5 * abs(gold)
+
+
+def test_dropin_loop_with_exported_windows_on_the_gpu():
+    """batched_optimize_problem_loop over exported golden windows, saved through the ECOS inversion."""
+    import types
+
+    import pandas as pd
+    ws = _windows("es")
+
+    class Exporter:
+        def export(self, functions, constraints):
+            data, col, ew, _ = functions["w"]
+            return dropin.CvxpyWindow(ew, ecos_forms.FakeProblem(data, col))
+
+    saved = []
+    sc = types.SimpleNamespace(
+        optimization_levels=pd.DataFrame({"predictive": np.arange(len(ws))}),
+        poi=types.SimpleNamespace(der_list=[], active_ders=[], is_sizing_optimization=False),
+        service_agg=types.SimpleNamespace(identify_system_requirements=lambda *a: {},
+                                          post_facto_reliability_only=lambda: False,
+                                          post_facto_reliability_only_and_user_defined_constraints=lambda: False,
+                                          value_streams={}),
+        opt_years=[2017], frequency="1h", opt_engine=True,
+        set_up_optimization=lambda w, annuity_scalar=1, ignore_der_costs=False: ({"w": ws[w]}, ["c"], w),
+        save_optimization_results=lambda w, si, prob, obj, err: saved.append((w, prob.status, prob.value, err)))
+    with BatchSolver(0) as s:
+        dropin.batched_optimize_problem_loop(sc, solver=s, exporter=Exporter())
+        assert s.kernel_stats()["band_windows"] == len(ws)
+    assert [w for w, *_ in saved] == list(range(len(ws)))
+    for (w, status, value, err), (_, _, _, gold) in zip(saved, ws):
+        assert status == "optimal" and err is None and abs(value - gold) <= 1e-5 * abs(gold)

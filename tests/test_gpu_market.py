@@ -90,6 +90,7 @@ def test_reserve_windows_match_highs(gpu_solver):
     days = list(range(0, 365, 15))
     g = scenarios.market_days(sig, meta["params"], days=days, reserves=reserve_series(sig, pdis))
     res = gpu_solver.solve(builder.group_window_lps(g))
+    assert gpu_solver.kernel_stats()["ell_windows"] == len(days), gpu_solver.kernel_stats()  # small-window ELL
     for k, (d, r) in enumerate(zip(days, res)):
         o = dict(K=sp_csr(g, k), q=g.q[k], c=g.c[k], c0=float(g.c0[k]), l=g.l[k], u=g.u[k], m_eq=g.m_eq)
         h = window_lp.solve_highs(o)
@@ -112,6 +113,13 @@ def test_load_following_windows_match_highs(gpu_solver, combined):
     g = scenarios.market_days(sig, meta["params"], days=days, reserves=reserve_series(sig, pdis),
                               lf=_lf(sig, pdis, combined=combined))
     res = gpu_solver.solve(builder.group_window_lps(g))
+    assert gpu_solver.kernel_stats()["ell_windows"] == len(days), gpu_solver.kernel_stats()
+    # the oracle's direct form (options written into the SOE rows, no aggregate columns; tests/test_market_reserves)
+    from test_market_reserves import _oracle_window
+    wins, _ = cases.market_windows("es")
+    res_series = reserve_series(sig, pdis)
+    lf = _lf(sig, pdis, combined=combined)
+    T = g.T
     for k, (d, r) in enumerate(zip(days, res)):
         o = dict(K=sp_csr(g, k), q=g.q[k], c=g.c[k], c0=float(g.c0[k]), l=g.l[k], u=g.u[k], m_eq=g.m_eq)
         h = window_lp.solve_highs(o)
@@ -119,3 +127,11 @@ def test_load_following_windows_match_highs(gpu_solver, combined):
         pres, _ = window_lp.primal_residual_rel(o, r.x)
         assert pres <= PRES_TOL, (d, pres)
         assert abs(r.obj - h["obj"]) <= OBJ_TOL * max(abs(h["obj"]), 1.0), (d, r.obj, h["obj"])
+        w = _oracle_window(wins[d], res_series, T)
+        sl = slice(d * T, d * T + T)
+        w["lf"] = {key: (v[sl] if np.ndim(v) else v) for key, v in lf.items()}
+        od = window_lp.build(w)
+        x0 = r.x[:od["K"].shape[1]]
+        # the uch / udis definition rows' residual adds to the SOE rows' in the direct form: bar x3
+        assert window_lp.primal_residual_rel(od, x0)[0] <= 3 * PRES_TOL, d
+        assert abs(od["c"] @ x0 + od["c0"] - r.obj) <= 1e-9 * max(abs(r.obj), 1.0)

@@ -88,12 +88,16 @@ def test_seeded_sweep_on_gpu_matches_cold_and_highs():
     ctags = [t for g in scenarios.config4(ids) for t in g.tags]
     cobj = {t: cst[k, 0] for k, t in enumerate(ctags)}
     rel = [abs(st[k, 0] - cobj[t]) / max(abs(cobj[t]), 1.0) for k, t in enumerate(sw.tags)]
-    assert max(rel) <= 2e-5
+    assert max(rel) <= 1e-5  # both within the objective-error termination (eps_obj 1e-6) of the optimum
     assert ist[sw.n_seed:, 1].mean() < 0.85 * cist[:, 1].mean()
-    for k in range(0, sw.packed.count, 97):
-        h = window_lp.solve_highs(window_lp.from_packed_window(sw.packed.window(k)))
-        assert abs(st[k, 0] - h["obj"]) <= 1e-5 * max(abs(h["obj"]), 1.0), (k, st[k, 0], h["obj"])
-        assert st[k, 1] <= 1e-6
+    # every window against HiGHS (the north_star gate: objective within 1e-5, primal residual <= 1e-6)
+    from oracle import cpu_baseline
+    lps = [window_lp.from_packed_window(sw.packed.window(k)) for k in range(sw.packed.count)]
+    hobj, hst, _, _ = cpu_baseline.highs_batch(lps, 8)
+    assert (hst == 0).all()
+    err = np.abs(st[:, 0] - hobj) / np.maximum(np.abs(hobj), 1.0)
+    assert err.max() <= 1e-5, (int(err.argmax()), float(err.max()))
+    assert st[:, 1].max() <= 1e-6
 
 
 def test_seed_split_feature_partners_are_nearest_in_standardised_features():
