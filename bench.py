@@ -42,6 +42,94 @@ def alg_bytes_per_iter(desc):
     n, m, nnz = desc[:, 0].astype(np.float64), desc[:, 1].astype(np.float64), desc[:, 3].astype(np.float64)
     return 24 * nnz + 4 * (n + m) + 72 * n + 48 * m
 
+# FP64 vector peak: 256 CUs x 4 SIMDs x 16 FP64 FMA lanes per clock x 2 FLOP x 2.4 GHz = 78.6 TFLOP/s (AMD spec; half the
+# 157.3 TFLOP/s FP32 vector rate of MI355X_MICROARCH.md "Chip-level parameters")
+FP64_PEAK_TFLOPS = 256 * 4 * 16 * 2 * 2.4e9 / 1e12
+
+
+def source_key():
+    """Hash of the kernel sources: PMC profiles under profiles/ are used only for the kernels they measured."""
+    import hashlib
+    h = hashlib.sha1()
+    csrc = os.path.join(ROOT, "der-vet_amd", "csrc")
+    for f in sorted(os.listdir(csrc)):
+        with open(os.path.join(csrc, f), "rb") as fh:
+            h.update(f.encode() + fh.read())
+    return h.hexdigest()[:12]
+
+
+def pmc_profiles(count, launches):
+    """PMC results of this exact workload and kernel build (profiles/pdhg_traffic.json: FETCH_SIZE / WRITE_SIZE
+    passes; profiles/pdhg_valu.json: SQ instruction counters), or {} when they were measured on other sources."""
+    out = {}
+    key = source_key()
+    for name in ("pdhg_traffic", "pdhg_valu"):
+        fn = os.path.join(ROOT, "profiles", f"{name}.json")
+        if not os.path.exists(fn):
+            continue
+        with open(fn) as f:
+            j = json.load(f)
+        if j.get("windows") == count and j.get("source_key") == key and \
+                j.get("launches_per_step", j.get("dispatches_per_step")) == launches:
+            out[name] = j
+    return out
+
+
+def stream_copy_gbps(dev, gib=2.0, reps=10):
+    """Measured HBM copy ceiling on this GPU (torch device-to-device copy, read + write bytes / time)."""
+    n = int(gib * 2 ** 30 / 8)
+    a = torch.empty(n, dtype=torch.float64, device=f"cuda:{dev}").fill_(1.0)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    gbps = 2.0 * 8 * n * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    return gbps
+
+
+def roofline_object(alg, pdhg_s, prof, kname, launches, copy_gbps):
+    """The dominant kernel's bound.  The iterate and scaled K of a window stay in VGPRs / LDS for the whole solve, so
+    HBM moves only inputs, warm starts and outputs: the binding resource is the FP64 VALU pipe and its latency, and
+    that is the headline (achieved FP64 FLOP/s from PMC instruction counts / PDHG kernel time, vs the 78.6 TFLOP/s
+    FP64 vector peak).  HBM: PMC bytes / time vs 8 TB/s and the measured copy ceiling.  The SURVEY.md 8d
+    algorithmic bytes / time is reported as the "effective" rate of an HBM-streaming formulation."""
+    r = {"bound": "valu-fp64", "achieved": None, "peak": round(FP64_PEAK_TFLOPS, 2), "unit": "TFLOP/s", "frac": None,
+         "traffic": None, "kernel": kname + f": {launches} launch(es) per step; times from HIP events on the solver "
+                                             "stream", "source_key": source_key()}
+    v = prof.get("pdhg_valu")
+    if v and pdhg_s > 0:
+        c = v["counters_per_step"]
+        fl = 64.0 * (2.0 * c.get("SQ_INSTS_VALU_FMA_F64", 0.0) + c.get("SQ_INSTS_VALU_ADD_F64", 0.0) +
+                     c.get("SQ_INSTS_VALU_MUL_F64", 0.0))
+        r["achieved"] = round(fl / pdhg_s / 1e12, 3)
+        r["frac"] = round(fl / pdhg_s / 1e12 / FP64_PEAK_TFLOPS, 4)
+        r["fp64_flops_per_step"] = fl
+        valu = c.get("SQ_INSTS_VALU", 0.0)
+        r["issue"] = {"valu_wave_insts_per_s": valu / pdhg_s, "peak": VALU_PEAK_WAVE_INSTS,
+                      "frac": round(valu / pdhg_s / VALU_PEAK_WAVE_INSTS, 4),
+                      "fp64_share_of_valu": round((c.get("SQ_INSTS_VALU_FMA_F64", 0.0) + c.get("SQ_INSTS_VALU_ADD_F64", 0.0)
+                                                   + c.get("SQ_INSTS_VALU_MUL_F64", 0.0)) / max(valu, 1.0), 4)}
+        r["pmc_counters"] = "profiles/pdhg_valu.json"
+    t = prof.get("pdhg_traffic")
+    hbm = {"peak": HBM_PEAK_GBS, "unit": "GB/s", "stream_copy": round(copy_gbps, 1)}
+    if t and pdhg_s > 0:
+        r["traffic"] = t["hbm_bytes_per_step"]
+        a = t["hbm_bytes_per_step"] / pdhg_s / 1e9
+        hbm.update(achieved=round(a, 1), frac=round(a / HBM_PEAK_GBS, 5), frac_of_stream_copy=round(a / copy_gbps, 5),
+                   pmc_counters="profiles/pdhg_traffic.json (FETCH_SIZE x2 + WRITE_SIZE)")
+    r["hbm"] = hbm
+    r["effective"] = {"alg_bytes_per_step": alg, "GBps": round(alg / pdhg_s / 1e9, 1) if pdhg_s > 0 else None,
+                      "note": "SURVEY.md 8d B_iter = 24 nnz + 4 (n + m) + 72 n + 48 m per window-iteration x iterations; "
+                              "what an HBM-streaming formulation of the same iterations would move"}
+    return r
+
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -151,35 +239,9 @@ def main():
     achieved = alg / pdhg_s / 1e9 if pdhg_s > 0 else None
     status_counts = np.bincount(ist[:, 0] + 1, minlength=6)[1:].tolist()  # OPTIMAL..NUMERICAL
     optimal_frac = float(np.mean(ist[:, 0] == 0))
-    traffic = None
-    tf = os.path.join(ROOT, "profiles", "pdhg_traffic.json")
-    if os.path.exists(tf):
-        with open(tf) as f:
-            tj = json.load(f)
-        if tj.get("windows") == count:
-            lps = 2 if sweep is not None and count > sweep.n_seed else 1
-            if tj.get("kernel", "").startswith(kname.split()[0]) and tj.get("launches_per_step", 1) == lps:
-                traffic = tj.get("hbm_bytes_per_step", tj.get("hbm_bytes_per_launch"))
-
-    # the kernel's actual bound: VALU issue (PMC SQ_INSTS_VALU of one step's PDHG launches, profiles/pdhg_valu.json)
-    compute = None
-    vf = os.path.join(ROOT, "profiles", "pdhg_valu.json")
-    if os.path.exists(vf) and achieved:
-        with open(vf) as f:
-            vj = json.load(f)
-        lps = 2 if sweep is not None and count > sweep.n_seed else 1
-        if vj.get("windows") == count and vj.get("dispatches_per_step") == lps:
-            cps = vj["counters_per_step"]
-            valu = cps.get("SQ_INSTS_VALU")
-            if valu:
-                compute = {"bound": "valu", "achieved": valu / pdhg_s, "peak": VALU_PEAK_WAVE_INSTS,
-                           "unit": "VALU wave-instructions/s", "frac": round(valu / pdhg_s / VALU_PEAK_WAVE_INSTS, 3),
-                           "valu_per_window_iteration": round(valu / float(iters.sum()), 1),
-                           "salu_per_window_iteration": round(cps.get("SQ_INSTS_SALU", 0.0) / float(iters.sum()), 1),
-                           "lds_per_window_iteration": round(cps.get("SQ_INSTS_LDS", 0.0) / float(iters.sum()), 1),
-                           "note": "PMC pass over one step (profiles/pdhg_valu.json, same schedule and batch); peak = "
-                                   "one VALU wave-instruction per 2 cycles per SIMD at 2.4 GHz; FP64 FMA / ADD / MUL "
-                                   "issue at half that rate"}
+    lps_step = 2 if sweep is not None and count > sweep.n_seed else 1
+    prof = pmc_profiles(count, lps_step)
+    roofline = roofline_object(alg, pdhg_s, prof, kname, lps_step, stream_copy_gbps(local))
 
     schedule = {"kind": args.schedule}
     if sweep is not None:
@@ -207,20 +269,28 @@ def main():
     cpu = None
     parity = None
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0:
-        from oracle import cpu_baseline, window_lp
+        from oracle import cba, cpu_baseline, window_lp
         idx = np.linspace(0, count - 1, min(args.cpu_sample, count)).astype(np.int64)
         lps = [window_lp.from_packed_window(pb.window(int(k))) for k in idx]
         objs, sts, wall, procs = cpu_baseline.highs_batch(lps, args.cpu_procs or None)
         cpu = {"value": round(len(idx) / wall, 2), "unit": "windows/s", "cores": procs, "kind": "port",
+               "cpu_model": cpu_baseline.cpu_model(),
                "sample": f"{len(idx)} of the {count} config-4 windows (evenly spaced), restated LP + HiGHS "
-                         f"(scipy {__import__('scipy').__version__}), one LP per process, {procs} processes, "
-                         f"{wall:.1f} s wall"}
+                         f"(scipy {__import__('scipy').__version__}), one LP per process, {procs} processes "
+                         f"(the GPU box's CPU share; os.cpu_count() there reports the whole host), {wall:.1f} s wall"}
         g = st[idx, 0]
         ok = sts == 0
         rel = np.abs(g[ok] - objs[ok]) / np.maximum(np.abs(objs[ok]), 1e-12)
+        # battery benefit: obj_no_battery - obj, the error of the GPU's relative to HiGHS'
+        nb = np.array([cba.no_battery_objective(lp) for lp in lps])
+        ben_h = nb[ok] - objs[ok]
+        ben_rel = np.abs(g[ok] - objs[ok]) / np.maximum(np.abs(ben_h), 1e-12)
         parity = {"sample_windows": int(len(idx)), "highs_optimal": int(ok.sum()),
                   "max_obj_rel_err_vs_highs": float(rel.max()) if ok.any() else None,
-                  "frac_obj_rel_err_le_1e-5": float(np.mean(rel <= 1e-5)) if ok.any() else None}
+                  "frac_obj_rel_err_le_1e-5": float(np.mean(rel <= 1e-5)) if ok.any() else None,
+                  "max_benefit_rel_err": float(ben_rel.max()) if ok.any() else None,
+                  "median_benefit_usd": float(np.median(ben_h)) if ok.any() else None,
+                  "full_population": "profiles/r02_certify.json (all 120,000 windows vs HiGHS)"}
 
     line = {
         "metric": METRIC,
@@ -251,18 +321,7 @@ def main():
         "kernel_ms": {"setup": round(tm["setup_ms"], 2), "pdhg": round(tm["pdhg_ms"], 2),
                       "solve_total": round(tm["total_ms"], 2)},
         "kernel_path": ks,
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 3) if achieved else None,
-                     "traffic": traffic,
-                     "traffic_note": "HBM bytes of one step's PDHG launches (PMC FETCH_SIZE x2 + WRITE_SIZE, "
-                                     "profiles/pdhg_traffic.json)",
-                     "kernel": kname + (": 2 launches per step (seed phase + warm phase)" if sweep is not None and
-                                        count > sweep.n_seed else ": 1 launch per step") +
-                               "; achieved = sum_w B_iter(w) * iters(w) / PDHG kernel time of the step "
-                               "(HIP events on the solver stream)",
-                     "note": "iterate and scaled K are VGPR/LDS-resident, so algorithmic bytes exceed what HBM "
-                             "moves; frac > 1 means the on-chip design beats the HBM roofline"},
-        "compute": compute,
+        "roofline": roofline,
         "schedule": schedule,
         "cpu_baseline": cpu,
         "parity": parity,

@@ -1668,7 +1668,7 @@ hipError_t launch_pdhg(const Batch& b, const Work& w, const Chunk& ch, const Opt
 // Small windows (the daily market-service window: T = 24, n = 168, m <= 217, K^T rows <= 6, K rows <= 8): one
 // single-wave workgroup per window, so the loop's barriers are one-wave barriers and several windows share a
 // CU (a 512-thread workgroup per window would leave most lanes without a column or a row).
-static int small_variant() {  // DVH_SMALL=-1: off (A/B against the 512-thread kernels); 0..5: force a variant
+static int small_variant() {  // DVH_SMALL=-1: off (A/B against the 512-thread kernels); 0..6: force a variant
   static const int v = getenv("DVH_SMALL") ? atoi(getenv("DVH_SMALL")) : 99;
   return v;
 }
@@ -1691,6 +1691,9 @@ hipError_t small_dispatch(int max_n, int max_m, int wx, int wy, const Batch& b, 
   // two waves, K and K^T values in LDS (their SOE rows are long rows, reduced by several targets per wave,
   // which the register-resident KR variants do not take)
   DVH_SMALL(5, 128, 3, 4, 6, 8, 0, 2)
+  // ... with CombinedMarket load following (one more equality block: n = 17 T = 408, m ~ 22 T at T = 24; the LF
+  // columns sit in 5 rows, beyond the 512-thread kernels' K^T width 4)
+  DVH_SMALL(6, 256, 2, 3, 6, 8, 0, 2)
 #undef DVH_SMALL
   return hipErrorInvalidValue;
 }
@@ -1698,7 +1701,7 @@ static bool small_enabled() { return small_variant() >= 0; }
 
 hipError_t launch_pdhg_ell(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n, int max_m,
                            int wx, int wy, hipStream_t s, int* variant_out, const int32_t* list, int nlist) {
-  if (max_n <= 384 && max_m <= 512 && wx <= 6 && wy <= 8 && small_enabled()) {
+  if (max_n <= 512 && max_m <= 768 && wx <= 6 && wy <= 8 && small_enabled()) {
     const hipError_t e = small_dispatch(max_n, max_m, wx, wy, b, w, ch, o, s, variant_out, list, nlist);
     if (e != hipErrorInvalidValue) return e;
     (void)hipGetLastError();  // no small variant covers the shape (e.g. DVH_SMALL forcing one): the 512-thread kernels

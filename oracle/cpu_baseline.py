@@ -15,6 +15,18 @@ import numpy as np
 from . import window_lp
 
 
+def cpu_model():
+    """CPU model name of this host (/proc/cpuinfo), for the bench line's cpu_baseline."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def _solve_one(lp):
     t = time.perf_counter()
     r = window_lp.solve_highs(lp)

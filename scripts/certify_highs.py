@@ -61,8 +61,26 @@ def solve(args):
     print(f"HiGHS: {len(idx)} windows in {wall:.0f} s on {args.procs} processes -> {args.out}", flush=True)
 
 
+def no_battery(scenarios_):
+    """obj_no_battery per window of the bench packing (battery idle, tau at the largest DCM rhs; oracle/cba.py
+    no_battery_objective, vectorised for the config-4 windows' single tau column)."""
+    from dervet_hip.lp import scenarios
+    from dervet_hip.sweep import SeededSweep
+    scen = range(scenarios_)
+    P = scenarios.sweep_parameters(scen)
+    pb = SeededSweep(scenarios.config4, scen, P["E"], stride=32, features=scenarios.sweep_features(P)).packed
+    d = pb.desc
+    nb = np.empty(pb.count)
+    for k in range(pb.count):
+        n, m, me, _, _, _, on, om = (int(v) for v in d[k])
+        assert n == 3 * (me - 1) + 1
+        nb[k] = pb.c0[k] + pb.c[on + n - 1] * pb.q[om + me:om + m].max()
+    return nb
+
+
 def compare(args):
     h = np.load(args.highs)
+    nb = no_battery(args.scenarios) if args.benefit else None
     out = {}
     for path in args.gpu:
         g = np.load(path)
@@ -75,7 +93,13 @@ def compare(args):
             rel = np.abs(st[:, 0] - h["obj"]) / np.abs(h["obj"])
             r = rel[ok]
             worst = np.argsort(-np.where(ok, rel, -1))[:20]
-            out[f"{os.path.basename(path)}:{ph}"] = dict(
+            ben = {}
+            if nb is not None:
+                br = (np.abs(st[:, 0] - h["obj"]) / np.abs(nb - h["obj"]))[ok]
+                ben = dict(max_benefit_rel=float(br.max()), p99_benefit_rel=float(np.quantile(br, 0.99)),
+                           median_benefit_usd=float(np.median((nb - h["obj"])[ok])),
+                           min_benefit_usd=float(np.min((nb - h["obj"])[ok])))
+            out[f"{os.path.basename(path)}:{ph}"] = dict(**ben,
                 windows=int(ok.sum()), gpu_optimal=int((ist[:, 0] == 0).sum()), max_rel=float(r.max()),
                 p99_rel=float(np.quantile(r, 0.99)), p999_rel=float(np.quantile(r, 0.999)), mean_rel=float(r.mean()),
                 n_gt_1e5=int((r > 1e-5).sum()), n_gt_5e6=int((r > 5e-6).sum()), n_gt_2e6=int((r > 2e-6).sum()),
@@ -100,6 +124,8 @@ def main():
     b.add_argument("--highs", default=os.path.join(ROOT, "gpurun_out", "certify", "highs.npz"))
     b.add_argument("--gpu", nargs="+", required=True)
     b.add_argument("--json", default=None)
+    b.add_argument("--benefit", action="store_true", help="also the battery-benefit error (obj_no_battery - obj)")
+    b.add_argument("--scenarios", type=int, default=10000)
     args = ap.parse_args()
     solve(args) if args.cmd == "solve" else compare(args)
 

@@ -52,7 +52,10 @@ def main():
     wv = [v for k in kern for v in write.get(k, [])]
     f_kb = sum(fv) / len(fv)
     w_kb = sum(wv) / len(wv) if wv else 0.0
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    from bench import source_key  # noqa: E402
     res = {
+        "source_key": source_key(),
         "kernel": re.search(r"pdhg_(band|ell)_kernel<[^>]*>", kern[0]).group(0),
         "windows": windows,
         "dispatches_fetch": len(fv), "dispatches_write": len(wv),

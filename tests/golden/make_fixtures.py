@@ -14,6 +14,8 @@ Sources (all paths relative to /root/reference):
   * test/datasets/000-004-timeseries_5min_negprices.csv                                           (config-3 input)
   * test/test_validation_report_sept1/Results/Usecase3/planned/step2/<case>/{timeseries_results,
     objective_values}uc3.csv + Model_params/Usecase3/planned/*_Step2.csv        (DA + FR market windows)
+  * test/test_validation_report_sept1/Results/Usecase2/<case>/step2/{simple_monthly_bill, pro_forma, npv}*.csv
+    (per-window bills with / without the DERs, the pro forma and its NPV row: battery-benefit and CBA parity)
 
 Usage:  python tests/golden/make_fixtures.py [/root/reference]
 """
@@ -240,8 +242,40 @@ def make_market_cases():
     print("wrote market cases", sorted(meta))
 
 
+def make_bills():
+    """Per-month bills (with the DERs / "Original" without them), the pro forma table and its NPV row of the
+    Usecase 2 monthly cases, plus the financial rates of their model parameters."""
+    out = {}
+    for name in ("es", "es+pv+dg"):
+        _, resdir, suf, mp = CASES[name]
+        _, bill = read_csv_cols(os.path.join(VR, resdir, f"simple_monthly_bill{suf}.csv"))
+        head, pf = read_csv_cols(os.path.join(VR, resdir, f"pro_forma{suf}.csv"))
+        nhead, npv = read_csv_cols(os.path.join(VR, resdir, f"npv{suf}.csv"))
+        params = read_params(os.path.join(VR, mp))
+        with open(os.path.join(VR, mp), encoding="utf-8-sig") as f:
+            rows = list(csv.DictReader(f))
+        raw = {(r["Tag"].strip(), r["Key"].strip()): (r["Optimization Value"] or "").strip() for r in rows if r["Key"]}
+        out[name] = {
+            "source_results": os.path.join("test/test_validation_report_sept1", resdir),
+            "month": bill["Month-Year"],
+            "energy_charge": fcol(bill, "Energy Charge ($)").tolist(),
+            "original_energy_charge": fcol(bill, "Original Energy Charge ($)").tolist(),
+            "demand_charge": fcol(bill, "Demand Charge ($)").tolist(),
+            "original_demand_charge": fcol(bill, "Original Demand Charge ($)").tolist(),
+            "proforma_index": pf[head[0]],
+            "proforma": {h: fcol(pf, h).tolist() for h in head[1:] if h},
+            "npv": {h: float(npv[h][0]) for h in nhead[1:] if h},
+            "npv_discount_rate": float(raw[("Finance", "npv_discount_rate")]),
+            "inflation_rate": float(raw[("Finance", "inflation_rate")]),
+            "growth": {"DCM": float(params["DCM"]["growth"]), "retailTimeShift": float(params["retailTimeShift"]["growth"])},
+        }
+    with open(os.path.join(HERE, "uc2_bills.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+    print("wrote bills", sorted(out))
+
+
 if __name__ == "__main__":
-    what = sys.argv[2:] or ["golden", "bench", "reliability", "market"]
+    what = sys.argv[2:] or ["golden", "bench", "reliability", "market", "bills"]
     if "golden" in what:
         make_golden_cases()
     if "bench" in what:
@@ -250,3 +284,5 @@ if __name__ == "__main__":
         make_reliability_cases()
     if "market" in what:
         make_market_cases()
+    if "bills" in what:
+        make_bills()
