@@ -197,6 +197,9 @@ def main():
 
     gathered = None
     phase = {}
+    runs = parallel.dispatch_runs(pb.desc) if dist is not None else None
+    tmax = max(r[4] for r in runs) if runs else 0
+    gather = {}
 
     def step():
         nonlocal gathered
@@ -205,8 +208,15 @@ def main():
         else:
             solver.solve_packed(dev)
         if dist is not None:
-            # the single RCCL all-gather of the results (objective, residuals, status, iterations)
-            gathered = parallel.gather_rows(parallel.result_rows(dev.stats, dev.istats))
+            # the single RCCL all-gather of every window's result row: objective, residuals, status, iterations and
+            # the ch / dis / ene dispatch (fixed stride 3 * tmax); equal window counts per rank (weak scaling)
+            torch.cuda.synchronize()
+            tg = time.perf_counter()
+            rows = parallel.result_rows(dev.stats, dev.istats, dev.x, pb.desc, tmax, runs)
+            gathered = parallel.gather_rows(rows, counts=[count] * world)
+            torch.cuda.synchronize()
+            gather.update(ms=round(1e3 * (time.perf_counter() - tg), 2), bytes_per_rank=int(rows.numel() * 8),
+                          bytes_total=int(gathered.numel() * 8), cols=int(rows.shape[1]), tmax=int(tmax))
 
     for _ in range(args.warmup):
         step()
@@ -324,6 +334,7 @@ def main():
         "roofline": roofline,
         "schedule": schedule,
         "cpu_baseline": cpu,
+        "gather": gather or None,
         "parity": parity,
         "build_s": round(build_s, 1),
     }

@@ -7,10 +7,12 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/dervet_hip.h"
@@ -67,6 +69,10 @@ struct dvh_handle {
   int kernel_path = 0;  // 0 band -> ELL -> generic, 1 generic only, 2 ELL -> generic (no band kernel)
   dvh::LargeSolver* large = nullptr;  // grid-wide path for windows above dvh::kSmallMax (created on first use)
   float large_ms[2] = {0, 0};         // setup, PDHG time of the large windows of the last solve
+  // Further devices of this handle (device_mask bits after the first, or dvh_create_devices): same options; a
+  // host-buffer batch is split into contiguous, cost-balanced ranges, one per device, solved concurrently (one host
+  // thread per device, no inter-device traffic), results written straight into the caller's buffers.
+  std::vector<dvh_handle*> peers;
 };
 
 static int fail(dvh_handle* h, int code, const std::string& msg) {
@@ -119,16 +125,43 @@ static std::string check_options(const dvh_options* o) {
   return "";
 }
 
+static int create_one(int dev, const dvh_options* opts, dvh_handle** out);
+
+int dvh_create_devices(const int32_t* devices, int32_t n, const dvh_options* opts, dvh_handle** out) {
+  if (!out || !devices || n < 1) return DVH_ERR_ARG;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return DVH_ERR_HIP;
+  for (int i = 0; i < n; ++i)
+    if (devices[i] < 0 || devices[i] >= ndev) return DVH_ERR_ARG;
+  dvh_handle* h = nullptr;
+  if (int rc = create_one(devices[0], opts, &h)) return rc;
+  for (int i = 1; i < n; ++i) {
+    dvh_handle* p = nullptr;
+    if (int rc = create_one(devices[i], opts, &p)) {
+      dvh_destroy(h);
+      return rc;
+    }
+    h->peers.push_back(p);
+  }
+  *out = h;
+  return DVH_OK;
+}
+
 int dvh_create(int device_mask, const dvh_options* opts, dvh_handle** out) {
   if (!out) return DVH_ERR_ARG;
   *out = nullptr;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return DVH_ERR_HIP;
-  int dev = 0;
-  if (device_mask > 0) {
-    while (dev < 31 && !((device_mask >> dev) & 1)) ++dev;
-  }
-  if (dev >= ndev) return DVH_ERR_ARG;
+  std::vector<int32_t> devs;
+  for (int d = 0; d < 31 && d < ndev; ++d)
+    if ((device_mask >> d) & 1) devs.push_back(d);
+  if (device_mask <= 0) devs = {0};
+  if (devs.empty() || (device_mask >> std::min(ndev, 31)) != 0) return DVH_ERR_ARG;  // a bit beyond the devices
+  return dvh_create_devices(devs.data(), (int32_t)devs.size(), opts, out);
+}
+
+static int create_one(int dev, const dvh_options* opts, dvh_handle** out) {
   dvh_handle* h = new dvh_handle();
   h->device = dev;
   dvh_default_options(&h->opts);
@@ -163,11 +196,16 @@ int dvh_set_options(dvh_handle* h, const dvh_options* opts) {
   std::string m = check_options(opts);
   if (!m.empty()) return fail(h, DVH_ERR_ARG, m);
   h->opts = *opts;
+  for (dvh_handle* p : h->peers) p->opts = *opts;
   return DVH_OK;
 }
 
+int dvh_device_count(const dvh_handle* h) { return h ? 1 + (int)h->peers.size() : 0; }
+
 int dvh_destroy(dvh_handle* h) {
   if (!h) return DVH_ERR_ARG;
+  for (dvh_handle* p : h->peers) dvh_destroy(p);
+  h->peers.clear();
   hipSetDevice(h->device);
   if (h->stream) hipStreamSynchronize(h->stream);
   DevBuf* bufs[] = {&h->d_desc, &h->d_indptr, &h->d_indices, &h->d_data, &h->d_c, &h->d_c0, &h->d_q, &h->d_l,
@@ -221,6 +259,7 @@ int dvh_last_path_counts4(const dvh_handle* h, int32_t* out4) {
 int dvh_set_kernel_path(dvh_handle* h, int mode) {
   if (!h || mode < 0 || mode > 2) return DVH_ERR_ARG;
   h->kernel_path = mode;
+  for (dvh_handle* p : h->peers) p->kernel_path = mode;
   return DVH_OK;
 }
 
@@ -702,10 +741,71 @@ static std::string validate(const dvh_lp& lp, int k) {
   return "";
 }
 
+static int solve_batch_one(dvh_handle* h, const dvh_lp* lps, int32_t count, dvh_result* out);
+
+// Contiguous, cost-balanced ranges of the batch for the handle's devices (windows the on-chip kernels take cost one
+// workgroup each; larger windows run grid-wide and cost in proportion to their nonzeros; dervet_hip/parallel.py
+// window_cost / shard_weighted are the same rule for ranks).
+static std::vector<int> split_batch(const dvh_lp* lps, int32_t count, int parts) {
+  std::vector<double> cum(count + 1, 0.0);
+  for (int k = 0; k < count; ++k) {
+    const dvh_lp& lp = lps[k];
+    const bool big = lp.n > dvh::kSmallMax || lp.m_eq + lp.m_ineq > dvh::kSmallMax;
+    cum[k + 1] = cum[k] + (big ? std::max(1.0, lp.nnz / 5208.0) : 1.0);
+  }
+  std::vector<int> b(parts + 1, count);
+  b[0] = 0;
+  for (int r = 1; r < parts; ++r) {
+    const double target = cum[count] * r / parts;
+    int k = b[r - 1];
+    while (k < count && cum[k] + 0.5 * (cum[k + 1] - cum[k]) < target) ++k;
+    b[r] = k;
+  }
+  return b;
+}
+
 extern "C" int dvh_solve_batch(dvh_handle* h, const dvh_lp* lps, int32_t count, dvh_result* out) {
   if (!h) return DVH_ERR_ARG;
   if (count < 0 || (count > 0 && (!lps || !out))) return fail(h, DVH_ERR_ARG, "null lps/out or negative count");
   if (count == 0) return DVH_OK;
+  if (h->peers.empty()) return solve_batch_one(h, lps, count, out);
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<dvh_handle*> hs = {h};
+  hs.insert(hs.end(), h->peers.begin(), h->peers.end());
+  const int P = (int)hs.size();
+  const std::vector<int> b = split_batch(lps, count, P);
+  std::vector<int> rc(P, DVH_OK);
+  std::vector<std::thread> th;
+  for (int i = 1; i < P; ++i)
+    if (b[i + 1] > b[i]) th.emplace_back([&, i] { rc[i] = solve_batch_one(hs[i], lps + b[i], b[i + 1] - b[i], out + b[i]); });
+  if (b[1] > b[0]) rc[0] = solve_batch_one(h, lps, b[1], out);
+  for (auto& t : th) t.join();
+  int nell = 0, ngen = 0, nlarge = 0, nband = 0;
+  double setup = 0.0, pdhg = 0.0;
+  for (int i = 0; i < P; ++i) {
+    if (rc[i] != DVH_OK) {
+      const std::string msg = hs[i]->err;  // copy first: hs[0] is h
+      return fail(h, rc[i], "device " + std::to_string(hs[i]->device) + " (part " + std::to_string(i) + "): " + msg);
+    }
+    if (b[i + 1] == b[i]) continue;
+    nell += hs[i]->n_ell;
+    ngen += hs[i]->n_generic;
+    nlarge += hs[i]->n_large;
+    nband += hs[i]->n_band;
+    setup = std::max(setup, hs[i]->timing[1]);
+    pdhg = std::max(pdhg, hs[i]->timing[2]);
+  }
+  h->n_ell = nell;
+  h->n_generic = ngen;
+  h->n_large = nlarge;
+  h->n_band = nband;
+  h->timing[0] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  h->timing[1] = setup;
+  h->timing[2] = pdhg;
+  return DVH_OK;
+}
+
+static int solve_batch_one(dvh_handle* h, const dvh_lp* lps, int32_t count, dvh_result* out) {
   DVH_HIP(h, hipSetDevice(h->device));
   std::vector<int64_t> desc(8 * (size_t)count);
   int64_t tn = 0, tm = 0, tz = 0, tr = 0;

@@ -65,6 +65,9 @@ SYMBOLS = {
     "dvh_version": (ctypes.c_char_p, []),
     "dvh_default_options": (None, [ctypes.POINTER(Options)]),
     "dvh_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(Options), ctypes.POINTER(ctypes.c_void_p)]),
+    "dvh_create_devices": (ctypes.c_int, [c_int32_p, ctypes.c_int32, ctypes.POINTER(Options),
+                                          ctypes.POINTER(ctypes.c_void_p)]),
+    "dvh_device_count": (ctypes.c_int, [ctypes.c_void_p]),
     "dvh_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "dvh_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
     "dvh_set_options": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Options)]),

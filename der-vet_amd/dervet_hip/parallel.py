@@ -2,10 +2,21 @@
 
 The reference runs sensitivity cases serially (dervet/DERVET.py:75) and windows serially
 (dervet/MicrogridScenario.py:310); every window LP is independent, so ranks take disjoint,
-contiguous scenario ranges, solve with no inter-GPU traffic, and ONE all-gather (RCCL over xGMI with the
-"nccl" backend, gloo in CPU tests) returns every window's result rows to every rank in global order.
+contiguous ranges of windows, solve with no inter-GPU traffic, and ONE all-gather (RCCL over xGMI with the "nccl"
+backend, gloo in CPU tests) returns every window's result row -- objective, residuals, status, iterations and the
+dispatch time series (ch, dis, ene, padded to a fixed stride) -- to every rank in global order, where the
+ServiceAggregator / POI results consume them.
+
+Partitions:
+  * ``weak_shard``: every rank owns the same number of scenarios (the bench's weak scaling);
+  * ``shard``: a fixed total split into near-equal contiguous counts;
+  * ``shard_weighted``: a fixed batch split into contiguous ranges of near-equal estimated cost
+    (``window_cost``: on-chip windows cost one workgroup each, grid-wide windows in proportion to their nonzeros),
+    for heterogeneous batches (strong scaling).
 """
 import numpy as np
+
+RESULT_COLS = 6  # obj, primal_res_rel, dual_res_rel, gap_rel, status, iters
 
 
 def shard(total, world, rank):
@@ -20,30 +31,97 @@ def weak_shard(per_rank, rank):
     return rank * per_rank, (rank + 1) * per_rank
 
 
-def gather_rows(rows, group=None):
-    """All-gather a [k_r, w] float64 tensor of per-window result rows from every rank (k_r may differ);
-    returns the concatenation in rank order (identical on every rank)."""
+def window_cost(desc, small_max=4096, ref_nnz=5208):
+    """Estimated relative solve cost per window from its descriptor rows {n, m, m_eq, nnz, ...}: windows the
+    on-chip kernels take (n, m <= small_max) cost one workgroup each (per-iteration time does not depend on their
+    size); larger windows run grid-wide, in proportion to their nonzeros (ref_nnz: a monthly battery + DCM window)."""
+    d = np.asarray(desc)
+    big = (d[:, 0] > small_max) | (d[:, 1] > small_max)
+    return np.where(big, np.maximum(d[:, 3] / float(ref_nnz), 1.0), 1.0)
+
+
+def shard_weighted(weights, world, rank):
+    """Contiguous [start, stop) of the units whose cumulative weight falls in rank's equal share (deterministic;
+    every unit assigned exactly once, ranges in rank order)."""
+    w = np.asarray(weights, np.float64)
+    if len(w) == 0:
+        return 0, 0
+    cum = np.concatenate([[0.0], np.cumsum(w)])
+    total = cum[-1]
+    # boundary r: first unit whose cumulative weight (up to its midpoint) reaches r / world of the total
+    mids = cum[:-1] + 0.5 * w
+    bounds = [0] + [int(np.searchsorted(mids, total * r / world)) for r in range(1, world)] + [len(w)]
+    return bounds[rank], bounds[rank + 1]
+
+
+def dispatch_runs(desc):
+    """Runs of consecutive windows with the same n and contiguous x offsets: (k0, k1, off_n of k0, n, T) with
+    T = m_eq - 1 the steps of a battery window (its dispatch = x[:3T] = ch, dis, ene)."""
+    d = np.asarray(desc)
+    runs = []
+    k = 0
+    while k < len(d):
+        k1 = k + 1
+        while k1 < len(d) and d[k1, 0] == d[k, 0] and d[k1, 2] == d[k, 2] and d[k1, 6] == d[k1 - 1, 6] + d[k, 0]:
+            k1 += 1
+        runs.append((k, k1, int(d[k, 6]), int(d[k, 0]), int(d[k, 2]) - 1))
+        k = k1
+    return runs
+
+
+def result_rows(stats, istats, x=None, desc=None, tmax=None, runs=None):
+    """Per-window result rows (float64): {obj, primal_res_rel, dual_res_rel, gap_rel, status, iters} and, with x /
+    desc, the window's dispatch ch, dis, ene in a fixed stride of 3 * tmax (zero padded).  Works on device or host
+    tensors (strided copies per run of equal windows; no index tensors)."""
+    import torch
+    base = torch.cat([stats.to(torch.float64), istats.to(torch.float64)], dim=1)
+    if x is None:
+        return base.contiguous()
+    runs = runs if runs is not None else dispatch_runs(desc)
+    tmax = int(tmax or max(r[4] for r in runs))
+    rows = torch.zeros((base.shape[0], RESULT_COLS + 3 * tmax), dtype=torch.float64, device=base.device)
+    rows[:, :RESULT_COLS] = base
+    for k0, k1, on, n, T in runs:
+        xs = x[on:on + (k1 - k0) * n].view(k1 - k0, n)
+        for v in range(3):  # ch, dis, ene blocks, each padded to tmax
+            rows[k0:k1, RESULT_COLS + v * tmax:RESULT_COLS + v * tmax + T] = xs[:, v * T:(v + 1) * T]
+    return rows
+
+
+def gather_rows(rows, group=None, counts=None):
+    """All-gather a [k_r, w] float64 tensor of per-window result rows from every rank; returns the concatenation in
+    rank order (identical on every rank).  counts: every rank's k_r when known on all ranks (weak scaling, a
+    deterministic shard): then the rows go out in ONE all-gather; otherwise the counts are exchanged first."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    k = torch.tensor([rows.shape[0]], dtype=torch.int64, device=rows.device)
-    ks = [torch.zeros_like(k) for _ in range(world)]
-    dist.all_gather(ks, k, group=group)
-    kmax = int(max(int(v.item()) for v in ks))
-    pad = torch.zeros((kmax, rows.shape[1]), dtype=rows.dtype, device=rows.device)
-    pad[: rows.shape[0]] = rows
-    outs = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(outs, pad, group=group)
-    return torch.cat([o[: int(n.item())] for o, n in zip(outs, ks)], dim=0)
+    if counts is None:
+        k = torch.tensor([rows.shape[0]], dtype=torch.int64, device=rows.device)
+        ks = [torch.zeros_like(k) for _ in range(world)]
+        dist.all_gather(ks, k, group=group)
+        counts = [int(v.item()) for v in ks]
+    kmax = max(counts)
+    if rows.shape[0] == kmax:
+        pad = rows.contiguous()
+    else:
+        pad = torch.zeros((kmax, rows.shape[1]), dtype=rows.dtype, device=rows.device)
+        pad[: rows.shape[0]] = rows
+    out = torch.empty((world * kmax, rows.shape[1]), dtype=rows.dtype, device=rows.device)
+    if hasattr(dist, "all_gather_into_tensor") and dist.get_backend(group) != "gloo":
+        dist.all_gather_into_tensor(out, pad, group=group)
+    else:
+        dist.all_gather(list(out.chunk(world)), pad, group=group)
+    if all(n == kmax for n in counts):
+        return out
+    return torch.cat([out[r * kmax:r * kmax + n] for r, n in enumerate(counts)], dim=0)
 
 
-def result_rows(stats, istats):
-    """Per-window result rows {obj, primal_res_rel, dual_res_rel, gap_rel, status, iters} (float64)."""
-    import torch
-    return torch.cat([stats.to(torch.float64), istats.to(torch.float64)], dim=1).contiguous()
-
-
-def rows_to_numpy(rows):
+def rows_to_numpy(rows, tmax=None):
     r = rows.detach().cpu().numpy()
-    return dict(obj=r[:, 0], primal_res_rel=r[:, 1], dual_res_rel=r[:, 2], gap_rel=r[:, 3],
-                status=r[:, 4].astype(np.int32), iters=r[:, 5].astype(np.int64))
+    out = dict(obj=r[:, 0], primal_res_rel=r[:, 1], dual_res_rel=r[:, 2], gap_rel=r[:, 3],
+               status=r[:, 4].astype(np.int32), iters=r[:, 5].astype(np.int64))
+    if r.shape[1] > RESULT_COLS:
+        tm = tmax or (r.shape[1] - RESULT_COLS) // 3
+        out.update(ch=r[:, RESULT_COLS:RESULT_COLS + tm], dis=r[:, RESULT_COLS + tm:RESULT_COLS + 2 * tm],
+                   ene=r[:, RESULT_COLS + 2 * tm:RESULT_COLS + 3 * tm])
+    return out

@@ -81,17 +81,26 @@ def _init_torch_first():
 
 
 class BatchSolver:
-    """One GPU, one HIP stream.  Options are dvh_options fields (eps, max_iters, ...)."""
+    """A libdervet_hip handle: one GPU (``device``) or several (``devices``: a host-buffer batch is split over them
+    and solved concurrently; devices may repeat).  Options are dvh_options fields (eps, max_iters, ...)."""
 
-    def __init__(self, device=0, **options):
+    def __init__(self, device=0, devices=None, **options):
         _init_torch_first()
         self._lib = _lib.load()
         self._opts = _lib.default_options(**options)
         h = ctypes.c_void_p()
-        rc = self._lib.dvh_create(1 << int(device), ctypes.byref(self._opts), ctypes.byref(h))
+        if devices is None:
+            rc = self._lib.dvh_create(1 << int(device), ctypes.byref(self._opts), ctypes.byref(h))
+        else:
+            arr = (ctypes.c_int32 * len(devices))(*[int(d) for d in devices])
+            rc = self._lib.dvh_create_devices(arr, len(devices), ctypes.byref(self._opts), ctypes.byref(h))
         if rc != 0:
-            raise SolverError(f"dvh_create failed ({rc}): no usable GPU device {device} or invalid options")
+            raise SolverError(f"dvh_create failed ({rc}): no usable GPU device {devices or device} or invalid options")
         self._h = h
+
+    @property
+    def device_count(self):
+        return int(self._lib.dvh_device_count(self._h))
 
     def close(self):
         if getattr(self, "_h", None):

@@ -22,8 +22,12 @@
  *                                PRIMAL_INFEASIBLE->"infeasible", DUAL_INFEASIBLE->"unbounded",
  *                                ITER_LIMIT->"optimal_inaccurate", NUMERICAL->"solver_error".
  *
- * Threading: one handle per host thread.  A handle drives one GPU (the lowest set bit of device_mask);
- * multi-GPU runs use one process (rank) per GPU, each with its own handle.
+ * Threading: one handle per host thread.  A handle drives every GPU whose bit is set in device_mask (0 = device 0):
+ * dvh_solve_batch splits a host-buffer batch into contiguous ranges of near-equal estimated cost, one per device,
+ * solved concurrently by one host thread per device (no inter-device traffic; each device writes its windows'
+ * results straight into the caller's dvh_result buffers).  Device-resident batches (dvh_solve_packed_device) and
+ * the reliability sweep run on the handle's first device.  Multi-process runs (one rank per GPU, torch.distributed
+ * / RCCL all-gather of the results) use one single-device handle per rank.
  * Return codes: 0 = OK, negative = usage / HIP error (message via dvh_last_error).
  */
 #ifndef DERVET_HIP_H
@@ -133,6 +137,10 @@ typedef struct dvh_handle dvh_handle;
 const char* dvh_version(void);
 void dvh_default_options(dvh_options* opts);
 int dvh_create(int device_mask, const dvh_options* opts, dvh_handle** out);
+/* The same with an explicit device list (devices may repeat: several concurrent sub-handles on one GPU). */
+int dvh_create_devices(const int32_t* devices, int32_t n, const dvh_options* opts, dvh_handle** out);
+/* Devices (sub-handles) of a handle. */
+int dvh_device_count(const dvh_handle* h);
 int dvh_destroy(dvh_handle* h);
 const char* dvh_last_error(const dvh_handle* h);
 int dvh_set_options(dvh_handle* h, const dvh_options* opts);

@@ -1,5 +1,6 @@
 """N > 1 path on CPU: two gloo ranks shard the scenario sweep with dervet_hip.parallel and all-gather the
-per-window result rows; the gathered rows equal a single-process run in global window order.
+per-window result rows (objective, residuals, status, iterations and the ch / dis / ene dispatch in a fixed
+stride); the gathered rows equal a single-process run in global window order, bit for bit.
 
 The per-window "solve" here is the oracle (HiGHS) standing in for the GPU kernel, because this container
 has no GPU; the sharding, ordering and the gather are exactly the code bench.py runs over RCCL.
@@ -23,19 +24,24 @@ def _free_port():
     return p
 
 
-def _rows_for(scenario_ids):
-    """Result rows (obj, 0, 0, 0, status, iters) for the windows of the given scenarios, via HiGHS."""
-    import scipy.sparse as sp
+def _rows_for(scenario_ids, tmax=744):
+    """Result rows (obj, 0, 0, 0, status, 0, ch, dis, ene padded to tmax) for the windows of the given scenarios,
+    via HiGHS."""
     from dervet_hip.lp import builder, scenarios
     from oracle import window_lp
     groups = scenarios.config4(scenario_ids)
     pb = builder.pack_groups(groups)
-    rows = []
+    stats = torch.zeros((pb.count, 4), dtype=torch.float64)
+    istats = torch.zeros((pb.count, 2), dtype=torch.int32)
+    x = torch.zeros(len(pb.c), dtype=torch.float64)
     for k in range(pb.count):
-        lp = window_lp.from_packed_window(pb.window(k))
-        r = window_lp.solve_highs(lp)
-        rows.append([r["obj"], 0.0, 0.0, 0.0, float(r["status"]), 0.0])
-    return torch.tensor(rows, dtype=torch.float64), pb.desc
+        w = pb.window(k)
+        r = window_lp.solve_highs(window_lp.from_packed_window(w))
+        stats[k, 0] = r["obj"]
+        istats[k, 0] = r["status"]
+        on = int(pb.desc[k, 6])
+        x[on:on + w["n"]] = torch.from_numpy(r["x"])
+    return parallel.result_rows(stats, istats, x, pb.desc, tmax), pb
 
 
 def _worker(rank, world, port, total, out):
@@ -45,7 +51,8 @@ def _worker(rank, world, port, total, out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     a, b = parallel.shard(total, world, rank)
     rows, _ = _rows_for(range(a, b))
-    g = parallel.gather_rows(rows)
+    counts = [12 * (lambda ab: ab[1] - ab[0])(parallel.shard(total, world, r)) for r in range(world)]
+    g = parallel.gather_rows(rows, counts=counts if total % world == 0 else None)
     if rank == 0:
         torch.save(g, out)
     dist.destroy_process_group()
@@ -69,7 +76,35 @@ def test_two_rank_gloo_gather_matches_single_process(tmp_path):
     mp.spawn(_worker, args=(2, _free_port(), total, out), nprocs=2, join=True)
     g = torch.load(out, weights_only=True)
     # single-process order: shard 0 = scenario 0 (then 1 on rank 1 ...): rebuild per shard and concatenate
-    ref = torch.cat([_rows_for(range(*parallel.shard(total, 2, r)))[0] for r in range(2)])
-    assert g.shape == (36, 6)
+    parts = [_rows_for(range(*parallel.shard(total, 2, r))) for r in range(2)]
+    ref = torch.cat([p[0] for p in parts])
+    assert g.shape == (36, 6 + 3 * 744)
     assert torch.equal(g, ref)
     assert (g[:, 4] == 0).all()
+    # the dispatch columns are the windows' ch / dis / ene
+    d = parallel.rows_to_numpy(g)
+    pb = parts[0][1]
+    w = pb.window(5)
+    T = w["m_eq"] - 1
+    assert np.array_equal(d["ch"][5, :T], ref.numpy()[5, 6:6 + T])
+    assert np.all(d["ene"][5, T:] == 0.0) or T == 744
+
+
+def test_weighted_shard_balances_cost_and_covers_once():
+    from dervet_hip.lp import builder, scenarios
+    w = np.array([1.0] * 50 + [40.0] + [1.0] * 49)
+    for world in (1, 2, 3, 4, 8):
+        seen, loads = [], []
+        for r in range(world):
+            a, b = parallel.shard_weighted(w, world, r)
+            seen += list(range(a, b))
+            loads.append(w[a:b].sum())
+        assert seen == list(range(len(w)))
+        assert max(loads) <= w.sum() / world + w.max()
+    pb = builder.pack_groups(scenarios.config4([0]))
+    c = parallel.window_cost(pb.desc)
+    assert np.all(c == 1.0)
+    big = pb.desc.copy()
+    big[0, 0] = 315360
+    big[0, 3] = 735840
+    assert parallel.window_cost(big)[0] == pytest.approx(735840 / 5208)

@@ -239,3 +239,28 @@ def test_warm_start_from_own_solution_and_neighbour():
     assert sum(r.iters for r in own) < 0.6 * sum(r.iters for r in cold), ([r.iters for r in own], [r.iters for r in cold])
     _check(lps, own, "config4-warm-own")
     _check(lps, nb, "config4-warm-neighbour")
+
+
+def test_multi_device_handle_splits_batch_and_matches_single_device():
+    """A handle over several devices (device_mask / dvh_create_devices; device 0 repeated on a one-GPU box) splits a
+    host batch into cost-balanced contiguous ranges solved concurrently: results bit-identical to one device, path
+    counts summed, an annual window costing as many monthly windows as its nonzeros."""
+    from dervet_hip.lp import scenarios as sc
+    ri = sc.reference_inputs()
+    load = ri["multi_der_site_load"][None, :]
+    gen = 1000.0 * np.nan_to_num(ri["multi_der_pv_profile"])[None, :]
+    annual = sc.windows_by_period(2017, 1.0, load, gen, sc.config2_battery(), tariff_def=sc.tariff(), n="year")
+    lps = _lps(sc.config4(range(6))) + _lps(annual) + _lps(sc.config2())
+    with BatchSolver(0) as one:
+        r1 = one.solve(lps)
+        k1 = one.kernel_stats()
+    with BatchSolver(devices=[0, 0, 0]) as three:
+        assert three.device_count == 3
+        r3 = three.solve(lps)
+        k3 = three.kernel_stats()
+    for a, b in zip(r1, r3):
+        assert a.status == b.status and a.iters == b.iters and a.obj == b.obj
+        assert np.array_equal(a.x, b.x) and np.array_equal(a.y, b.y)
+    for key in ("band_windows", "ell_windows", "generic_windows", "large_windows"):
+        assert k1[key] == k3[key], (key, k1, k3)
+    _check(lps[::7], r3[::7], "multi-device")
