@@ -60,7 +60,8 @@ def _col(a, G, T=None):
 
 
 def battery_group(T, dt, base_load, bat, retail_price=None, da_price=None, demand_masks=None, demand_prices=None,
-                  ene_min=None, ene_max=None, name="es", tags=None, pv_curtail_max=None, ice=None):
+                  ene_min=None, ene_max=None, name="es", tags=None, pv_curtail_max=None, ice=None, poi=None,
+                  grid_charge=True, pv_gen=None):
     """Build G windows sharing T steps and the demand masks.
 
     base_load [G, T]  : site load minus fixed generation (kW), hp is added here from ``bat``
@@ -75,7 +76,14 @@ def battery_group(T, dt, base_load, bat, retail_price=None, da_price=None, deman
                       variable_om_cost ($/kWh): storagevet RotatingGenerator rows
                       min_power n on_t <= elec_t <= rated n on_t with on_t in [0, 1] (the opt-in LP relaxation
                       of the binary commitment, RotatingGeneratorSizing.py:110-136; UNPINNED)
-    Variable order [ch, dis, ene, tau, pv?, elec?, on?]; >= rows: DCM epigraph, then per step the two ICE rows.
+    poi               : dict max_import (<= 0 kW), max_export (>= 0 kW), scalars or [G]: storagevet POI interconnection
+                      limits (Scenario apply_interconnection_constraints, Schema.json:2123,2194,2199), the net export
+                      -(net load) within [max_import, max_export] every step (UNPINNED)
+    grid_charge       : False = PV grid_charge 0 (Schema.json:1875): the battery charges from PV only, ch_t <= pv_gen_t
+                      (+ pv_t if curtailable); with fixed PV only it tightens ch's upper bound (UNPINNED)
+    pv_gen [G, T]     : the fixed PV generation inside base_load (for grid_charge = False)
+    Variable order [ch, dis, ene, tau, pv?, elec?, on?]; >= rows: DCM epigraph, per step the two ICE rows, the POI
+    import rows, the POI export rows, the charge-from-PV rows (grid_charge = False with curtailable PV).
     """
     base_load = np.atleast_2d(np.asarray(base_load, np.float64))
     G = base_load.shape[0]
@@ -104,9 +112,12 @@ def battery_group(T, dt, base_load, bat, retail_price=None, da_price=None, deman
     rows_i = [np.nonzero(mk)[0] for mk in masks]
     mI = int(sum(len(r) for r in rows_i))
     w_dcm = 3 + len(net_extra)
-    m = T + 1 + mI + (2 * T if ice is not None else 0)
+    n_poi = 2 * T if poi is not None else 0
+    n_gc = T if (not grid_charge and ipv >= 0) else 0
+    m = T + 1 + mI + (2 * T if ice is not None else 0) + n_poi + n_gc
     lens = np.concatenate([[1], np.full(T - 1, 4), [3], np.full(mI, w_dcm),
-                           np.full(2 * T if ice is not None else 0, 2)]).astype(np.int64)
+                           np.full(2 * T if ice is not None else 0, 2), np.full(n_poi, w_dcm - 1),
+                           np.full(n_gc, 2)]).astype(np.int64)
     indptr = np.zeros(m + 1, np.int64)
     np.cumsum(lens, out=indptr[1:])
     nnz = int(indptr[-1])
@@ -156,11 +167,32 @@ def battery_group(T, dt, base_load, bat, retail_price=None, da_price=None, deman
         data[:, r2] = 1.0
         data[:, r2 + 1] = -pmin[:, None]
         row += 2 * T
+    if poi is not None:  # import: -ch + dis + pv + elec >= base + max_import; export: the negation >= -max_export - base
+        for sign, rhs in ((-1.0, base + _col(poi["max_import"], G)[:, None]),
+                          (1.0, -_col(poi["max_export"], G)[:, None] - base)):
+            rr = indptr[row:row + T].reshape(-1, 1) + np.arange(w_dcm - 1)
+            indices[rr] = np.stack([ich + t, idis + t] + [c0_ + t for c0_ in net_extra], axis=1)
+            data[:, rr[:, 0]] = sign
+            data[:, rr[:, 1]] = -sign
+            for e in range(2, w_dcm - 1):
+                data[:, rr[:, e]] = -sign
+            q[:, row:row + T] = rhs
+            row += T
+    pvg = np.zeros((G, T)) if pv_gen is None else _col(pv_gen, G, T)
+    if n_gc:  # charge from PV only: pv_t - ch_t >= -pv_gen_t
+        rr = indptr[row:row + T].reshape(-1, 1) + np.arange(2)
+        indices[rr] = np.stack([ich + t, ipv + t], axis=1)
+        data[:, rr[:, 0]] = -1.0
+        data[:, rr[:, 1]] = 1.0
+        q[:, row:row + T] = -pvg
+        row += T
 
     # ---- bounds
     l = np.zeros((G, n))
     u = np.empty((G, n))
     u[:, ich:ich + T] = pch[:, None]
+    if not grid_charge and ipv < 0:  # charge from the fixed PV only
+        u[:, ich:ich + T] = np.minimum(pch[:, None], pvg)
     u[:, idis:idis + T] = pdis[:, None]
     lo = (_col(bat.get("llsoc", 0.0), G) * E)[:, None] * np.ones((1, T))
     hi = (_col(bat.get("ulsoc", 1.0), G) * E)[:, None] * np.ones((1, T))

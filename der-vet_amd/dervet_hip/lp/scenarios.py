@@ -33,10 +33,11 @@ def tariff(name="data_tariff"):
 
 def windows_by_period(year, dt, load, gen, bat, tariff_def=None, da_price=None, n="month", ene_min=None,
                       ene_max=None, demand_price_override=None, price_scale=None, tags_prefix=None,
-                      pv_curtail_max=None, ice=None):
+                      pv_curtail_max=None, ice=None, poi=None, grid_charge=True):
     """Split S scenarios' series [S, Tall] into windows; returns a list of WindowGroup (one per window id).
 
     demand_price_override [S] replaces every demand charge's $/kW (sweep); price_scale [S] scales energy prices.
+    poi / grid_charge: POI interconnection limits and PV grid_charge (builder.battery_group; parity unpinned).
     """
     load = np.atleast_2d(np.asarray(load, np.float64))
     S, Tall = load.shape
@@ -78,7 +79,7 @@ def windows_by_period(year, dt, load, gen, bat, tariff_def=None, da_price=None, 
             ene_max=None if ene_max is None else np.broadcast_to(ene_max, (S, Tall))[:, sel],
             tags=[(s if tags_prefix is None else tags_prefix[s], int(w)) for s in range(S)],
             pv_curtail_max=None if pv_curtail_max is None else np.broadcast_to(pv_curtail_max, (S, Tall))[:, sel],
-            ice=ice)
+            ice=ice, poi=poi, grid_charge=grid_charge, pv_gen=None if grid_charge else gen[:, sel])
         g.index = sel
         groups.append(g)
     return groups

@@ -56,7 +56,14 @@ def build(win):
          pv_curtail_max (array or None), ice (dict or None),
          fr (dict or None): eou, eod, regu_price, regd_price, fr_price [T]; optional regu_max, regu_min, regd_max,
              regd_min [T] (u/d_ts_constraints), combined (bool),
-         binary_relax (bool): the LP relaxation row ch / P_ch + dis / P_dis <= 1.
+         binary_relax (bool): the LP relaxation row ch / P_ch + dis / P_dis <= 1,
+         poi (dict or None, PARITY UNPINNED): max_import (<= 0 kW), max_export (>= 0 kW) -- storagevet POI import /
+             export limits with Scenario apply_interconnection_constraints (Schema.json:2123,2194,2199; applied in
+             POI.optimization_problem, extended at dervet/MicrogridPOI.py:215-258): the net export
+             -(net load) stays in [max_import, max_export] at every step,
+         grid_charge (bool, default True; PARITY UNPINNED): False = PV grid_charge 0 (Schema.json:1875): the battery
+             charges from the PV only, ch_t <= G_t + pv_t (a bound on ch with fixed PV, a >= row with curtailable
+             PV).
     Returns dict(K csr, q, c, c0, l, u, m_eq, funcs{name: (coef, const)}, layout)."""
     T = int(win["T"])
     dt = float(win["dt"])
@@ -197,6 +204,25 @@ def build(win):
         if fr.get("regd_max") is not None:
             ge_rows([("dc", -1.0), ("dd", -1.0)], -np.asarray(fr["regd_max"], float))
             ge_rows([("dc", 1.0), ("dd", 1.0)], np.asarray(fr["regd_min"], float))
+    poi = win.get("poi")
+    if poi is not None:
+        # net load_t = base_t + ch_t - dis_t - pv_t - elec_t in [-max_export, -max_import]
+        for t in range(T):  # import: -net >= max_import  ->  -ch + dis + pv + elec >= base + max_import
+            cc, vv = net_coefs(t)
+            rows += [r] * len(cc); cols += cc; vals += [-v for v in vv]
+            q.append(base[t] + float(poi["max_import"]))
+            r += 1
+        for t in range(T):  # export: net >= -max_export  ->  ch - dis - pv - elec >= -max_export - base
+            cc, vv = net_coefs(t)
+            rows += [r] * len(cc); cols += cc; vals += list(vv)
+            q.append(-float(poi["max_export"]) - base[t])
+            r += 1
+    gen_fixed = np.asarray(win.get("gen", np.zeros(T)), float)
+    if not win.get("grid_charge", True) and pvmax is not None:
+        for t in range(T):  # charge from PV only: pv_t - ch_t >= -G_t
+            rows += [r, r]; cols += [off["pv"] + t, off["ch"] + t]; vals += [1.0, -1.0]
+            q.append(-gen_fixed[t])
+            r += 1
     if win.get("binary_relax"):
         for t in range(T):  # -ch/P_ch - dis/P_dis >= -1
             rows += [r, r]; cols += [off["ch"] + t, off["dis"] + t]; vals += [-1.0 / pch, -1.0 / pdis]
@@ -227,6 +253,8 @@ def build(win):
     lo = np.zeros(n)
     hi = np.full(n, np.inf)
     hi[off["ch"]:off["ch"] + T] = pch
+    if not win.get("grid_charge", True) and pvmax is None:  # charge from the fixed PV only
+        hi[off["ch"]:off["ch"] + T] = np.minimum(pch, gen_fixed)
     hi[off["dis"]:off["dis"] + T] = pdis
     lo[off["ene"]:off["ene"] + T] = elo
     hi[off["ene"]:off["ene"] + T] = ehi
