@@ -9,8 +9,9 @@ config-4 slice for comparison).
   config 3  5-minute annual window (T = 105,120): the grid-wide large-LP path, with and without retail + DCM
   config 4  --c4-scenarios scenarios x 12 monthly windows, seeded and cold schedules
   config 5  battery + PV + LP-relaxed ICE + 4-h reliability min-SOE, --c5-scenarios scenarios x 12 monthly windows
-            per opt year; the 20-year horizon is 20 independent year batches of the same shape (the horizon's
-            windows do not couple), so one year batch resident in HBM is the timed unit
+            per opt year: the 'Reliability Min State of Energy' of every scenario computed on the GPU
+            (dvh_outage_min_soe = Reliability.min_soe_iterative), then the whole --c5-years horizon solved as year
+            batches (seeded schedule; the horizon's windows do not couple), every window counted
   market    (`--only 6`) Usecase 3 daily DA + FR windows of the three golden cases (3 x 365), and
             the same days with load following + spinning / non-spinning reserve added (synthetic LF / SR / NSR
             prices from the fixture's Reg Up / Down prices; parity unpinned beyond HiGHS on the same LP)
@@ -114,6 +115,7 @@ def main():
     ap.add_argument("--only", default="1,2,3,4,5")
     ap.add_argument("--c4-scenarios", type=int, default=2000)
     ap.add_argument("--c5-scenarios", type=int, default=1000)
+    ap.add_argument("--c5-years", type=int, default=20)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--sample", type=int, default=48)
     ap.add_argument("--procs", type=int, default=16)
@@ -188,14 +190,65 @@ def main():
         run("market-uc3+lf+sr+nsr", "the same 3 x 365 days with load following + SR + NSR (synthetic prices)",
             P(groups), s, args.reps, args.sample, args.procs)
     if 5 in only:
-        ids = range(args.c5_scenarios)
-        mk = lambda v: scenarios.config5(v, years=1)  # noqa: E731
-        run("config5", f"{args.c5_scenarios} scenarios x 12 monthly windows of one opt year (x 20 years = 20 such "
-                       f"batches)", P(mk(ids)), s, args.reps, args.sample, args.procs)
-        P5 = scenarios.sweep_parameters(ids)
-        sw = SeededSweep(mk, ids, P5["E"], stride=32, features=scenarios.sweep_features(P5))
-        run("config5", f"{args.c5_scenarios} scenarios x 12 monthly windows of one opt year, seeded schedule",
-            sw.packed, s, args.reps, args.sample, args.procs, sweep=sw)
+        config5_horizon(s, range(args.c5_scenarios), args.c5_years, args)
+
+
+def config5_horizon(s, ids, years, args):
+    """BASELINE config 5 end to end: GPU min-SOE requirement, then every window of the horizon (year batches,
+    seeded schedule, batch resident in HBM while timed); one JSON line with the totals."""
+    from dervet_hip import reliability
+    from dervet_hip.lp import scenarios
+    from dervet_hip.sweep import SeededSweep
+    ids = list(ids)
+    t = time.perf_counter()
+    ms = scenarios.config5_min_soe(ids, s)
+    minsoe_s = time.perf_counter() - t
+    minsoe_kernel_ms = reliability.last_kernel_ms(s)
+    P5 = scenarios.sweep_parameters(ids)
+    # windows whose requirement exceeds E somewhere (infeasible as stated -> clipped at E for the timed horizon)
+    over = ms > P5["E"][:, None]
+    month = np.concatenate([np.full(d, k) for k, d in enumerate([31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31])])
+    month = np.repeat(month, 24)[:ms.shape[1]]
+    clipped = int(sum(over[:, month == k].any(axis=1).sum() for k in range(12)))
+    feats = scenarios.sweep_features(P5)
+    solve_s = build_s = 0.0
+    iters, opt, windows, par = [], 0, 0, None
+    for y in range(years):
+        t = time.perf_counter()
+        mk = lambda v, y=y: scenarios.config5(v, years=1, start_year=2017 + y,  # noqa: E731
+                                              min_soe=ms[np.searchsorted(ids, np.asarray(list(v)))],
+                                              cap_min_soe=True)
+        sw = SeededSweep(mk, ids, P5["E"], stride=32, features=feats)
+        dev = sw.packed.to_torch("cuda:0").alloc_outputs()
+        build_s += time.perf_counter() - t
+        if y == 0:
+            sw.solve(s, dev)  # warm-up (workspace sizing)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        _, paths = sw.solve(s, dev)
+        torch.cuda.synchronize()
+        solve_s += time.perf_counter() - t
+        ist = dev.istats.cpu().numpy()
+        iters.append(ist[:, 1])
+        opt += int((ist[:, 0] == 0).sum())
+        windows += sw.packed.count
+        if y == 0 and args.sample > 0:
+            par = _parity(sw.packed, dev.stats.cpu().numpy(), dev.x.cpu().numpy(), args.sample, args.procs)
+        del dev
+    it = np.concatenate(iters)
+    line = {"config": "config5", "workload": f"{len(ids)} scenarios x {years} opt years x 12 monthly windows: battery + "
+                                             "PV + LP-relaxed ICE + DCM + retail + GPU reliability min-SOE requirement",
+            "windows": windows, "schedule": "seeded, one batch per opt year",
+            "min_soe": {"wall_ms": round(minsoe_s * 1e3, 1), "kernel_ms": round(minsoe_kernel_ms, 2),
+                        "outages_simulated": len(ids) * 8760, "max_kwh": float(ms.max()), "mean_kwh": float(ms.mean()),
+                        "hours_above_E": int(over.sum()), "windows_clipped_per_year": clipped,
+                        "note": "requirement clipped at E: unclipped, those windows have crossed ene bounds and "
+                                "the solver reports them PRIMAL_INFEASIBLE at setup (tests/test_gpu_outage.py)"},
+            "solve_ms_total": round(solve_s * 1e3, 1), "windows_per_s": round(windows / solve_s, 1),
+            "scenario_years_per_s": round(len(ids) * years / solve_s, 1), "host_build_s": round(build_s, 1),
+            "iters_mean": round(float(it.mean()), 1), "iters_max": int(it.max()), "optimal": opt,
+            "kernel_path_last_year": paths, "parity_year0": par}
+    print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":

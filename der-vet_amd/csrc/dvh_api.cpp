@@ -728,8 +728,9 @@ static std::string validate(const dvh_lp& lp, int k) {
     }
   }
   for (int j = 0; j < lp.n; ++j) {
-    if (!std::isfinite(lp.c[j]) || std::isnan(lp.l[j]) || std::isnan(lp.u[j]) || lp.l[j] > lp.u[j] ||
-        lp.l[j] == INFINITY || lp.u[j] == -INFINITY) {
+    // crossed finite bounds (l > u) are a valid, infeasible window: status PRIMAL_INFEASIBLE (setup kernel)
+    if (!std::isfinite(lp.c[j]) || std::isnan(lp.l[j]) || std::isnan(lp.u[j]) || lp.l[j] == INFINITY ||
+        lp.u[j] == -INFINITY) {
       snprintf(buf, sizeof buf, "window %d: invalid objective or bounds at variable %d", k, j);
       return buf;
     }

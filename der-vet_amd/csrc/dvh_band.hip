@@ -83,6 +83,7 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
       b.istats[2 * k + 1] = 0;
     }
   };
+  if (scal[6] == 3.0) return;  // reported infeasible by the setup kernel
   if (scal[6] != 0.0 || T < 1 || T > B || J < 0 || J > kJMax || MD < 0 || MD > T || (J == 0 && MD > 0)) {
     bail();
     return;

@@ -88,6 +88,23 @@ __global__ __launch_bounds__(kSetupB) void setup_kernel(const Batch b, const Wor
     }
     return;
   }
+  // 0. crossed bounds (l_j > u_j, e.g. a reliability min-SOE requirement above the battery's energy rating): the
+  //    window is primal infeasible as given; reported at once (status PRIMAL_INFEASIBLE, 0 iterations), and flagged
+  //    solved (scal[6] = 3) so no PDHG kernel takes it
+  {
+    int crossed = 0;
+    for (int j = tid; j < n; j += kSetupB) crossed |= b.l[W.on + j] > b.u[W.on + j];
+    if (__syncthreads_or(crossed)) {
+      if (tid == 0) {
+        w.scal[(int64_t)kl * kScal] = 0.0;
+        w.scal[(int64_t)kl * kScal + 6] = 3.0;
+        b.istats[2 * k] = 1;  // DVH_PRIMAL_INFEASIBLE
+        b.istats[2 * k + 1] = 0;
+        for (int u = 0; u < 4; ++u) b.stats[4 * k + u] = u == 0 ? NAN : 0.0;
+      }
+      return;
+    }
+  }
 
   const int32_t* Kp = b.indptr + W.row;
   const int32_t* Kc = b.indices + W.nz;
@@ -412,6 +429,7 @@ __global__ __launch_bounds__(B) void pdhg_kernel(const Batch b, const Work w, co
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const double* scal = w.scal + (int64_t)kl * kScal;
   const int nlk = (int)scal[4], nlt = (int)scal[5];
+  if (scal[6] == 3.0) return;  // reported infeasible by the setup kernel
   if (scal[6] != 0.0 || n > XS * B || m > YS * B || (MLDS && (n > 65535 || m > 65535))) {
     if (tid == 0) {
       b.istats[2 * k] = kNumerical;
@@ -840,6 +858,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(WPE))) void p
       b.istats[2 * k + 1] = 0;
     }
   };
+  if (scal[6] == 3.0) return;  // reported infeasible by the setup kernel
   if (scal[6] != 0.0 || n > RX || m > RY || n < 1) {
     bail();
     return;

@@ -179,11 +179,49 @@ def reliability_min_soe(critical_load, hours=4.0, dt=1.0, cap=None):
     return out
 
 
-def config5(scenarios, years=20, start_year=2017):
+def config5_outage_cases(scenarios, count_ice=False):
+    """Per scenario, the DER mix the Reliability value stream simulates outages with (Reliability.min_soe_iterative,
+    dervet/MicrogridValueStreams/Reliability.py:685-733, via get_der_mix_properties :276-332): the scenario's
+    critical load (data/multi_der_hourly_timeseries.csv "Critical Load (kW)" x its load scale), its battery
+    (E, P, rte; soc_init 100 %, template "post_facto_initial_soc"), its PV (rated x profile, template nu 20 % /
+    gamma 43 %, Model_Parameters_Template_DER.csv:118-119) and, with count_ice, the ICE units (7 x 750 kW; they
+    alone carry the critical load, which makes the requirement zero -- the bench's config 5 leaves them out of the
+    outage mix so the 4-h requirement binds)."""
+    from ..reliability import OutageCase
+    ri = reference_inputs()
+    scen = list(scenarios)
+    P = sweep_parameters(scen)
+    pv = np.nan_to_num(ri["multi_der_pv_profile"])
+    cases = []
+    for i in range(len(scen)):
+        E = float(P["E"][i])
+        Pw = E / float(P["duration"][i])
+        cases.append(OutageCase(critical_load=ri["multi_der_critical_load"] * float(P["load_scale"][i]), dt=1.0,
+                                max_outage_duration=80,
+                                ess=dict(E=E, P_ch=Pw, P_dis=Pw, rte=float(P["rte"][i]), llsoc=0.0, ulsoc=1.0),
+                                soc_init=1.0, pv_max=[float(P["pv_rated"][i]) * pv], pv_nu=[0.20], pv_gamma=[0.43],
+                                dg_power=[750.0] * 7 if count_ice else []))
+    return cases
+
+
+def config5_min_soe(scenarios, solver, target_hours=4, count_ice=False):
+    """[S, 8760] 'Reliability Min State of Energy' per scenario, computed on the GPU (dvh_outage_min_soe, the
+    Reliability.min_soe_iterative restatement) -- the ene lower bound every config-5 window applies (row a10)."""
+    from ..reliability import min_soe
+    return np.stack(min_soe(config5_outage_cases(scenarios, count_ice), target_hours, solver))
+
+
+def config5(scenarios, years=20, start_year=2017, min_soe=None, cap_min_soe=False):
     """Battery + fixed PV + LP-relaxed ICE + 4-h reliability min-SOE, retail + DCM, monthly windows over
     `years` opt years (the 2017 profile re-used each year).  Perturbations as config 4 (same seeds) plus
     ICE fuel cost; ICE parameters from the Usecase3 ES+PV+DG model parameters (750 kW x 7 units,
-    0.0866 gal/kWh) with a 250 kW minimum stable output per unit so the relaxation binds."""
+    0.0866 gal/kWh) with a 250 kW minimum stable output per unit so the relaxation binds.
+    min_soe [S, 8760]: the reliability requirement (``config5_min_soe``, computed on the GPU); None: the synthetic
+    4-h critical-load coverage vector ``reliability_min_soe`` (CPU tests).  Hours whose requirement exceeds the
+    battery's energy rating (the restated simulate_outage lets SOE climb past E while it "discharges" a negative
+    net load, Reliability.py:543-556) give crossed ene bounds: those windows are infeasible as the reference
+    states them and the solver reports PRIMAL_INFEASIBLE without iterating; cap_min_soe=True clips the requirement
+    at ulsoc * E instead (the bench's timed horizon, which reports how many windows the clip touched)."""
     from scipy.signal import lfilter
     ri = reference_inputs()
     scen = list(scenarios)
@@ -199,8 +237,13 @@ def config5(scenarios, years=20, start_year=2017):
     fuel = 2.5 + P["price_scale"]  # U[3.2, 3.8] $/gal, deterministic from the same draws
     ice = dict(rated_power=750.0, n=7.0, min_power=250.0, efficiency=0.086618705, fuel_cost=fuel,
                variable_om_cost=0.0)
-    crit = ri["multi_der_critical_load"][None, :] * P["load_scale"][:, None]
-    emin = reliability_min_soe(crit, 4.0, 1.0, cap=E)
+    if min_soe is None:
+        crit = ri["multi_der_critical_load"][None, :] * P["load_scale"][:, None]
+        emin = reliability_min_soe(crit, 4.0, 1.0, cap=E)
+    else:
+        emin = np.asarray(min_soe, np.float64).reshape(len(scen), -1)
+        if cap_min_soe:
+            emin = np.minimum(emin, (bat["ulsoc"] * E)[:, None])
     groups = []
     for y in range(years):
         groups += windows_by_period(start_year + y, 1.0, load, gen, bat, tariff_def=tariff(),

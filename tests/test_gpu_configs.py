@@ -179,6 +179,27 @@ def test_infeasible_window_is_not_reported_optimal():
     assert r.status != 0 and r.primal_res_rel > 1e-6
 
 
+@pytest.mark.parametrize("path", ["default", "ell", "generic"])
+def test_crossed_bounds_window_reported_infeasible_on_every_kernel_path(path):
+    """A window with l_j > u_j (a reliability requirement above E) is PRIMAL_INFEASIBLE at 0 iterations from the
+    setup kernel; no PDHG kernel overwrites it and its neighbours solve as alone (oracle/cpu_pdhg.cpp applies the
+    same rule)."""
+    import dataclasses
+    lps = _lps(scenarios.config4([3]))[:4]
+    T = lps[2].m_eq - 1
+    bad_l = lps[2].l.copy()
+    bad_l[2 * T + 7] = lps[2].u[2 * T + 7] + 10.0
+    bad = list(lps)
+    bad[2] = dataclasses.replace(lps[2], l=bad_l)
+    with BatchSolver(0) as s:
+        s.set_kernel_path(path)
+        ref = s.solve(lps)
+        res = s.solve(bad)
+    assert res[2].status_name == "infeasible" and res[2].iters == 0
+    for k in (0, 1, 3):
+        assert res[k].status == 0 and res[k].obj == ref[k].obj and res[k].iters == ref[k].iters
+
+
 def test_invalid_inputs_raise_with_message(gpu_solver):
     bad = WindowLP(np.array([0, 1], np.int32), np.array([5], np.int32), np.array([1.0]), np.array([1.0, 1.0]),
                    np.array([1.0]), np.zeros(2), np.ones(2), 1, 0.0)

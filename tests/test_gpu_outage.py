@@ -92,3 +92,53 @@ def test_min_soe_bit_exact(gpu_solver):
         np.testing.assert_array_equal(g, ref, err_msg=f"case {k}")
         assert (g >= 0).all()
     assert got[0].max() > 0
+
+
+def test_config5_min_soe_from_the_gpu_outage_kernel_feeds_the_windows(gpu_solver):
+    """BASELINE config 5 end to end (row a10): the 'Reliability Min State of Energy' requirement of each scenario
+    is computed by dvh_outage_min_soe (bit-exact with the oracle restatement of Reliability.min_soe_iterative) and
+    applied as every window's ene lower bound; the windows solve to the HiGHS optimum on the battery-banded ICE
+    kernel.  With the ICE units in the outage mix they carry the critical load alone and the requirement is 0."""
+    import scipy.sparse as sp
+    from dervet_hip.lp import builder, scenarios
+    from oracle import outage, window_lp
+    ids = [0, 1, 2]
+    ms = scenarios.config5_min_soe(ids, gpu_solver)
+    assert ms.shape == (3, 8760) and ms.max() > 0
+    for c, g in zip(scenarios.config5_outage_cases(ids), ms):
+        dg, pmax, props, pvar, gamma = reliability.der_mix_properties(c)
+        ref = outage.min_soe(np.asarray(c.critical_load, np.float64), np.repeat(dg, len(pmax)), pmax, pvar, gamma,
+                             props, c.soc_init, 4, c.max_outage_duration, c.dt, c.load_shed_pct)
+        np.testing.assert_array_equal(g, ref)
+    assert scenarios.config5_min_soe(ids, gpu_solver, count_ice=True).max() == 0.0
+    E = scenarios.sweep_parameters(ids)["E"]
+    for cap in (False, True):
+        groups = scenarios.config5(ids, years=1, min_soe=ms, cap_min_soe=cap)
+        lps = [lp for g in groups for lp in builder.group_window_lps(g)]
+        res = gpu_solver.solve(lps)
+        assert gpu_solver.kernel_stats()["band_windows"] == len(lps)
+        k = 0
+        seen = set()
+        for g in groups:
+            T = g.T
+            for i in range(g.G):
+                r = res[k]
+                k += 1
+                req = ms[i][g.index]
+                # the requirement is the ene lower bound (clipped at E with cap)
+                assert np.array_equal(g.l[i][2 * T:3 * T], np.minimum(req, E[i]) if cap else req)
+                crossed = not cap and bool((req > E[i]).any())
+                if crossed:  # infeasible as stated: reported at once, no iterations
+                    assert r.status_name == "infeasible" and r.iters == 0, (k, r.status_name)
+                else:
+                    assert r.status == 0, (k, r.status_name)
+                if (crossed, i) in seen:
+                    continue
+                seen.add((crossed, i))
+                o = dict(K=sp.csr_matrix((g.data[i], g.indices, g.indptr), shape=(g.m, g.n)), q=g.q[i], c=g.c[i],
+                         c0=float(g.c0[i]), l=g.l[i], u=g.u[i], m_eq=g.m_eq)
+                if crossed:
+                    continue  # HiGHS rejects crossed bounds outright; nothing further to compare
+                h = window_lp.solve_highs(o)
+                assert h["status"] == 0 and abs(r.obj - h["obj"]) <= 1e-5 * abs(h["obj"]), (k, r.obj, h["obj"])
+                assert window_lp.primal_residual_rel(o, r.x)[0] <= 1e-6
