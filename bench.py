@@ -15,8 +15,11 @@ solved from zero first, then every other window warm from its nearest seed's sol
 two solver calls per step, every window solved once per step to the same KKT tolerance; nothing carries over
 between steps (the seed phase starts from zero and the warm phase overwrites every warm start).  After the
 timed steps the same batch is solved once more with every window cold, reported as schedule.cold_*.
-The CPU baseline (rank 0, N=1 only) solves a bounded sample of the same windows with HiGHS on a process
-pool (oracle/cpu_baseline.py) and is also the parity check of the GPU objectives on that sample.
+The CPU baseline (rank 0, N=1 only) times two CPU solvers on bounded samples of the same windows, on the box's
+16-core CPU share: the same restarted-Halpern PDHG in C++/OpenMP behind the same C ABI (oracle/cpu_pdhg.cpp, every
+window cold -- compare with schedule.cold_windows_per_s), which is the faster of the two and gives `value`, and
+the restated LP + HiGHS on a process pool (oracle/cpu_baseline.py), which is also the parity check of the GPU
+objectives on its sample.
 """
 import argparse
 import json
@@ -139,6 +142,7 @@ def main():
     ap.add_argument("--scenarios", type=int, default=10000, help="scenarios per GPU (x 12 monthly windows)")
     ap.add_argument("--cpu-sample", type=int, default=960, help="windows in the HiGHS CPU-baseline sample")
     ap.add_argument("--cpu-procs", type=int, default=0)
+    ap.add_argument("--cpu-pdhg-sample", type=int, default=960, help="windows in the C++ CPU PDHG baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--check-every", type=int, default=0, help="restart-check period (0: library default)")
     ap.add_argument("--kkt-every", type=int, default=0, help="KKT check every n restart checks (0: default)")
@@ -283,11 +287,36 @@ def main():
         idx = np.linspace(0, count - 1, min(args.cpu_sample, count)).astype(np.int64)
         lps = [window_lp.from_packed_window(pb.window(int(k))) for k in idx]
         objs, sts, wall, procs = cpu_baseline.highs_batch(lps, args.cpu_procs or None)
-        cpu = {"value": round(len(idx) / wall, 2), "unit": "windows/s", "cores": procs, "kind": "port",
-               "cpu_model": cpu_baseline.cpu_model(),
-               "sample": f"{len(idx)} of the {count} config-4 windows (evenly spaced), restated LP + HiGHS "
-                         f"(scipy {__import__('scipy').__version__}), one LP per process, {procs} processes "
-                         f"(the GPU box's CPU share; os.cpu_count() there reports the whole host), {wall:.1f} s wall"}
+        highs = {"value": round(len(idx) / wall, 2), "unit": "windows/s", "cores": procs,
+                 "sample": f"{len(idx)} of the {count} config-4 windows (evenly spaced), restated LP + HiGHS "
+                           f"(scipy {__import__('scipy').__version__}), one LP per process, {procs} processes "
+                           f"(the GPU box's CPU share; os.cpu_count() there reports the whole host), {wall:.1f} s wall"}
+        cpu = dict(highs, kind="port", cpu_model=cpu_baseline.cpu_model(), solver="HiGHS")
+        if args.cpu_pdhg_sample > 0:
+            from oracle.cpu_pdhg import CpuPdhgSolver
+            threads = args.cpu_procs or 16
+            jdx = np.linspace(0, count - 1, min(args.cpu_pdhg_sample, count)).astype(np.int64)
+            plps = [pb.window_lp(int(k)) for k in jdx]
+            cs = CpuPdhgSolver(threads=threads)
+            tc = time.perf_counter()
+            pres = cs.solve(plps)
+            cwall = time.perf_counter() - tc
+            cs.close()
+            pobj = np.array([r.obj for r in pres])
+            cpu_pdhg = {"value": round(len(jdx) / cwall, 2), "unit": "windows/s", "cores": threads,
+                        "iters_mean": round(float(np.mean([r.iters for r in pres])), 1),
+                        "optimal_frac": float(np.mean([r.status == 0 for r in pres])),
+                        "sample": f"{len(jdx)} of the {count} config-4 windows (evenly spaced), every window cold, "
+                                  f"oracle/cpu_pdhg.cpp (same algorithm and options as the GPU, C++ -O3, OpenMP "
+                                  f"{threads} threads, one window per thread), {cwall:.1f} s wall",
+                        "compare_to": "schedule.cold_windows_per_s (the GPU, every window cold)"}
+            highs_rate = highs["value"]
+            cpu = {"value": cpu_pdhg["value"], "unit": "windows/s", "cores": threads, "kind": "port",
+                   "cpu_model": cpu_baseline.cpu_model(), "solver": "C++ PDHG restatement (the faster CPU path)",
+                   "sample": cpu_pdhg["sample"], "pdhg": cpu_pdhg, "highs": highs}
+            if highs_rate > cpu_pdhg["value"]:
+                cpu.update(value=highs_rate, cores=highs["cores"], solver="HiGHS (the faster CPU path)",
+                           sample=highs["sample"])
         g = st[idx, 0]
         ok = sts == 0
         rel = np.abs(g[ok] - objs[ok]) / np.maximum(np.abs(objs[ok]), 1e-12)

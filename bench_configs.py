@@ -12,6 +12,9 @@ config-4 slice for comparison).
             per opt year: the 'Reliability Min State of Energy' of every scenario computed on the GPU
             (dvh_outage_min_soe = Reliability.min_soe_iterative), then the whole --c5-years horizon solved as year
             batches (seeded schedule; the horizon's windows do not couple), every window counted
+  medium    (`--only 7`) windows above the on-chip limit of 4,096 columns / rows as a batch: --med-scenarios
+            config-4 scenarios with n = "year" (annual hourly windows, T = 8,760, n = 26,292) and with dt = 0.25
+            (15-minute monthly windows, T = 2,688..2,976, n <= 8,929)
   market    (`--only 6`) Usecase 3 daily DA + FR windows of the three golden cases (3 x 365), and
             the same days with load following + spinning / non-spinning reserve added (synthetic LF / SR / NSR
             prices from the fixture's Reg Up / Down prices; parity unpinned beyond HiGHS on the same LP)
@@ -116,6 +119,7 @@ def main():
     ap.add_argument("--c4-scenarios", type=int, default=2000)
     ap.add_argument("--c5-scenarios", type=int, default=1000)
     ap.add_argument("--c5-years", type=int, default=20)
+    ap.add_argument("--med-scenarios", type=int, default=1000)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--sample", type=int, default=48)
     ap.add_argument("--procs", type=int, default=16)
@@ -191,6 +195,13 @@ def main():
             P(groups), s, args.reps, args.sample, args.procs)
     if 5 in only:
         config5_horizon(s, range(args.c5_scenarios), args.c5_years, args)
+    if 7 in only:
+        ids = range(args.med_scenarios)
+        run("medium-annual", f"{args.med_scenarios} config-4 scenarios x 1 annual hourly window (n = 'year', T = 8,760)",
+            P(scenarios.config4(ids, n="year")), s, args.reps, min(args.sample, 8), args.procs)
+        ids = range(max(1, args.med_scenarios // 12))
+        run("medium-15min", f"{len(ids)} config-4 scenarios x 12 monthly windows at dt = 0.25 h",
+            P(scenarios.config4(ids, dt=0.25)), s, args.reps, min(args.sample, 8), args.procs)
 
 
 def config5_horizon(s, ids, years, args):

@@ -59,13 +59,15 @@ struct dvh_handle {
   DevBuf w_tptr, w_tind, w_tval, w_kval, w_rowof, w_perm, w_dr, w_dc, w_cs, w_ls, w_us, w_qs, w_vbuf, w_wbuf,
       w_tmpc, w_tmpr, w_longk, w_longt, w_scal;
   DevBuf d_list, d_hinv;
+  DevBuf m_list, m_plan, m_pos, m_xbuf, m_abort;  // medium tier (dvh_chain.hip)
+  int chain_cap = -1;                             // resident 768-thread workgroups (cooperative limit)
   DevBuf o_data, o_cases, o_len, o_hist, o_soe;  // reliability sweep
   double outage_ms = 0.0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<std::array<hipEvent_t, 3>> chunk_events;
   double timing[3] = {0, 0, 0};
   int last_variant = -1;
-  int n_ell = 0, n_generic = 0, n_large = 0, n_band = 0;
+  int n_ell = 0, n_generic = 0, n_large = 0, n_band = 0, n_chain = 0;
   int kernel_path = 0;  // 0 band -> ELL -> generic, 1 generic only, 2 ELL -> generic (no band kernel)
   dvh::LargeSolver* large = nullptr;  // grid-wide path for windows above dvh::kSmallMax (created on first use)
   float large_ms[2] = {0, 0};         // setup, PDHG time of the large windows of the last solve
@@ -212,7 +214,7 @@ int dvh_destroy(dvh_handle* h) {
                     &h->d_u, &h->d_list, &h->d_hinv, &h->d_x, &h->d_y, &h->d_stats, &h->d_istats, &h->w_tptr, &h->w_tind, &h->w_tval,
                     &h->w_kval, &h->w_rowof, &h->w_perm, &h->w_dr, &h->w_dc, &h->w_cs, &h->w_ls, &h->w_us,
                     &h->w_qs, &h->w_vbuf, &h->w_wbuf, &h->w_tmpc, &h->w_tmpr, &h->w_longk, &h->w_longt, &h->w_scal,
-                    &h->o_data, &h->o_cases, &h->o_len, &h->o_hist, &h->o_soe};
+                    &h->m_list, &h->m_plan, &h->m_pos, &h->m_xbuf, &h->m_abort, &h->o_data, &h->o_cases, &h->o_len, &h->o_hist, &h->o_soe};
   for (DevBuf* b : bufs) b->release();
   for (auto& e : h->ev)
     if (e) hipEventDestroy(e);
@@ -244,6 +246,16 @@ int dvh_last_path_counts(const dvh_handle* h, int32_t* out3) {
   out3[0] = h->n_ell;
   out3[1] = h->n_generic;
   out3[2] = h->n_large;
+  return DVH_OK;
+}
+
+int dvh_last_path_counts5(const dvh_handle* h, int32_t* out5) {
+  if (!h || !out5) return DVH_ERR_ARG;
+  out5[0] = h->n_ell;
+  out5[1] = h->n_generic;
+  out5[2] = h->n_large;
+  out5[3] = h->n_band;
+  out5[4] = h->n_chain;
   return DVH_OK;
 }
 
@@ -430,6 +442,72 @@ int dvh_last_timing(const dvh_handle* h, double* ms3) {
 
 }  // extern "C"
 
+// Medium tier over the candidates of one chunk (setup already run): plan, then the team kernel over the windows the
+// plan accepts; med_done[k] = 1 for the windows it solved or that the setup reported infeasible.  The others stay
+// with the grid-wide path.
+static int chain_pass(dvh_handle* h, const dvh::Batch& b, const dvh::Work& w, const dvh::Chunk& ch,
+                      const dvh::Opts& o, const std::vector<int32_t>& med, int max_T, std::vector<char>& med_done,
+                      hipStream_t s) {
+  const int nm = (int)med.size();
+  if (nm == 0) return DVH_OK;
+  const size_t I = sizeof(int32_t);
+  DVH_HIP(h, h->m_plan.ensure(I * (size_t)nm * dvh::kPlanInts));
+  hipError_t e = dvh::launch_chain_plan(b, w, ch, h->m_list.as<int32_t>(), nm, max_T, h->m_plan.as<int32_t>(), s);
+  if (e != hipSuccess) return hip_fail(h, e, "launch_chain_plan");
+  std::vector<int32_t> plan((size_t)nm * dvh::kPlanInts);
+  DVH_HIP(h, hipMemcpyAsync(plan.data(), h->m_plan.p, I * plan.size(), hipMemcpyDeviceToHost, s));
+  DVH_HIP(h, hipStreamSynchronize(s));
+  std::vector<int32_t> pos;
+  int PT = 0;
+  for (int i = 0; i < nm; ++i) {
+    const int P = plan[(size_t)i * dvh::kPlanInts];
+    if (P < 0) med_done[med[i]] = 1;  // crossed bounds: PRIMAL_INFEASIBLE from the setup kernel
+    if (P > 0) {
+      pos.push_back(i);
+      PT = std::max(PT, P);
+    }
+  }
+  if (pos.empty()) return DVH_OK;
+  if (h->chain_cap < 0) {
+    int cap = 0;
+    if (dvh::chain_capacity(h->device, &cap) != hipSuccess) cap = 0;
+    (void)hipGetLastError();
+    h->chain_cap = cap;
+  }
+  const int NT = std::min((int)pos.size(), h->chain_cap / std::max(PT, 1));
+  if (NT < 1) return DVH_OK;  // cannot keep a team resident: the grid-wide path takes them
+  DVH_HIP(h, h->m_pos.ensure(I * pos.size()));
+  DVH_HIP(h, hipMemcpyAsync(h->m_pos.p, pos.data(), I * pos.size(), hipMemcpyHostToDevice, s));
+  DVH_HIP(h, h->m_xbuf.ensure(dvh::chain_xbuf_bytes(NT, PT)));
+  DVH_HIP(h, h->m_abort.ensure(dvh::chain_abort_bytes(NT, PT)));
+  e = dvh::launch_chain(b, w, ch, o, h->m_pos.as<int32_t>(), (int)pos.size(), h->m_plan.as<int32_t>(), PT, NT,
+                        h->m_xbuf.p, h->m_abort.as<int32_t>(), s);
+  if (e == hipErrorCooperativeLaunchTooLarge) {  // not resident after all: leave them to the grid-wide path
+    (void)hipGetLastError();
+    h->chain_cap = 0;
+    return DVH_OK;
+  }
+  if (e != hipSuccess) return hip_fail(h, e, "launch_chain");
+  std::vector<int32_t> ab(dvh::chain_abort_bytes(NT, PT) / I);
+  DVH_HIP(h, hipMemcpyAsync(ab.data(), h->m_abort.p, I * ab.size(), hipMemcpyDeviceToHost, s));
+  DVH_HIP(h, hipStreamSynchronize(s));
+  if (ab[0] != 0) {
+    std::string msg = "medium tier: a segment exchange timed out (PT " + std::to_string(PT) + ", NT " +
+                      std::to_string(NT) + "); workgroups {team.segment: state list round entry tag seen}:";
+    for (int g = 0; g < NT * PT; ++g) {
+      const int32_t* d = &ab[16 + 8 * (size_t)g];
+      if (d[0] == 0) continue;
+      char buf[128];
+      snprintf(buf, sizeof buf, " %d.%d: %d %d %d 0x%x 0x%x 0x%x;", g / PT, g % PT, d[0], d[1], d[2], d[3], d[4], d[5]);
+      msg += buf;
+    }
+    return fail(h, DVH_ERR_HIP, msg);
+  }
+  for (int i : pos) med_done[med[i]] = 1;
+  h->n_chain += (int)pos.size();
+  return DVH_OK;
+}
+
 // Solve a packed device batch given a host copy of its descriptors.
 static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<int64_t>& desc, hipStream_t s) {
   const int count = bt->count;
@@ -458,12 +536,24 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
     int mn, mm;      // maxima over the chunk's small windows (the on-chip kernels' LDS sizing)
     int64_t mnz;
     int nsmall;
+    std::vector<int32_t> med;  // medium-tier candidates of the chunk
+    int med_n = 0, med_T = 0;
   };
   auto is_large = [&](int k) {
     const int64_t* d = &desc[8 * (size_t)k];
     return d[0] > dvh::kSmallMax || d[1] > dvh::kSmallMax;
   };
+  // medium tier candidates: battery-shaped sizes (n = 3T + J, m <= 2T + 1) up to kPMax segments of kChainB steps;
+  // the plan kernel verifies the pattern, anything else goes to the grid-wide path
+  const bool chain_on = h->kernel_path == 0 && o.rho == 1.0 && o.max_iters + o.power_iters < (1 << 17);
+  auto is_medium = [&](int k) {
+    const int64_t* d = &desc[8 * (size_t)k];
+    const int64_t T = d[2] - 1;
+    return chain_on && is_large(k) && T > dvh::kChainB && T <= (int64_t)dvh::kPMax * dvh::kChainB &&
+           d[0] >= 3 * T && d[0] <= 3 * T + dvh::kChainJMax && d[1] <= 2 * T + 1 && d[0] < 40000;
+  };
   std::vector<int> large;
+  std::vector<char> med_done(count, 0);  // solved (or reported infeasible) by the medium tier
   std::vector<C> chunks;
   int64_t wn = 0, wm = 0, wnz = 0;
   int wc = 0;
@@ -482,6 +572,11 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
       c.snz = std::max(c.snz, d[5] + d[3] - c.ch.base_nz);
       if (is_large(k)) {
         large.push_back(k);
+        if (is_medium(k)) {
+          c.med.push_back(k);
+          c.med_n = std::max<int>(c.med_n, (int)d[0]);
+          c.med_T = std::max<int>(c.med_T, (int)d[2] - 1);
+        }
         continue;
       }
       ++c.nsmall;
@@ -521,22 +616,33 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
               h->w_vbuf.as<double>(), h->w_wbuf.as<double>(), h->w_tmpc.as<double>(), h->w_tmpr.as<double>(),
               h->w_longk.as<int32_t>(), h->w_longt.as<int32_t>(), h->d_hinv.as<double>(), h->w_scal.as<double>()};
   DVH_HIP(h, h->d_list.ensure(I * (size_t)wc));
-  h->n_ell = h->n_generic = h->n_large = h->n_band = 0;
+  h->n_ell = h->n_generic = h->n_large = h->n_band = h->n_chain = 0;
   h->large_ms[0] = h->large_ms[1] = 0.0f;
   h->chunk_events.clear();
   DVH_HIP(h, hipEventRecord(h->ev[0], s));
   std::vector<double> scal;
   std::vector<int32_t> ist;
   for (const C& c : chunks) {
-    if (c.nsmall == 0) continue;
+    if (c.nsmall == 0 && c.med.empty()) continue;
     hipEvent_t e0, e1, e2;
     DVH_HIP(h, hipEventCreate(&e0));
     DVH_HIP(h, hipEventCreate(&e1));
     DVH_HIP(h, hipEventCreate(&e2));
     h->chunk_events.push_back({e0, e1, e2});
     DVH_HIP(h, hipEventRecord(e0, s));
-    DVH_HIP(h, dvh::launch_setup(b, w, c.ch, o, c.mn, c.mm, s));
+    if (c.nsmall > 0) DVH_HIP(h, dvh::launch_setup(b, w, c.ch, o, c.mn, c.mm, s));
+    if (!c.med.empty()) {
+      DVH_HIP(h, h->m_list.ensure(I * c.med.size()));
+      DVH_HIP(h, hipMemcpyAsync(h->m_list.p, c.med.data(), I * c.med.size(), hipMemcpyHostToDevice, s));
+      hipError_t e = dvh::launch_setup_medium(b, w, c.ch, o, c.med_n, h->m_list.as<int32_t>(), (int)c.med.size(), s);
+      if (e != hipSuccess) return hip_fail(h, e, "launch_setup_medium");
+    }
     DVH_HIP(h, hipEventRecord(e1, s));
+    if (c.nsmall == 0) {
+      if (int rc = chain_pass(h, b, w, c.ch, o, c.med, c.med_T, med_done, s)) return rc;
+      DVH_HIP(h, hipEventRecord(e2, s));
+      continue;
+    }
     // ELL widths from the setup statistics (one small D2H per chunk)
     scal.resize((size_t)c.ch.count * dvh::kScal);
     DVH_HIP(h, hipMemcpyAsync(scal.data(), w.scal, sizeof(double) * scal.size(), hipMemcpyDeviceToHost, s));
@@ -651,11 +757,13 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
       if (variant < 0) variant = gv;
       DVH_HIP(h, hipStreamSynchronize(s));  // d_list is reused by the next chunk
     }
+    if (int rc = chain_pass(h, b, w, c.ch, o, c.med, c.med_T, med_done, s)) return rc;
     DVH_HIP(h, hipEventRecord(e2, s));
     h->last_variant = variant;
   }
-  // windows above the on-chip limits: one at a time, the whole GPU each
+  // windows above the on-chip limits that the medium tier did not take: one at a time, the whole GPU each
   for (int k : large) {
+    if (med_done[k]) continue;
     if (!h->large) h->large = dvh::large_create();
     std::string msg;
     hipError_t e = dvh::large_solve(h->large, b, k, &desc[8 * (size_t)k], o, h->d_hinv.as<double>(), s, &msg,
@@ -781,7 +889,7 @@ extern "C" int dvh_solve_batch(dvh_handle* h, const dvh_lp* lps, int32_t count, 
     if (b[i + 1] > b[i]) th.emplace_back([&, i] { rc[i] = solve_batch_one(hs[i], lps + b[i], b[i + 1] - b[i], out + b[i]); });
   if (b[1] > b[0]) rc[0] = solve_batch_one(h, lps, b[1], out);
   for (auto& t : th) t.join();
-  int nell = 0, ngen = 0, nlarge = 0, nband = 0;
+  int nell = 0, ngen = 0, nlarge = 0, nband = 0, nchain = 0;
   double setup = 0.0, pdhg = 0.0;
   for (int i = 0; i < P; ++i) {
     if (rc[i] != DVH_OK) {
@@ -793,6 +901,7 @@ extern "C" int dvh_solve_batch(dvh_handle* h, const dvh_lp* lps, int32_t count, 
     ngen += hs[i]->n_generic;
     nlarge += hs[i]->n_large;
     nband += hs[i]->n_band;
+    nchain += hs[i]->n_chain;
     setup = std::max(setup, hs[i]->timing[1]);
     pdhg = std::max(pdhg, hs[i]->timing[2]);
   }
@@ -800,6 +909,7 @@ extern "C" int dvh_solve_batch(dvh_handle* h, const dvh_lp* lps, int32_t count, 
   h->n_generic = ngen;
   h->n_large = nlarge;
   h->n_band = nband;
+  h->n_chain = nchain;
   h->timing[0] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   h->timing[1] = setup;
   h->timing[2] = pdhg;

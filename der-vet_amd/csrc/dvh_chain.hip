@@ -1,0 +1,1017 @@
+// dvh_chain.hip -- the medium tier: battery windows longer than one workgroup (T > 768 steps, e.g. the annual
+// hourly window n = "year", T = 8,760, or a 15-minute monthly window, T = 2,976; Model_Parameters_Template_DER.csv
+// `n`, `dt`), solved as a batch.
+//
+// A window is cut into P <= kPMax segments of <= 768 consecutive time steps; each segment is one 768-thread
+// workgroup that runs the battery-banded PDHG of dvh_band.hip on its steps (lane = step, every coefficient and
+// iterate in VGPRs), and the P workgroups of a window form a team that advances in lock step.  What couples the
+// segments each iteration:
+//   * the SOE chain: the first step of segment s needs the dual of the SOE row of the step before it (owned by
+//     s-1) in its primal half-step, and that row needs the reflected primal of s's first ene in its dual half-step
+//     -- one 8-byte value each way;
+//   * DCM demand columns (tau) whose rows lie in several segments: every segment holding rows of a tau column
+//     publishes its partial K'y sum for it, and every such segment performs the column's update redundantly from
+//     the partials summed in segment order, so all copies are bit-identical;
+//   * the restart / termination checks (every check_every iterations): per-segment partial sums, added in segment
+//     order by every segment, so every segment takes the same decision.
+// The hand-offs are 8-byte {tag, 32-bit half} granules written by one relaxed agent-scope atomic store and polled
+// by relaxed agent-scope loads (MI355X_MICROARCH.md, inter-workgroup visibility: granules need no fence); tags are
+// (window ordinal, round), so no flag or buffer ever needs resetting inside a launch, and every buffer is
+// double-buffered by round parity (a producer can be at most one round ahead of any consumer, because it needs the
+// consumer's data of the round in between).  Teams are persistent: a cooperative launch of NT x PT workgroups, all
+// resident, team t taking windows t, t + NT, ...; every spin is bounded and an expired one aborts the launch (the
+// host then reports an error), so a fault can never leave waves spinning.
+//
+// Same algorithm, scaling, steps and checks as the band kernel (restated in oracle/pdlp_ref.py); a segment's
+// arithmetic is the band kernel's for its steps, so results agree with the on-chip kernels to rounding.
+#include <type_traits>
+
+#include "dvh_device.h"
+
+namespace dvh {
+namespace {
+
+constexpr int kCB = kChainB;  // threads (and maximum steps) per segment
+constexpr int kJSeg = 4;      // tau columns per segment
+constexpr int kXSeg = 96;     // granules per segment in the exchange buffer
+// granule offsets inside a segment's area (p = round parity)
+constexpr int kOffA1 = 0;     // + 2p: dual of the segment's last SOE row
+constexpr int kOffB = 4;      // + 2p: reflected primal of the segment's first ene
+constexpr int kOffA2 = 8;     // + 8p + 2u: partial K'y of tau slot u
+constexpr int kOffK = 24;     // + 12p: KKT images {last row dual, first ene, 4 tau partials}
+constexpr int kOffC = 48;     // + 20p + 2v: check partial sums
+// poll-list entries per segment: A list at [0, 256), K list at [256, 512), C list at [512, 1020), B at [1020, 1022)
+constexpr int kPollMax = 1024;
+constexpr int kPollK = 256, kPollC = 512, kPollB = 1020;
+constexpr unsigned kSpinMax = 1u << 22;
+
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) int gi32;
+
+// KKT pieces of one column / one row (out of line, as in dvh_band.hip: the check runs every kkt_every * check_every
+// iterations and inlined it would raise the kernel's register allocation)
+struct ColKktC {
+  double rd2, cx, bt;
+};
+__device__ __noinline__ ColKktC col_kkt_c(double kt, double cj, double loj, double hij, double xj, double d) {
+  const double rc = (cj - kt) / d;
+  const bool fl = isfinite(loj), fh = isfinite(hij);
+  const double lam = (fl && fh) ? rc : (fl ? fmax(rc, 0.0) : (fh ? fmin(rc, 0.0) : 0.0));
+  const double rd = rc - lam;
+  return {rd * rd, cj * xj, (fl ? loj * d * fmax(lam, 0.0) : 0.0) + (fh ? hij * d * fmin(lam, 0.0) : 0.0)};
+}
+struct RowKktC {
+  double rp2, y2;
+};
+__device__ __noinline__ RowKktC row_kkt_c(double kv, double qi, double yi, double dr, bool ge) {
+  double r = (qi - kv) / dr;
+  if (ge) r = fmax(r, 0.0);
+  return {r * r, (yi * dr) * (yi * dr)};
+}
+
+__device__ __forceinline__ unsigned chain_tag(int wseq, int round) {
+  return ((unsigned)(wseq & 0x3FFF) << 18) | ((unsigned)round & 0x3FFFFu);
+}
+// one double as two granules {tag, hi} {tag, lo}
+__device__ __forceinline__ void put_f64(gu64* g, unsigned tag, double v) {
+  const unsigned long long t = (unsigned long long)tag << 32;
+  __hip_atomic_store(g, t | (unsigned)__double2hiint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(g + 1, t | (unsigned)__double2loint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// LDS layout (doubles): XE[B+1] YS[B+1] XT[4] XK[4] red[kNRed(NW+1)+4] TP[4][B] XP[3][B] YP[2][B] CR[kPMax][kNRed]
+//   RO[6][B] (objective and upper bound of the lane's ch, dis, ene: read-only, kept out of VGPRs)
+//   | ints: poll offsets [kPollMax], poll values [kPollMax], misc[16]
+__host__ __device__ inline size_t chain_lds_doubles() {
+  const int NW = kCB / kWave;
+  return 2 * (size_t)(kCB + 1) + 8 + (size_t)kNRed * (NW + 1) + 4 + (size_t)kJSeg * kCB + 5 * (size_t)kCB +
+         (size_t)kPMax * kNRed + 6 * (size_t)kCB;
+}
+__host__ __device__ inline size_t chain_lds_bytes() {
+  return align16(sizeof(double) * chain_lds_doubles()) + sizeof(int32_t) * (2 * (size_t)kPollMax + 16);
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Plan: one workgroup per listed window.  Verifies the battery + DCM pattern (as the band kernel), writes the
+// step -> DCM row / tau maps into the window's vbuf workspace, and cuts the steps into segments greedily: a new
+// segment starts when the current one holds kCB steps, or when a step brings a tau column the segment has no
+// slot left for.  plan[0] = P (0: not this tier; -1: already reported by the setup kernel).
+// ---------------------------------------------------------------------------------------------------------------
+constexpr int kPlanB = 1024;
+
+__global__ __launch_bounds__(kPlanB) void chain_plan_kernel(const Batch b, const Work w, const Chunk ch,
+                                                            const int32_t* list, int32_t* plan) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  int32_t* jl = reinterpret_cast<int32_t*>(smem);  // [T] tau id per step (-1: no DCM row)
+  __shared__ int32_t jmask[kChainJMax];
+  __shared__ int32_t set[kJSeg];
+  __shared__ int flag;
+  const int k = list[blockIdx.x];
+  const int kl = k - ch.first;
+  const WinOff W = win_offsets(b, ch, k);
+  const int n = W.n, m = W.m, meq = W.meq;
+  const int tid = threadIdx.x;
+  int32_t* pl = plan + (int64_t)blockIdx.x * kPlanInts;
+  const double* scal = w.scal + (int64_t)kl * kScal;
+  if (scal[6] != 0.0) {  // crossed bounds (reported) or unsupported structure
+    if (tid == 0) pl[0] = scal[6] == 3.0 ? -1 : 0;
+    return;
+  }
+  const int T = meq - 1, J = n - 3 * T, MI = m - meq;
+  if (T < 1 || T > kPMax * kCB || J < 0 || J > kChainJMax || MI < 0 || MI > T || (J == 0 && MI > 0)) {
+    if (tid == 0) pl[0] = 0;
+    return;
+  }
+  const int32_t* gkp = b.indptr + W.row;
+  const int32_t* gkc = b.indices + W.nz;
+  const double* ls = w.ls + W.wn;
+  int32_t* dm = reinterpret_cast<int32_t*>(w.vbuf + W.wn);  // [T] DCM row, [T..2T) tau id
+  for (int t = tid; t < T; t += kPlanB) {
+    dm[t] = -1;
+    dm[T + t] = -1;
+  }
+  for (int j = tid; j < kChainJMax; j += kPlanB) jmask[j] = 0;
+  if (tid == 0) flag = 0;
+  __syncthreads();
+  int bad = 0;
+  for (int r = tid; r <= T; r += kPlanB) {
+    const int p0 = gkp[r], len = gkp[r + 1] - p0;
+    if (r == 0) {
+      bad |= !(len == 1 && gkc[p0] == 2 * T);
+      continue;
+    }
+    const int t = r - 1;
+    if (len != (r < T ? 4 : 3)) {
+      bad = 1;
+      continue;
+    }
+    unsigned seen = 0;
+    for (int e = 0; e < len; ++e) {
+      const int c = gkc[p0 + e];
+      const int kind = c == t ? 0 : c == T + t ? 1 : c == 2 * T + t ? 2 : (r < T && c == 2 * T + t + 1) ? 3 : 4;
+      if (kind == 4 || ((seen >> kind) & 1u)) bad = 1;
+      seen |= 1u << kind;
+    }
+    bad |= ls[t] != 0.0 || ls[T + t] != 0.0;  // no lower bound kept for ch / dis
+  }
+  for (int i = meq + tid; i < m; i += kPlanB) {
+    const int p0 = gkp[i], len = gkp[i + 1] - p0;
+    if (len != 3) {
+      bad = 1;
+      continue;
+    }
+    int tc = -1, td = -1, jj = -1;
+    for (int e = 0; e < 3; ++e) {
+      const int c = gkc[p0 + e];
+      if (c < T) {
+        bad |= tc >= 0;
+        tc = c;
+      } else if (c < 2 * T) {
+        bad |= td >= 0;
+        td = c - T;
+      } else if (c >= 3 * T && c < 3 * T + J) {
+        bad |= jj >= 0;
+        jj = c - 3 * T;
+      } else {
+        bad = 1;
+      }
+    }
+    if (tc < 0 || td != tc || jj < 0) {
+      bad = 1;
+      continue;
+    }
+    if (atomicCAS(&dm[tc], -1, i) != -1) {  // at most one DCM row per step
+      bad = 1;
+      continue;
+    }
+    dm[T + tc] = jj;
+  }
+  if (__syncthreads_or(bad)) {
+    if (tid == 0) pl[0] = 0;
+    return;
+  }
+  for (int t = tid; t < T; t += kPlanB) jl[t] = dm[T + t];
+  __syncthreads();
+  if (tid == 0) {
+    int P = 0, s0 = 0, ns = 0, ok = 1;
+    pl[4] = 0;
+    for (int t = 0; t <= T && ok; ++t) {
+      const int j = t < T ? jl[t] : -1;
+      bool newj = j >= 0;
+      for (int u = 0; u < ns && newj; ++u) newj = set[u] != j;
+      if (t == T || t - s0 == kCB || (newj && ns == kJSeg)) {  // close segment P = [s0, t)
+        for (int u = 0; u < kJSeg; ++u) {
+          pl[24 + 4 * P + u] = u < ns ? set[u] : -1;
+          if (u < ns) jmask[set[u]] |= 1 << P;
+        }
+        ++P;
+        pl[4 + P] = t;
+        s0 = t;
+        ns = 0;
+        if (t == T) break;
+        if (P >= kPMax) ok = 0;
+        newj = j >= 0;
+      }
+      if (newj) set[ns++] = j;
+    }
+    for (int j = 0; j < J; ++j) ok &= jmask[j] != 0;  // every tau column has rows (its update has an owner)
+    for (int s = 0; s < P && ok; ++s)
+      for (int u = 0; u < kJSeg; ++u) {
+        const int id = pl[24 + 4 * s + u];
+        pl[88 + 4 * s + u] = id >= 0 ? jmask[id] : 0;
+      }
+    pl[1] = T;
+    pl[2] = J;
+    pl[3] = k;
+    pl[0] = ok ? P : 0;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// The team kernel.
+// ---------------------------------------------------------------------------------------------------------------
+struct ChainArgs {
+  const int32_t* pos;   // positions (into plan) of the windows to solve
+  int npos;
+  const int32_t* plan;
+  unsigned long long* xbuf;  // NT * PT * kXSeg granules, zeroed before the launch
+  int* abort_word;           // zeroed before the launch; set on an expired spin
+  int PT, NT;
+};
+
+__global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const Work w, const Chunk ch,
+                                                           const Opts o, const ChainArgs a) {
+  constexpr int B = kCB;
+  constexpr int NW = B / kWave;
+  constexpr int NC = 3, NR = 2;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int team = blockIdx.x / a.PT, seg = blockIdx.x % a.PT;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  double* XE = reinterpret_cast<double*>(smem);  // x-bar of ene of the lane's step; [L] = next segment's first
+  double* YS = XE + (B + 1);                     // y of row t0 + i; [0] = init row (segment 0) or the halo
+  double* XT = YS + (B + 1);                     // x-bar of the tau slots
+  double* XK = XT + kJSeg;                       // tau K'y totals of the KKT images
+  double* red = XK + kJSeg;
+  double* TP = red + kNRed * (NW + 1) + 4;       // [kJSeg][B] per-lane partial K'y of the tau slots
+  double* XP = TP + kJSeg * B;                   // [3][B] T(z) of the lane's columns (check iterations)
+  double* YP = XP + NC * B;                      // [2][B] T(z) of the lane's rows
+  double* CR = YP + NR * B;                      // [kPMax][kNRed] check partials of every segment
+  double* RO = CR + kPMax * kNRed;               // [6][B]: c of ch, dis, ene; upper bound of ch, dis, ene
+  int32_t* poff = reinterpret_cast<int32_t*>(smem + align16(sizeof(double) * chain_lds_doubles()));
+  unsigned* pval = reinterpret_cast<unsigned*>(poff + kPollMax);
+  // misc: [0] dead flag, [1] A entries, [2] K entries, [3] tau-partial start in A, [4] in K,
+  //       [8 + u] offset of slot u's partials relative to the tau start, [12 + u] share mask of slot u
+  int32_t* misc = poff + 2 * kPollMax;
+  gu64* tb = (gu64*)a.xbuf + (int64_t)team * a.PT * kXSeg;  // the team's exchange area
+  gi32* abort_word = (gi32*)a.abort_word;
+  gu64* mine = tb + (int64_t)seg * kXSeg;
+
+  if (tid == 0) misc[0] = 0;
+  __syncthreads();
+  int wseq = 0;
+  for (int wi = team; wi < a.npos; wi += a.NT) {
+    ++wseq;
+    const int32_t* pl = a.plan + (int64_t)a.pos[wi] * kPlanInts;
+    const int P = pl[0];
+    if (seg >= P) continue;
+    const int T = pl[1], k = pl[3];
+    const int t0 = pl[4 + seg], L = pl[5 + seg] - t0;
+    const bool first = seg == 0, last = seg == P - 1;
+    const int kl = k - ch.first;
+    const WinOff W = win_offsets(b, ch, k);
+    const int n = W.n;
+    const double* scal = w.scal + (int64_t)kl * kScal;
+    int nsl = 0;
+#pragma unroll
+    for (int u = 0; u < kJSeg; ++u) nsl += pl[24 + 4 * seg + u] >= 0;
+    const int wl = (L - 1) >> 6;  // wave holding the segment's last step
+    const int32_t* gkp = b.indptr + W.row;
+    const int32_t* gkc = b.indices + W.nz;
+    const double* gkv = w.kval + W.wz;
+    const double* cs = w.cs + W.wn;
+    const double* ls = w.ls + W.wn;
+    const double* us = w.us + W.wn;
+    const double* qs = w.qs + W.wm;
+    const double* dcv = w.dc + W.wn;
+    const double* drv = w.dr + W.wm;
+    const int32_t* dm = reinterpret_cast<const int32_t*>(w.vbuf + W.wn);
+    double* xo_g = b.x + W.on;
+    double* yo_g = b.y + W.om;
+    int cA = 0, cB = 0, cK = 0, cC = 0;  // rounds of each exchange kind (identical in every segment)
+
+    // ---- poll lists (offset at parity 0 in the low 16 bits, parity stride above): A = {halo dual from s-1, tau
+    //      partials of the other segments sharing a slot}; K = {halo dual image from s-1, first-ene image from
+    //      s+1, tau image partials}; partials ordered by (slot, segment)
+    if (tid == 0) {
+      int e = 0;
+      if (!first) {
+        poff[e++] = ((seg - 1) * kXSeg + kOffA1) | (2 << 16);
+        poff[e++] = ((seg - 1) * kXSeg + kOffA1 + 1) | (2 << 16);
+      }
+      misc[3] = e;
+      int ek = kPollK;
+      if (!first) {
+        poff[ek++] = ((seg - 1) * kXSeg + kOffK) | (12 << 16);
+        poff[ek++] = ((seg - 1) * kXSeg + kOffK + 1) | (12 << 16);
+      }
+      if (!last) {
+        poff[ek++] = ((seg + 1) * kXSeg + kOffK + 2) | (12 << 16);
+        poff[ek++] = ((seg + 1) * kXSeg + kOffK + 3) | (12 << 16);
+      }
+      misc[4] = ek - kPollK;
+      int rel = 0;
+      for (int u = 0; u < nsl; ++u) {
+        const int id = pl[24 + 4 * seg + u], msk = pl[88 + 4 * seg + u];
+        misc[8 + u] = rel;
+        misc[12 + u] = msk;
+        for (int r = 0; r < P; ++r) {
+          if (!((msk >> r) & 1) || r == seg) continue;
+          int ur = 0;
+          while (ur < kJSeg - 1 && pl[24 + 4 * r + ur] != id) ++ur;
+          poff[e++] = (r * kXSeg + kOffA2 + 2 * ur) | (8 << 16);
+          poff[e++] = (r * kXSeg + kOffA2 + 2 * ur + 1) | (8 << 16);
+          poff[ek++] = (r * kXSeg + kOffK + 4 + 2 * ur) | (12 << 16);
+          poff[ek++] = (r * kXSeg + kOffK + 5 + 2 * ur) | (12 << 16);
+          rel += 2;
+        }
+      }
+      misc[1] = e;
+      misc[2] = ek - kPollK;
+    }
+    __syncthreads();
+    const int nA = misc[1], nK = misc[2], aTau = misc[3], kTau = misc[4];
+
+    // polls entries [e0, e0 + cnt) for round c (tag, parity); the 32-bit halves land in pval[e0 ..]; false: the
+    // spin expired or another workgroup aborted (the abort word is then set)
+    auto poll = [&](int e0, int cnt, int c) -> bool {
+      const unsigned tag = chain_tag(wseq, c);
+      const int par = c & 1;
+      for (int base = 0; base < cnt; base += kWave) {
+        const int e = base + lane;
+        const bool act = e < cnt;
+        const int ent = act ? poff[e0 + e] : 0;
+        gu64* p = tb + (ent & 0xFFFF) + par * (ent >> 16);
+        bool ok = !act;
+        unsigned v = 0, seen = 0;
+        unsigned spins = 0;
+        while (true) {
+          if (!ok) {
+            const unsigned long long xv = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            seen = (unsigned)(xv >> 32);
+            if (seen == tag) {
+              ok = true;
+              v = (unsigned)xv;
+            }
+          }
+          if (__all(ok)) break;
+          ++spins;
+          if ((spins & 1023u) == 0 &&
+              (spins > kSpinMax || __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+            // diagnostics per workgroup (abort_word[16 + 8 blockIdx]): {1 = timed out / 2 = saw the abort, list
+            // start, round, entry, expected tag, tag seen}
+            const unsigned long long bad = __ballot(!ok);
+            const int fl = bad ? __ffsll((long long)bad) - 1 : 0;
+            if (lane == fl) {
+              const int d[6] = {spins > kSpinMax ? 1 : 2, e0, c, ent, (int)tag, (int)seen};
+              for (int u = 0; u < 6; ++u)
+                __hip_atomic_store(abort_word + 16 + 8 * (int)blockIdx.x + u, d[u], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (lane == 0) __hip_atomic_store(abort_word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+          }
+        }
+        if (act) pval[e0 + e] = v;
+      }
+      return true;
+    };
+    auto pv64 = [&](int e) { return __hiloint2double((int)pval[e], (int)pval[e + 1]); };
+    // tau total of slot u from this segment's partial and the polled ones (entries at e0 + rel[u] ..), summed in
+    // segment order -- the same additions in every segment holding the slot's rows
+    auto tau_total = [&](int u, double own, int e0) -> double {
+      const int msk = misc[12 + u];
+      int e = e0 + misc[8 + u];
+      double s = 0.0;
+      for (int r = 0; r < P; ++r) {
+        if (!((msk >> r) & 1)) continue;
+        if (r == seg) {
+          s += own;
+        } else {
+          s += pv64(e);
+          e += 2;
+        }
+      }
+      return s;
+    };
+
+    // ---- the lane's step t = t0 + tid
+    const int t = t0 + tid;
+    const bool val = tid < L;
+    auto col = [&](int v) { return v * T + t; };
+    double x[NC], xa[NC];
+    double loe = 0.0;
+    double ks[4] = {0.0, 0.0, 0.0, 0.0};  // SOE row of step t: ch_t, dis_t, ene_t, ene_{t+1}
+    double kd[3] = {0.0, 0.0, 0.0};       // DCM row of step t: ch_t, dis_t, tau
+    double kp = 0.0;                      // ene_t in row t (init row or the previous step's SOE row)
+    double y[NR], ya[NR], q[2];
+    int drow = -1, jt = 0;
+#pragma unroll
+    for (int v = 0; v < NC; ++v) {
+      x[v] = xa[v] = 0.0;
+      RO[v * B + tid] = RO[(NC + v) * B + tid] = 0.0;
+    }
+    auto cof = [&](int v) -> double { return RO[v * B + tid]; };
+    auto hib = [&](int v) -> double { return RO[(NC + v) * B + tid]; };
+#pragma unroll
+    for (int r = 0; r < NR; ++r) y[r] = ya[r] = 0.0;
+    q[0] = q[1] = 0.0;
+    if (val) {
+#pragma unroll
+      for (int v = 0; v < NC; ++v) {
+        const int j = col(v);
+        RO[(NC + v) * B + tid] = us[j];
+        RO[v * B + tid] = cs[j];
+        x[v] = xa[v] = fmin(fmax(0.0, ls[j]), us[j]);
+      }
+      loe = ls[2 * T + t];
+      for (int p = gkp[t + 1]; p < gkp[t + 2]; ++p) {
+        const int c = gkc[p];
+        const double av = gkv[p];
+        if (c == t) ks[0] = av;
+        else if (c == T + t) ks[1] = av;
+        else if (c == 2 * T + t) ks[2] = av;
+        else ks[3] = av;
+      }
+      for (int p = gkp[t]; p < gkp[t + 1]; ++p)
+        if (gkc[p] == 2 * T + t) kp = gkv[p];
+      q[0] = qs[t + 1];
+      drow = dm[t];
+      if (drow >= 0) {
+        const int jg = dm[T + t];
+#pragma unroll
+        for (int u = 0; u < kJSeg; ++u)
+          if (pl[24 + 4 * seg + u] == jg) jt = u;
+        for (int p = gkp[drow]; p < gkp[drow + 1]; ++p) {
+          const int c = gkc[p];
+          const double av = gkv[p];
+          if (c < T) kd[0] = av;
+          else if (c < 2 * T) kd[1] = av;
+          else kd[2] = av;
+        }
+        q[1] = qs[drow];
+      }
+      if (o.warm) {
+#pragma unroll
+        for (int v = 0; v < NC; ++v) {
+          const int j = col(v);
+          x[v] = xa[v] = fmin(fmax(xo_g[j] / dcv[j], ls[j]), us[j]);
+        }
+        y[0] = ya[0] = yo_g[t + 1] / drv[t + 1];
+        if (drow >= 0) y[1] = ya[1] = fmax(yo_g[drow] / drv[drow], 0.0);
+      }
+    }
+    const int xta = lds_addr(XT + jt);
+    // wave 0 special lanes: u < nsl the tau slots {x, xa, c, lo, hi, x+}; kInitLane (segment 0) the init row
+    // {y, ya, y+, q, coefficient, -}
+    constexpr int kInitLane = kWave - 1;
+    static_assert(kJSeg < kInitLane, "tau lanes and the init-row lane are distinct");
+    const bool tlane = wid == 0 && lane < nsl, ilane = first && wid == 0 && lane == kInitLane;
+    int jg0 = 0;
+    bool town = false;  // this segment owns the slot (the lowest segment holding its rows): KKT / norm terms
+    if (tlane) {
+      jg0 = pl[24 + 4 * seg + lane];
+      town = (__ffs(pl[88 + 4 * seg + lane]) - 1) == seg;
+    }
+    double sp[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    if (tlane) {
+      const double l0 = ls[3 * T + jg0], h0 = us[3 * T + jg0];
+      sp[0] = sp[1] = sp[5] = fmin(fmax(0.0, l0), h0);
+      sp[2] = cs[3 * T + jg0];
+      sp[3] = l0;
+      sp[4] = h0;
+      if (o.warm) sp[0] = sp[1] = sp[5] = fmin(fmax(xo_g[3 * T + jg0] / dcv[3 * T + jg0], l0), h0);
+    }
+    if (ilane) {
+      sp[3] = qs[0];
+      sp[4] = gkv[gkp[0]];
+      if (o.warm) sp[0] = sp[1] = sp[2] = yo_g[0] / drv[0];
+    }
+    if (tid < kJSeg) XT[tid] = XK[tid] = 0.0;
+    if (tid == 0) XE[B] = YS[B] = 0.0;
+    XE[tid] = YS[tid] = 0.0;
+    for (int u = tid; u < kJSeg * B; u += B) TP[u] = 0.0;
+#pragma unroll
+    for (int v = 0; v < NC; ++v) XP[v * B + tid] = x[v];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) YP[r * B + tid] = y[r];
+    __syncthreads();
+
+    // ---- SpMV pieces (as dvh_band.hip)
+    auto ktr = [&](const double (&vr)[NR], double vprev, double (&out)[NC]) {
+      out[0] = fma(kd[0], vr[1], ks[0] * vr[0]);
+      out[1] = fma(kd[1], vr[1], ks[1] * vr[0]);
+      out[2] = fma(ks[2], vr[0], kp * vprev);
+    };
+    auto kown = [&](const double (&v)[NC], double (&os)[NR]) {
+      os[0] = fma(ks[2], v[2], fma(ks[1], v[1], ks[0] * v[0]));
+      os[1] = fma(kd[1], v[1], kd[0] * v[0]);
+    };
+    auto kfin = [&](double (&os)[NR], double vnext) {
+      os[0] = fma(ks[3], vnext, os[0]);
+      os[1] = fma(kd[2], lds_ld(xta), os[1]);
+    };
+    auto tau_parts = [&](double vd) {
+      if (nsl == 1) {
+        TP[tid] = kd[2] * vd;
+      } else {
+        for (int j = 0; j < nsl; ++j) TP[j * B + tid] = (jt == j ? kd[2] : 0.0) * vd;
+      }
+    };
+    // wave 0: lane u < nsl gets this segment's partial sum of TP[u][.] (fixed order)
+    auto tau_own = [&]() {
+      double res = 0.0;
+      for (int j = 0; j < nsl; ++j) {
+        double s = 0.0;
+#pragma unroll
+        for (int r = 0; r < NW; ++r) s += TP[j * B + r * kWave + lane];
+        s = uniform(wave_sum_dpp(s));
+        if (lane == j) res = s;
+      }
+      return res;
+    };
+    // wave 0, start of a primal phase (after every wave advanced cA): publish this segment's tau partials (round
+    // cA), poll round cA (the halo dual of s-1 -> YS[0], the sharers' partials); returns the tau totals in lanes
+    // u < nsl; false in ok: abort
+    auto round_a = [&](bool& ok) -> double {
+      const unsigned tag = chain_tag(wseq, cA);
+      const double own = tau_own();
+      if (lane < nsl) put_f64(mine + kOffA2 + 8 * (cA & 1) + 2 * lane, tag, own);
+      if (!poll(0, nA, cA)) {
+        ok = false;
+        return 0.0;
+      }
+      if (!first && lane == 0) YS[0] = pv64(0);
+      double tot = 0.0;
+      for (int u = 0; u < nsl; ++u) {
+        const double tu = tau_total(u, readlane_f64(own, u), aTau);
+        if (lane == u) tot = tu;
+      }
+      return tot;
+    };
+    auto publish_a1 = [&](double ylast) {  // lane L-1: dual of the last SOE row for s+1 (round cA + 1)
+      if (!last && tid == L - 1) put_f64(mine + kOffA1 + 2 * ((cA + 1) & 1), chain_tag(wseq, cA + 1), ylast);
+    };
+    auto publish_b = [&](double xe0) {  // lane 0: reflected first ene for s-1 (round cB)
+      if (!first && tid == 0) put_f64(mine + kOffB + 2 * (cB & 1), chain_tag(wseq, cB), xe0);
+    };
+    auto poll_b = [&]() -> bool {  // wave wl: the next segment's first ene (round cB) -> XE[L]
+      if (last) return true;
+      if (lane == 0) {
+        poff[kPollB] = ((seg + 1) * kXSeg + kOffB) | (2 << 16);
+        poff[kPollB + 1] = ((seg + 1) * kXSeg + kOffB + 1) | (2 << 16);
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (!poll(kPollB, 2, cB)) return false;
+      if (lane == 0) XE[L] = pv64(kPollB);
+      return true;
+    };
+    // check reduction: this segment's NV partials (identical in every lane on entry) -> the sums over all segments
+    // in segment order, in every lane; false: abort
+    auto round_c = [&](auto& acc) -> bool {
+      constexpr int nv = sizeof(acc) / sizeof(double);
+      ++cC;
+      if (wid == 0) {
+        const unsigned tag = chain_tag(wseq, cC);
+        double mv = 0.0;
+#pragma unroll
+        for (int v = 0; v < nv; ++v)
+          if (lane == v) mv = acc[v];
+        if (lane < nv) put_f64(mine + kOffC + 20 * (cC & 1) + 2 * lane, tag, mv);
+        int e = 0;
+        for (int r = 0; r < P; ++r) {
+          if (r == seg) continue;
+          if (lane < 2 * nv) poff[kPollC + e + lane] = (r * kXSeg + kOffC + lane) | (20 << 16);
+          e += 2 * nv;
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (!poll(kPollC, e, cC)) {
+          if (lane == 0) misc[0] = 1;
+        } else {
+          e = 0;
+          for (int r = 0; r < P; ++r) {
+            if (lane < nv) CR[r * kNRed + lane] = r == seg ? mv : pv64(kPollC + e + 2 * lane);
+            if (r != seg) e += 2 * nv;
+          }
+        }
+      }
+      lds_barrier();
+      if (misc[0]) return false;
+#pragma unroll
+      for (int v = 0; v < nv; ++v) {
+        double s = 0.0;
+        for (int r = 0; r < P; ++r) s += CR[r * kNRed + v];
+        acc[v] = s;
+      }
+      lds_barrier();  // CR is rewritten by the next reduction
+      return true;
+    };
+
+    // ---- ||Kt||_2 by power iteration (as the band kernel, exchanging across the segment boundaries)
+    double eta = scal[0];
+    bool alive = true;
+    {
+      const int PI = o.power_iters;
+      const double v0 = 1.0 / sqrt((double)n);
+      double vc[NC];
+#pragma unroll
+      for (int v = 0; v < NC; ++v) vc[v] = val ? v0 : 0.0;
+      double vtau = tlane ? v0 : 0.0;
+      double nv[2] = {0.0, 0.0};
+      double wr[NR] = {0.0, 0.0};
+      for (int pi = 0; pi <= PI; ++pi) {
+        if (pi > 0) {
+          double kt = 0.0;
+          ++cA;  // every wave: publish_a1 (wave wl) names the next round by it
+          if (wid == 0) {
+            bool ok = true;
+            kt = round_a(ok);
+            if (!ok && lane == 0) misc[0] = 1;
+          }
+          ktr(wr, YS[tid], vc);
+          if (tlane) vtau = kt;
+        }
+        if (pi >= PI - 1) {
+          double s = town ? vtau * vtau : 0.0;
+#pragma unroll
+          for (int v = 0; v < NC; ++v) s = fma(vc[v], vc[v], s);
+          nv[pi - (PI - 1)] = s;
+        }
+        if (pi == PI) break;
+        XE[tid] = vc[2];
+        if (tlane) XT[lane] = vtau;
+        ++cB;
+        publish_b(vc[2]);
+        lds_barrier();
+        if (misc[0]) {
+          alive = false;
+          break;
+        }
+        if (wid == wl && !poll_b() && lane == 0) misc[0] = 1;
+        kown(vc, wr);
+        kfin(wr, XE[tid + 1]);
+        YS[tid + 1] = wr[0];
+        publish_a1(wr[0]);
+        if (ilane) YS[0] = sp[4] * XE[0];
+        if (nsl > 0) tau_parts(wr[1]);
+        lds_barrier();
+        if (misc[0]) {
+          alive = false;
+          break;
+        }
+      }
+      if (alive) {
+        lds_barrier();
+        if (misc[0]) alive = false;
+      }
+      if (alive) {
+        block_sum<B, 2>(nv, red);
+        alive = round_c(nv);
+        if (alive && nv[0] > 0.0 && nv[1] > 0.0) eta = o.step_safety / sqrt(sqrt(nv[1] / nv[0]));
+      }
+      YS[tid] = 0.0;
+      if (tid == 0) YS[B] = 0.0;
+      for (int u = tid; u < kJSeg * B; u += B) TP[u] = 0.0;
+      __syncthreads();
+    }
+    if (!alive) break;
+    // y images of the starting point (YS, TP), and the halo dual for the first primal phase
+    if (val) YS[tid + 1] = y[0];
+    if (ilane) YS[0] = sp[0];
+    if (nsl > 0) tau_parts(y[1]);
+    publish_a1(y[0]);
+    __syncthreads();
+
+    eta = uniform(eta);
+    double pw = uniform(scal[1]);
+    const double cnorm = uniform(scal[2]), qnorm = uniform(scal[3]), c0 = uniform(b.c0[k]);
+    int it = 0, kin = 0, status = kIterLimit;
+    double r0 = -1.0, rprev = -1.0;
+    double fin[4] = {NAN, NAN, NAN, NAN};
+    const int chk = o.check_every > 0 ? o.check_every : 64;
+    double tau = uniform(eta / pw), sigma = uniform(eta * pw);
+    const int kkt_every = o.kkt_every > 0 ? o.kkt_every : 1;
+    int ck = chk, kk_ = kkt_every;
+    int kbase = 0;
+    auto hload = [&](int k0_) {
+      const int kq = k0_ + lane;
+      return kq < kHalpernTab ? w.hinv[kq] : 1.0 / (kq + 2.0);
+    };
+    double hw = hload(0);
+    double mv0, mv1, mv2, mv3;
+    double kx[NR];  // own-column part of K x-bar for the dual half-step
+
+    auto iterate = [&](auto chk_tag) __attribute__((always_inline)) {
+      constexpr bool CHECK = decltype(chk_tag)::value;
+      if (kin - kbase >= kWave) {
+        kbase = kin;
+        hw = hload(kin);
+      }
+      const double cb = readlane_f64(hw, kin - kbase), ca = 1.0 - cb;
+      mv0 = mv1 = mv2 = mv3 = 0.0;
+      // ---------------- primal half-step (reflected Halpern, rho = 1)
+      {
+        double kt = 0.0;
+        ++cA;
+        if (wid == 0) {
+          bool ok = true;
+          kt = round_a(ok);
+          if (!ok && lane == 0) misc[0] = 1;
+        }
+        double kty[NC], xb[NC];
+        ktr(y, YS[tid], kty);
+#pragma unroll
+        for (int v = 0; v < NC; ++v) {  // padding steps have c = lo = hi = 0 and stay at 0
+          const double lo = v == 2 ? loe : 0.0;
+          const double p1 = vmin(vmax(fma(-tau, cof(v) - kty[v], x[v]), lo), hib(v));
+          xb[v] = fma(2.0, p1, -x[v]);
+          if (CHECK) {
+            const double d = x[v] - p1, da = p1 - xa[v];
+            mv0 += d * d;
+            mv1 += da * da;
+            XP[v * B + tid] = p1;
+          }
+          x[v] = fma(ca, xb[v], cb * xa[v]);
+        }
+        XE[tid] = xb[2];
+        ++cB;
+        publish_b(xb[2]);
+        if (tlane) {
+          const double xo = sp[0], xan = sp[1];
+          const double p1 = vmin(vmax(fma(-tau, sp[2] - kt, xo), sp[3]), sp[4]);
+          const double xbt = fma(2.0, p1, -xo);
+          XT[lane] = xbt;
+          sp[0] = fma(ca, xbt, cb * xan);
+          if (CHECK) {
+            if (town) {
+              const double d = xo - p1, da = p1 - xan;
+              mv0 += d * d;
+              mv1 += da * da;
+            }
+            sp[5] = p1;
+          }
+        }
+        kown(xb, kx);
+      }
+      lds_barrier();
+      // ---------------- dual half-step
+      {
+        if (wid == wl && !poll_b() && lane == 0) misc[0] = 1;
+        kfin(kx, XE[tid + 1]);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {  // row 0 (SOE) is an equality; the DCM row is >=: its dual stays >= 0
+          double p1 = fma(sigma, q[r] - kx[r], y[r]);
+          if (r > 0) p1 = vmax(p1, 0.0);
+          if (CHECK) {
+            const double d = y[r] - p1, da = p1 - ya[r];
+            mv2 += d * d;
+            mv3 += da * da;
+            YP[r * B + tid] = p1;
+          }
+          y[r] = fma(ca, fma(2.0, p1, -y[r]), cb * ya[r]);
+        }
+        YS[tid + 1] = y[0];
+        if (!CHECK) publish_a1(y[0]);
+        if (nsl > 0) tau_parts(y[1]);
+        if (ilane) {  // init row (segment 0): ene_0 = target
+          const double y0 = sp[0], ya0 = sp[1];
+          const double q1 = fma(sigma, sp[3] - sp[4] * XE[0], y0);
+          if (CHECK) {
+            const double d = y0 - q1, da = q1 - ya0;
+            mv2 += d * d;
+            mv3 += da * da;
+            sp[2] = q1;
+          }
+          const double yn = fma(ca, fma(2.0, q1, -y0), cb * ya0);
+          sp[0] = yn;
+          YS[0] = yn;
+        }
+      }
+      ++it;
+      ++kin;
+      lds_barrier();
+    };
+
+    using F = std::integral_constant<bool, false>;
+    using Tt = std::integral_constant<bool, true>;
+    while (it < o.max_iters) {
+      if (--ck != 0) {
+        iterate(F());
+        if (misc[0]) break;
+        continue;
+      }
+      ck = chk;
+      iterate(Tt());
+      if (misc[0]) break;
+      // ---------------- check (as the band kernel), over the whole window
+      const bool kkt = (--kk_ == 0) || (it + chk > o.max_iters);
+      if (kkt) kk_ = kkt_every;
+      double acc[kNRed];
+      acc[0] = mv0;
+      acc[1] = mv1;
+      acc[2] = mv2;
+      acc[3] = mv3;
+#pragma unroll
+      for (int u = 4; u < kNRed; ++u) acc[u] = 0.0;
+      if (kkt) {
+        // images of T(z_k); the boundary images and the tau image totals come from the neighbours / sharers
+        double xp[NC], yp[NR];
+#pragma unroll
+        for (int v = 0; v < NC; ++v) xp[v] = XP[v * B + tid];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) yp[r] = YP[r * B + tid];
+        XE[tid] = xp[2];
+        YS[tid + 1] = yp[0];
+        if (ilane) YS[0] = sp[2];
+        if (tlane) XT[lane] = sp[5];
+        if (nsl > 0) tau_parts(yp[1]);
+        lds_barrier();
+        if (wid == 0) {
+          ++cK;
+          const unsigned tag = chain_tag(wseq, cK);
+          gu64* g = mine + kOffK + 12 * (cK & 1);
+          const double own = tau_own();
+          if (lane == 0 && !last) put_f64(g, tag, YS[L]);
+          if (lane == 1 && !first) put_f64(g + 2, tag, XE[0]);
+          if (lane < nsl) put_f64(g + 4 + 2 * lane, tag, own);
+          if (!poll(kPollK, nK, cK)) {
+            if (lane == 0) misc[0] = 1;
+          } else {
+            int e = kPollK;
+            if (!first) {
+              if (lane == 0) YS[0] = pv64(e);
+              e += 2;
+            }
+            if (!last && lane == 0) XE[L] = pv64(e);
+            double tot = 0.0;
+            for (int u = 0; u < nsl; ++u) {
+              const double tu = tau_total(u, readlane_f64(own, u), kPollK + kTau);
+              if (lane == u) tot = tu;
+            }
+            if (lane < nsl) XK[lane] = tot;
+          }
+        }
+        lds_barrier();
+        if (misc[0]) break;
+        auto col_kkt = [&](int j, double kt, double cj, double loj, double hij, double xj) {
+          const ColKktC r = col_kkt_c(kt, cj, loj, hij, xj, dcv[opaque(j)]);
+          acc[5] += r.rd2;
+          acc[6] += r.cx;
+          acc[8] += r.bt;
+        };
+        auto row_kkt = [&](int i, double kv, double qi, double yi, bool ge) {
+          const RowKktC r = row_kkt_c(kv, qi, yi, drv[opaque(i)], ge);
+          acc[4] += r.rp2;
+          acc[7] += qi * yi;
+          acc[9] += r.y2;
+        };
+        double kt[NC];
+        ktr(yp, YS[tid], kt);
+        if (val) {
+#pragma unroll
+          for (int v = 0; v < NC; ++v) col_kkt(col(v), kt[v], cof(v), v == 2 ? loe : 0.0, hib(v), xp[v]);
+        }
+        if (tlane && town) col_kkt(3 * T + jg0, XK[lane], sp[2], sp[3], sp[4], sp[5]);
+        double kv[NR];
+        kown(xp, kv);
+        kfin(kv, XE[tid + 1]);
+        if (val) row_kkt(t + 1, kv[0], q[0], yp[0], false);
+        if (drow >= 0) row_kkt(drow, kv[1], q[1], yp[1], true);
+        if (ilane) row_kkt(0, sp[4] * XE[0], sp[3], sp[2], false);
+      }
+      if (kkt) {
+        block_sum1<B, kNRed, true>(acc, red);
+        if (!round_c(acc)) break;
+      } else {
+        double acc4[4] = {acc[0], acc[1], acc[2], acc[3]};
+        block_sum1<B, 4, true>(acc4, red);
+        if (!round_c(acc4)) break;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[u] = acc4[u];
+      }
+      if (kkt) {
+        const double pobj = acc[6] + c0, dobj = acc[7] + acc[8] + c0;
+        const double pres = sqrt(acc[4]) / (1.0 + qnorm), dres = sqrt(acc[5]) / (1.0 + cnorm);
+        const double gap = fabs(pobj - dobj) / (1.0 + fabs(pobj) + fabs(dobj));
+        fin[0] = pobj;
+        fin[1] = pres;
+        fin[2] = dres;
+        fin[3] = gap;
+        if (kkt_done(o, pres, dres, gap, pobj, dobj, acc[4], acc[9])) {
+          status = kOptimal;
+          break;
+        }
+        if (!(isfinite(pobj) && isfinite(dobj))) {
+          status = kNumerical;
+          break;
+        }
+      }
+      const double r = sqrt(pw * acc[0] + acc[2] / pw);
+      if (r0 < 0.0) r0 = r;
+      const bool restart = (r <= o.b_suff * r0) || (r <= o.b_nec * r0 && rprev >= 0.0 && r > rprev) ||
+                           ((double)kin >= o.b_art * (double)it);
+      if (restart) {
+        const double ddx = sqrt(acc[1]), ddy = sqrt(acc[3]);
+        if (ddx > 1e-10 && ddy > 1e-10) pw = uniform(pw_update(ddy / ddx, pw, o.theta));
+        tau = uniform(eta / pw);
+        sigma = uniform(eta * pw);
+#pragma unroll
+        for (int v = 0; v < NC; ++v) x[v] = xa[v] = XP[v * B + tid];
+#pragma unroll
+        for (int rr = 0; rr < NR; ++rr) y[rr] = ya[rr] = YP[rr * B + tid];
+        if (ilane) sp[0] = sp[1] = sp[2];
+        if (tlane) sp[0] = sp[1] = sp[5];
+        kin = 0;
+        kbase = 0;
+        hw = hload(0);
+        r0 = r;
+        rprev = -1.0;
+      } else {
+        rprev = r;
+      }
+      if (restart || kkt) {  // the y images must hold z again (after a restart z = T(z_k))
+        YS[tid + 1] = y[0];
+        if (ilane) YS[0] = sp[0];
+        if (nsl > 0) tau_parts(y[1]);
+      }
+      publish_a1(y[0]);  // the halo dual for the next primal phase, after the check (restart included)
+      lds_barrier();
+    }
+    if (misc[0]) break;
+    // outputs: the last check's T(z_k), unscaled
+    if (val) {
+#pragma unroll
+      for (int v = 0; v < NC; ++v) xo_g[col(v)] = XP[v * B + tid] * dcv[col(v)];
+      yo_g[t + 1] = YP[tid] * drv[t + 1];
+      if (drow >= 0) yo_g[drow] = YP[B + tid] * drv[drow];
+    }
+    if (tlane && town) xo_g[3 * T + jg0] = sp[5] * dcv[3 * T + jg0];
+    if (ilane) yo_g[0] = sp[2] * drv[0];
+    if (first && tid == 0) {
+      b.istats[2 * k] = status;
+      b.istats[2 * k + 1] = it;
+      for (int u = 0; u < 4; ++u) b.stats[4 * k + u] = fin[u];
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+hipError_t launch_chain_plan(const Batch& b, const Work& w, const Chunk& ch, const int32_t* list, int nlist,
+                             int max_T, int32_t* plan, hipStream_t s) {
+  const size_t lds = sizeof(int32_t) * (size_t)std::max(max_T, 1);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  hipError_t e = hipFuncSetAttribute((const void*)chain_plan_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(chain_plan_kernel, dim3(nlist), dim3(kPlanB), lds, s, b, w, ch, list, plan);
+  return hipGetLastError();
+}
+
+hipError_t chain_capacity(int device, int* blocks) {
+  const size_t lds = chain_lds_bytes();
+  hipError_t e = hipFuncSetAttribute((const void*)pdhg_chain_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds);
+  if (e != hipSuccess) return e;
+  int per_cu = 0, cus = 0;
+  e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)pdhg_chain_kernel, kCB, lds);
+  if (e != hipSuccess) return e;
+  e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+  if (e != hipSuccess) return e;
+  *blocks = per_cu * cus;
+  return hipSuccess;
+}
+
+size_t chain_abort_bytes(int NT, int PT) { return sizeof(int32_t) * (16 + 8 * (size_t)NT * PT); }
+size_t chain_xbuf_bytes(int NT, int PT) { return sizeof(unsigned long long) * (size_t)NT * PT * kXSeg; }
+
+hipError_t launch_chain(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, const int32_t* pos, int npos,
+                        const int32_t* plan, int PT, int NT, void* xbuf, int32_t* abort_word, hipStream_t s) {
+  const size_t lds = chain_lds_bytes();
+  hipError_t e = hipFuncSetAttribute((const void*)pdhg_chain_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(xbuf, 0, chain_xbuf_bytes(NT, PT), s);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(abort_word, 0, chain_abort_bytes(NT, PT), s);
+  if (e != hipSuccess) return e;
+  ChainArgs a{pos, npos, plan, static_cast<unsigned long long*>(xbuf), abort_word, PT, NT};
+  Batch bb = b;
+  Work ww = w;
+  Chunk cc = ch;
+  Opts oo = o;
+  void* args[] = {&bb, &ww, &cc, &oo, &a};
+  return hipLaunchCooperativeKernel((const void*)pdhg_chain_kernel, dim3(NT * PT), dim3(kCB), args, (unsigned)lds, s);
+}
+
+}  // namespace dvh

@@ -12,7 +12,12 @@ constexpr int kLongRow = 32;   // CSR rows longer than this are reduced by a who
 constexpr int kLMax = 64;      // long rows per matrix per window handled on chip
 constexpr int kScal = 16;      // per-window scalars written by the setup kernel
 constexpr int kHalpernTab = 65536;  // table of Halpern weights 1/(k+2)
-constexpr int kSmallMax = 4096;     // windows with n or m above this go to the grid-wide large-LP path
+constexpr int kSmallMax = 4096;     // windows with n or m above this go to the medium tier or the large-LP path
+// Medium tier (dvh_chain.hip): battery windows of up to kPMax segments of kChainB steps, one workgroup per segment
+constexpr int kChainB = 768;
+constexpr int kPMax = 16;
+constexpr int kChainJMax = 256;     // tau (demand) columns per medium window
+constexpr int kPlanInts = 160;      // plan words per window: P, T, J, k, starts[17], slot ids[16][4], masks[16][4]
 
 // Kernel-side copy of dvh_options (POD, passed by value).
 struct Opts {
@@ -92,6 +97,19 @@ hipError_t launch_pdhg_ell(const Batch& b, const Work& w, const Chunk& ch, const
 hipError_t launch_pdhg_band(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, hipStream_t s, bool ice,
                             const int32_t* list, int nlist);
 size_t setup_lds_bytes(int max_n, int max_m);
+// Setup (scaling, transpose) of the listed medium windows (scaling vectors kept in the global workspace).
+hipError_t launch_setup_medium(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n,
+                               const int32_t* list, int nlist, hipStream_t s);
+// Medium tier (dvh_chain.hip): plan (structure check + segmentation, plan[kPlanInts] per listed window, plan[0] =
+// P, 0 = not this tier, -1 = reported infeasible by the setup) and the team kernel over the windows at positions
+// pos[] of the plan (PT workgroups per team, NT teams, cooperative launch; xbuf >= chain_xbuf_bytes(NT, PT)).
+hipError_t launch_chain_plan(const Batch& b, const Work& w, const Chunk& ch, const int32_t* list, int nlist,
+                             int max_T, int32_t* plan, hipStream_t s);
+hipError_t chain_capacity(int device, int* blocks);
+size_t chain_xbuf_bytes(int NT, int PT);
+size_t chain_abort_bytes(int NT, int PT);  // abort word + per-workgroup diagnostics
+hipError_t launch_chain(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, const int32_t* pos, int npos,
+                        const int32_t* plan, int PT, int NT, void* xbuf, int32_t* abort_word, hipStream_t s);
 // Power iteration for ||Kt||_2 of the listed windows (generic path; the ELL kernel does its own on chip).
 hipError_t launch_power(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, const int32_t* list, int nlist,
                         hipStream_t s);

@@ -70,18 +70,22 @@ __device__ __forceinline__ void rows_reduce(const int32_t* ptr, int rows, const 
   }
 }
 
-__global__ __launch_bounds__(kSetupB) void setup_kernel(const Batch b, const Work w, const Chunk ch, const Opts o) {
+// MED: the listed windows of the medium tier (n or m above small_max, solved by the chain kernel, dvh_chain.hip):
+// Dr / Dc stay in the global workspace instead of LDS (they do not fit), everything else as for on-chip windows.
+template <bool MED>
+__global__ __launch_bounds__(kSetupB) void setup_kernel(const Batch b, const Work w, const Chunk ch, const Opts o,
+                                                        const int32_t* list) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ double red[(kSetupB / kWave + 1) * 4];
   __shared__ int sh_part[kSetupB];
   __shared__ int sh_cnt[2];
-  const int k = ch.first + blockIdx.x;
-  const int kl = blockIdx.x;
+  const int k = MED ? list[blockIdx.x] : ch.first + (int)blockIdx.x;
+  const int kl = k - ch.first;
   const WinOff W = win_offsets(b, ch, k);
   const int n = W.n, m = W.m, nnz = W.nnz;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   int32_t* cursor = reinterpret_cast<int32_t*>(smem);  // [n + 1]
-  if (n > o.small_max || m > o.small_max) {  // solved by the grid-wide large-LP path (dvh_large.hip)
+  if (!MED && (n > o.small_max || m > o.small_max)) {  // medium tier or the grid-wide large-LP path
     if (tid == 0) {
       w.scal[(int64_t)kl * kScal] = 0.0;
       w.scal[(int64_t)kl * kScal + 6] = 2.0;
@@ -232,8 +236,8 @@ __global__ __launch_bounds__(kSetupB) void setup_kernel(const Batch b, const Wor
   // 5. Ruiz (inf-norm) passes, then one Pock-Chambolle (alpha = 1) pass.  Dr / Dc live in LDS from here on
   //    (the transpose cursors are dead): the row / column passes gather Dc[Kc[p]] and Dr[Ti[p]] from LDS
   //    instead of a dependent global load; copied to the workspace at the end.
-  double* Dr = reinterpret_cast<double*>(smem);
-  double* Dc = Dr + m;
+  double* Dr = MED ? gDr : reinterpret_cast<double*>(smem);
+  double* Dc = MED ? gDc : Dr + m;
   for (int j = tid; j < n; j += kSetupB) Dc[j] = 1.0;
   for (int i = tid; i < m; i += kSetupB) Dr[i] = 1.0;
   __syncthreads();
@@ -287,8 +291,10 @@ __global__ __launch_bounds__(kSetupB) void setup_kernel(const Batch b, const Wor
     nrm[1] += qi * d * qi * d;
     nrm[3] += qi * qi;
   }
-  for (int j = tid; j < n; j += kSetupB) gDc[j] = Dc[j];
-  for (int i = tid; i < m; i += kSetupB) gDr[i] = Dr[i];
+  if (!MED) {
+    for (int j = tid; j < n; j += kSetupB) gDc[j] = Dc[j];
+    for (int i = tid; i < m; i += kSetupB) gDr[i] = Dr[i];
+  }
   block_sum<kSetupB, 4>(nrm, red);
   // 8. row-length statistics for the ELL fast path: max length among rows with <= kEllMax entries and
   //    the number of longer rows, for K and K^T
@@ -1657,9 +1663,23 @@ hipError_t launch_setup(const Batch& b, const Work& w, const Chunk& ch, const Op
   const size_t lds = setup_lds_bytes(max_n, max_m);
   Opts o2 = o;
   o2.setup_segments = setup_segments(max_n);
-  hipError_t e = hipFuncSetAttribute((const void*)setup_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipError_t e = hipFuncSetAttribute((const void*)setup_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(setup_kernel, dim3(ch.count), dim3(kSetupB), lds, s, b, w, ch, o2);
+  hipLaunchKernelGGL(setup_kernel<false>, dim3(ch.count), dim3(kSetupB), lds, s, b, w, ch, o2, (const int32_t*)nullptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_setup_medium(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n,
+                               const int32_t* list, int nlist, hipStream_t s) {
+  Opts o2 = o;
+  o2.setup_segments = setup_segments(max_n);
+  const size_t lds = align16(sizeof(int32_t) * (size_t)o2.setup_segments * ((size_t)max_n + 1));
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  hipError_t e = hipFuncSetAttribute((const void*)setup_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(setup_kernel<true>, dim3(nlist), dim3(kSetupB), lds, s, b, w, ch, o2, list);
   return hipGetLastError();
 }
 

@@ -78,6 +78,7 @@ SYMBOLS = {
     "dvh_last_stats": (ctypes.c_int, [ctypes.c_void_p, c_int32_p]),
     "dvh_last_path_counts": (ctypes.c_int, [ctypes.c_void_p, c_int32_p]),
     "dvh_last_path_counts4": (ctypes.c_int, [ctypes.c_void_p, c_int32_p]),
+    "dvh_last_path_counts5": (ctypes.c_int, [ctypes.c_void_p, c_int32_p]),
     "dvh_set_kernel_path": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "dvh_outage_coverage": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(OutageCase), ctypes.c_int32, c_int32_p,
                                            c_double_p]),

@@ -146,8 +146,10 @@ def sweep_features(P):
     return np.stack([np.log(P["E"] / P["load_scale"]), P["duration"], P["pv_rated"] / P["load_scale"]], axis=1)
 
 
-def config4(scenarios):
-    """Synthetic sweep windows for the given scenario ids (12 monthly windows each)."""
+def config4(scenarios, n="month", dt=1.0):
+    """Synthetic sweep windows for the given scenario ids (12 monthly windows each).  n: the optimisation window
+    (Model_Parameters_Template_DER.csv:8 `n`: "month", "year" or a step count); dt < 1: sub-hourly steps, the hourly
+    series held constant within each hour (Model_Parameters_Template_DER.csv:4 `dt`)."""
     from scipy.signal import lfilter
     ri = reference_inputs()
     P = sweep_parameters(scenarios)
@@ -160,7 +162,10 @@ def config4(scenarios):
     E = P["E"]
     bat = dict(E=E, Pch=E / P["duration"], Pdis=E / P["duration"], rte=P["rte"], sdr=0.0, soc_target=1.0,
                ulsoc=1.0, llsoc=0.0, fixedOM=10.0, OMexpenses=0.0, hp=0.0)
-    return windows_by_period(2017, 1.0, load, gen, bat, tariff_def=tariff(), demand_price_override=P["demand"],
+    rep = int(round(1.0 / dt))
+    if rep > 1:
+        load, gen = np.repeat(load, rep, axis=1), np.repeat(gen, rep, axis=1)
+    return windows_by_period(2017, dt, load, gen, bat, tariff_def=tariff(), n=n, demand_price_override=P["demand"],
                              price_scale=P["price_scale"], tags_prefix=list(scenarios))
 
 

@@ -91,6 +91,14 @@ class PackedBatch:
                     l=self.l[on:on + n], u=self.u[on:on + n], q=self.q[om:om + m], c0=float(self.c0[k]),
                     x=None if self.x is None else self.x[on:on + n], y=None if self.y is None else self.y[om:om + m])
 
+    def window_lp(self, k):
+        """Window k as a solver.WindowLP (host copies)."""
+        from .solver import WindowLP
+        w = self.window(k)
+        ip = np.asarray(w["indptr"], np.int32)
+        return WindowLP(ip - ip[0], np.array(w["indices"], np.int32), np.array(w["data"]), np.array(w["c"]),
+                        np.array(w["q"]), np.array(w["l"]), np.array(w["u"]), w["m_eq"], w["c0"])
+
 
 def pack(lps):
     """Concatenate a list of solver.WindowLP into a numpy PackedBatch."""

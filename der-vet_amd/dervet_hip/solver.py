@@ -143,10 +143,10 @@ class BatchSolver:
     def kernel_stats(self):
         v = (ctypes.c_int32 * 4)()
         self._check(self._lib.dvh_last_stats(self._h, v), "dvh_last_stats")
-        c = (ctypes.c_int32 * 4)()
-        self._check(self._lib.dvh_last_path_counts4(self._h, c), "dvh_last_path_counts4")
+        c = (ctypes.c_int32 * 5)()
+        self._check(self._lib.dvh_last_path_counts5(self._h, c), "dvh_last_path_counts5")
         return {"band_windows": c[3], "ell_windows": v[0], "generic_windows": v[1], "variant": v[2],
-                "generic_only": bool(v[3]), "large_windows": c[2]}
+                "generic_only": bool(v[3]), "large_windows": c[2], "chain_windows": c[4]}
 
     _PATHS = {"default": 0, "generic": 1, "ell": 2}
 

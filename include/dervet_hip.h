@@ -166,6 +166,10 @@ int dvh_last_path_counts(const dvh_handle* h, int32_t* out3);
 /* The same plus the battery-banded kernel: out4 = {ELL kernel, generic CSR kernel, grid-wide large-LP path,
  * battery-banded kernel (windows with the storagevet battery + DCM structure, detected on the device)}. */
 int dvh_last_path_counts4(const dvh_handle* h, int32_t* out4);
+/* The same plus the medium tier: out5 = {ELL, generic, grid-wide, battery-banded, medium tier (battery windows of
+ * 769 .. 12,288 steps -- the annual hourly window n = "year", sub-hourly monthly windows -- solved as a batch, a
+ * team of one workgroup per <= 768-step segment per window, dvh_chain.hip)}. */
+int dvh_last_path_counts5(const dvh_handle* h, int32_t* out5);
 /* ---- Post-facto reliability sweep.
  * Replaces Reliability.load_coverage_probability (dervet/MicrogridValueStreams/Reliability.py:876-967) and the
  * serial recursion it drives (data_process :447-487, simulate_outage :489-570): for every case, an outage is

@@ -375,6 +375,10 @@ int dvh_last_path_counts4(const dvh_handle*, int32_t* out4) {
   if (out4) std::memset(out4, 0, 4 * sizeof(int32_t));
   return DVH_OK;
 }
+int dvh_last_path_counts5(const dvh_handle*, int32_t* out5) {
+  if (out5) std::memset(out5, 0, 5 * sizeof(int32_t));
+  return DVH_OK;
+}
 int dvh_set_kernel_path(dvh_handle*, int) { return DVH_OK; }
 int dvh_outage_coverage(dvh_handle*, const dvh_outage_case*, int32_t, int32_t*, double*) { return DVH_ERR_UNSUPPORTED; }
 int dvh_outage_min_soe(dvh_handle*, const dvh_outage_case*, int32_t, const int32_t*, double*) {

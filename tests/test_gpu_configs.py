@@ -228,9 +228,10 @@ def test_config3_annual_5min_window_large_path(gpu_solver):
     _check(lps, res, "config3")
 
 
-def test_large_path_with_dcm_columns_in_mixed_batch(gpu_solver):
-    """An annual hourly window with 12 monthly DCM tau columns (long columns -> own workgroups) batched
-    together with monthly windows: each goes to its path, all match HiGHS."""
+def test_large_path_with_dcm_columns_in_mixed_batch():
+    """An annual hourly window with 12 monthly DCM tau columns batched together with monthly windows: each goes to
+    its path -- the medium tier (dvh_chain.hip) by default, the grid-wide large-LP path when the band kernels are off
+    -- and all match HiGHS."""
     ri = scenarios.reference_inputs()
     load = ri["multi_der_site_load"][None, :]
     gen = 1000.0 * np.nan_to_num(ri["multi_der_pv_profile"])[None, :]
@@ -238,10 +239,16 @@ def test_large_path_with_dcm_columns_in_mixed_batch(gpu_solver):
                                          n="year")
     lps = _lps(scenarios.config4([3])[:2]) + _lps(annual) + _lps(scenarios.config4([4])[:1])
     assert lps[2].n == 3 * 8760 + 12
-    res = gpu_solver.solve(lps)
-    ks = gpu_solver.kernel_stats()
-    assert ks["large_windows"] == 1 and ks["band_windows"] == 3
-    _check(lps, res, "mixed")
+    with BatchSolver(0) as s:
+        res = s.solve(lps)
+        ks = s.kernel_stats()
+        assert ks["chain_windows"] == 1 and ks["band_windows"] == 3 and ks["large_windows"] == 0, ks
+        _check(lps, res, "mixed")
+        s.set_kernel_path("ell")
+        res = s.solve(lps)
+        ks = s.kernel_stats()
+        assert ks["large_windows"] == 1 and ks["ell_windows"] == 3, ks
+        _check(lps, res, "mixed-large")
 
 
 def test_warm_start_from_own_solution_and_neighbour():
