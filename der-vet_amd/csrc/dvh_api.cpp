@@ -474,13 +474,14 @@ static int chain_pass(dvh_handle* h, const dvh::Batch& b, const dvh::Work& w, co
     (void)hipGetLastError();
     h->chain_cap = cap;
   }
-  const int NT = std::min((int)pos.size(), h->chain_cap / std::max(PT, 1));
+  const int S = h->chain_cap / 8;  // resident slots per XCD
+  const int NT = S >= PT ? dvh::chain_team_count(S, PT) : 0;
   if (NT < 1) return DVH_OK;  // cannot keep a team resident: the grid-wide path takes them
   DVH_HIP(h, h->m_pos.ensure(I * pos.size()));
   DVH_HIP(h, hipMemcpyAsync(h->m_pos.p, pos.data(), I * pos.size(), hipMemcpyHostToDevice, s));
   DVH_HIP(h, h->m_xbuf.ensure(dvh::chain_xbuf_bytes(NT, PT)));
-  DVH_HIP(h, h->m_abort.ensure(dvh::chain_abort_bytes(NT, PT)));
-  e = dvh::launch_chain(b, w, ch, o, h->m_pos.as<int32_t>(), (int)pos.size(), h->m_plan.as<int32_t>(), PT, NT,
+  DVH_HIP(h, h->m_abort.ensure(dvh::chain_abort_bytes(S)));
+  e = dvh::launch_chain(b, w, ch, o, h->m_pos.as<int32_t>(), (int)pos.size(), h->m_plan.as<int32_t>(), PT, S,
                         h->m_xbuf.p, h->m_abort.as<int32_t>(), s);
   if (e == hipErrorCooperativeLaunchTooLarge) {  // not resident after all: leave them to the grid-wide path
     (void)hipGetLastError();
@@ -488,17 +489,17 @@ static int chain_pass(dvh_handle* h, const dvh::Batch& b, const dvh::Work& w, co
     return DVH_OK;
   }
   if (e != hipSuccess) return hip_fail(h, e, "launch_chain");
-  std::vector<int32_t> ab(dvh::chain_abort_bytes(NT, PT) / I);
+  std::vector<int32_t> ab(dvh::chain_abort_bytes(S) / I);
   DVH_HIP(h, hipMemcpyAsync(ab.data(), h->m_abort.p, I * ab.size(), hipMemcpyDeviceToHost, s));
   DVH_HIP(h, hipStreamSynchronize(s));
   if (ab[0] != 0) {
     std::string msg = "medium tier: a segment exchange timed out (PT " + std::to_string(PT) + ", NT " +
-                      std::to_string(NT) + "); workgroups {team.segment: state list round entry tag seen}:";
-    for (int g = 0; g < NT * PT; ++g) {
+                      std::to_string(NT) + "); workgroups {block: state list round entry tag seen}:";
+    for (int g = 0; g < 8 * S; ++g) {
       const int32_t* d = &ab[16 + 8 * (size_t)g];
       if (d[0] == 0) continue;
       char buf[128];
-      snprintf(buf, sizeof buf, " %d.%d: %d %d %d 0x%x 0x%x 0x%x;", g / PT, g % PT, d[0], d[1], d[2], d[3], d[4], d[5]);
+      snprintf(buf, sizeof buf, " %d: %d %d %d 0x%x 0x%x 0x%x;", g, d[0], d[1], d[2], d[3], d[4], d[5]);
       msg += buf;
     }
     return fail(h, DVH_ERR_HIP, msg);

@@ -5,13 +5,21 @@
 // A window is cut into P <= kPMax segments of <= 768 consecutive time steps; each segment is one 768-thread
 // workgroup that runs the battery-banded PDHG of dvh_band.hip on its steps (lane = step, every coefficient and
 // iterate in VGPRs), and the P workgroups of a window form a team that advances in lock step.  What couples the
-// segments each iteration:
-//   * the SOE chain: the first step of segment s needs the dual of the SOE row of the step before it (owned by
-//     s-1) in its primal half-step, and that row needs the reflected primal of s's first ene in its dual half-step
-//     -- one 8-byte value each way;
+// segments each iteration (teams are formed from workgroups that share an XCD where the grid allows: one L2 for
+// the hand-offs; windows are handed out dynamically, one atomic per window, so a slow window does not idle the
+// rest of the chip):
+//   * the SOE chain: the SOE row of the last step of segment s-1 (the boundary row) couples that step's ch, dis,
+//     ene with the first ene of segment s.  Segment s-1 owns the row; segment s keeps a ghost copy (wave 0, the
+//     last lane) and repeats its dual update with the same operands in the same order, so the copies are
+//     bit-identical and s never needs the row's dual from s-1.  After each primal half-step, s-1 sends the
+//     reflected ch, dis, ene of its last step up and s sends the reflected first ene down: ONE exchange per
+//     iteration, both directions at once;
 //   * DCM demand columns (tau) whose rows lie in several segments: every segment holding rows of a tau column
-//     publishes its partial K'y sum for it, and every such segment performs the column's update redundantly from
-//     the partials summed in segment order, so all copies are bit-identical;
+//     publishes its partial K'y sum for it at the start of the primal half-step and collects the others' after
+//     its own primal work (the column's x-bar is needed only in the dual half-step, so this hop overlaps the
+//     other); every such segment performs the column's update redundantly from the partials summed in segment
+//     order, so all copies are bit-identical.  The plan cuts segments at demand-period boundaries where it can
+//     (the annual window's months are segments of their own), so most windows share no column;
 //   * the restart / termination checks (every check_every iterations): per-segment partial sums, added in segment
 //     order by every segment, so every segment takes the same decision.
 // The hand-offs are 8-byte {tag, 32-bit half} granules written by one relaxed agent-scope atomic store and polled
@@ -33,16 +41,18 @@ namespace {
 
 constexpr int kCB = kChainB;  // threads (and maximum steps) per segment
 constexpr int kJSeg = 4;      // tau columns per segment
-constexpr int kXSeg = 96;     // granules per segment in the exchange buffer
+constexpr int kXSeg = 100;    // granules per segment in the exchange buffer
 // granule offsets inside a segment's area (p = round parity)
-constexpr int kOffA1 = 0;     // + 2p: dual of the segment's last SOE row
-constexpr int kOffB = 4;      // + 2p: reflected primal of the segment's first ene
-constexpr int kOffA2 = 8;     // + 8p + 2u: partial K'y of tau slot u
-constexpr int kOffK = 24;     // + 12p: KKT images {last row dual, first ene, 4 tau partials}
-constexpr int kOffC = 48;     // + 20p + 2v: check partial sums
-// poll-list entries per segment: A list at [0, 256), K list at [256, 512), C list at [512, 1020), B at [1020, 1022)
+constexpr int kOffD = 0;      // + 2p: reflected first ene (down, to s-1)
+constexpr int kOffU = 4;      // + 6p: reflected ch, dis, ene of the last step (up, to s+1)
+constexpr int kOffA2 = 16;    // + 8p + 2u: partial K'y of tau slot u
+constexpr int kOffK = 32;     // + 12p: KKT images {first ene, 4 tau partials}
+constexpr int kOffC = 56;     // + 20p + 2v: check partial sums
+constexpr int kOffW = 96;     // + p: the team's next window (segment 0's area)
+constexpr int kOffAck = 98;   // + p: this segment has read it
+// poll-list entries per segment: A [0, 256), K [256, 512), C [512, 1016), up [1016, 1022), down [1022, 1024)
 constexpr int kPollMax = 1024;
-constexpr int kPollK = 256, kPollC = 512, kPollB = 1020;
+constexpr int kPollK = 256, kPollC = 512, kPollU = 1016, kPollD = 1022;
 constexpr unsigned kSpinMax = 1u << 22;
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
@@ -79,12 +89,13 @@ __device__ __forceinline__ void put_f64(gu64* g, unsigned tag, double v) {
   __hip_atomic_store(g + 1, t | (unsigned)__double2loint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// LDS layout (doubles): XE[B+1] YS[B+1] XT[4] XK[4] red[kNRed(NW+1)+4] TP[4][B] XP[3][B] YP[2][B] CR[kPMax][kNRed]
+// LDS layout (doubles): XE[B+1] YS[B+1] XT[4] XK[4] GK[4] red[kNRed(NW+1)+4] TP[4][B] XP[3][B] YP[2][B]
+//   CR[kPMax][kNRed]
 //   RO[6][B] (objective and upper bound of the lane's ch, dis, ene: read-only, kept out of VGPRs)
 //   | ints: poll offsets [kPollMax], poll values [kPollMax], misc[16]
 __host__ __device__ inline size_t chain_lds_doubles() {
   const int NW = kCB / kWave;
-  return 2 * (size_t)(kCB + 1) + 8 + (size_t)kNRed * (NW + 1) + 4 + (size_t)kJSeg * kCB + 5 * (size_t)kCB +
+  return 2 * (size_t)(kCB + 1) + 12 + (size_t)kNRed * (NW + 1) + 4 + (size_t)kJSeg * kCB + 5 * (size_t)kCB +
          (size_t)kPMax * kNRed + 6 * (size_t)kCB;
 }
 __host__ __device__ inline size_t chain_lds_bytes() {
@@ -94,8 +105,10 @@ __host__ __device__ inline size_t chain_lds_bytes() {
 // ---------------------------------------------------------------------------------------------------------------
 // Plan: one workgroup per listed window.  Verifies the battery + DCM pattern (as the band kernel), writes the
 // step -> DCM row / tau maps into the window's vbuf workspace, and cuts the steps into segments greedily: a new
-// segment starts when the current one holds kCB steps, or when a step brings a tau column the segment has no
-// slot left for.  plan[0] = P (0: not this tier; -1: already reported by the setup kernel).
+// segment starts when the current one holds kCB steps, when a step brings a tau column the segment has no slot
+// left for, or where a run of steps of one tau column begins that would not end inside the current segment but
+// fits in a segment of its own (so demand periods that fit are not split).  plan[0] = P (0: not this tier;
+// -1: already reported by the setup kernel).
 // ---------------------------------------------------------------------------------------------------------------
 constexpr int kPlanB = 1024;
 
@@ -103,6 +116,7 @@ __global__ __launch_bounds__(kPlanB) void chain_plan_kernel(const Batch b, const
                                                             const int32_t* list, int32_t* plan) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   int32_t* jl = reinterpret_cast<int32_t*>(smem);  // [T] tau id per step (-1: no DCM row)
+  int32_t* re = jl + kPMax * kCB;                   // [T] end of the run of equal tau ids through step t
   __shared__ int32_t jmask[kChainJMax];
   __shared__ int32_t set[kJSeg];
   __shared__ int flag;
@@ -193,13 +207,15 @@ __global__ __launch_bounds__(kPlanB) void chain_plan_kernel(const Batch b, const
   for (int t = tid; t < T; t += kPlanB) jl[t] = dm[T + t];
   __syncthreads();
   if (tid == 0) {
+    for (int t = T - 1; t >= 0; --t) re[t] = (t + 1 < T && jl[t + 1] == jl[t]) ? re[t + 1] : t + 1;
     int P = 0, s0 = 0, ns = 0, ok = 1;
     pl[4] = 0;
     for (int t = 0; t <= T && ok; ++t) {
       const int j = t < T ? jl[t] : -1;
       bool newj = j >= 0;
       for (int u = 0; u < ns && newj; ++u) newj = set[u] != j;
-      if (t == T || t - s0 == kCB || (newj && ns == kJSeg)) {  // close segment P = [s0, t)
+      const bool run_cut = t < T && t > s0 && jl[t] != jl[t - 1] && re[t] - s0 > kCB && re[t] - t <= kCB;
+      if (t == T || t - s0 == kCB || (newj && ns == kJSeg) || run_cut) {  // close segment P = [s0, t)
         for (int u = 0; u < kJSeg; ++u) {
           pl[24 + 4 * P + u] = u < ns ? set[u] : -1;
           if (u < ns) jmask[set[u]] |= 1 << P;
@@ -231,13 +247,33 @@ __global__ __launch_bounds__(kPlanB) void chain_plan_kernel(const Batch b, const
 // The team kernel.
 // ---------------------------------------------------------------------------------------------------------------
 struct ChainArgs {
-  const int32_t* pos;   // positions (into plan) of the windows to solve
+  const int32_t* pos;        // positions (into plan) of the windows to solve
   int npos;
   const int32_t* plan;
   unsigned long long* xbuf;  // NT * PT * kXSeg granules, zeroed before the launch
-  int* abort_word;           // zeroed before the launch; set on an expired spin
+  int* abort_word;           // zeroed before the launch (with the diagnostics); [0] abort, [8] next window
   int PT, NT;
+  int S;                     // workgroup slots per XCD (grid = 8 S)
 };
+
+// Team and segment of workgroup b: blocks b and b + 8 share an XCD (round-robin dispatch, MI355X_MICROARCH.md --
+// a speed assumption only, never a correctness one), so each XCD's first floor(S / PT) * PT slots form local
+// teams and the remaining slots of all XCDs are pooled into further teams.  team >= NT: idle.
+__host__ __device__ inline void chain_team_of(int b, int S, int PT, int* team, int* seg) {
+  const int xcd = b % 8, slot = b / 8, LT = S / PT, used = LT * PT;
+  if (slot < used) {
+    *team = xcd * LT + slot / PT;
+    *seg = slot % PT;
+  } else {
+    const int li = (slot - used) * 8 + xcd;
+    *team = 8 * LT + li / PT;
+    *seg = li % PT;
+  }
+}
+__host__ __device__ inline int chain_teams(int S, int PT) {
+  const int LT = S / PT;
+  return 8 * LT + (8 * (S - LT * PT)) / PT;
+}
 
 __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const Work w, const Chunk ch,
                                                            const Opts o, const ChainArgs a) {
@@ -245,13 +281,16 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
   constexpr int NW = B / kWave;
   constexpr int NC = 3, NR = 2;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int team = blockIdx.x / a.PT, seg = blockIdx.x % a.PT;
+  int team, seg;
+  chain_team_of((int)blockIdx.x, a.S, a.PT, &team, &seg);
+  if (team >= a.NT) return;
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   double* XE = reinterpret_cast<double*>(smem);  // x-bar of ene of the lane's step; [L] = next segment's first
-  double* YS = XE + (B + 1);                     // y of row t0 + i; [0] = init row (segment 0) or the halo
+  double* YS = XE + (B + 1);                     // y of row t0 + i; [0] = init row (segment 0) or the ghost row
   double* XT = YS + (B + 1);                     // x-bar of the tau slots
   double* XK = XT + kJSeg;                       // tau K'y totals of the KKT images
-  double* red = XK + kJSeg;
+  double* GK = XK + kJSeg;                       // ghost row coefficients: ch, dis, ene of step t0 - 1, ene_t0
+  double* red = GK + 4;
   double* TP = red + kNRed * (NW + 1) + 4;       // [kJSeg][B] per-lane partial K'y of the tau slots
   double* XP = TP + kJSeg * B;                   // [3][B] T(z) of the lane's columns (check iterations)
   double* YP = XP + NC * B;                      // [2][B] T(z) of the lane's rows
@@ -259,7 +298,7 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
   double* RO = CR + kPMax * kNRed;               // [6][B]: c of ch, dis, ene; upper bound of ch, dis, ene
   int32_t* poff = reinterpret_cast<int32_t*>(smem + align16(sizeof(double) * chain_lds_doubles()));
   unsigned* pval = reinterpret_cast<unsigned*>(poff + kPollMax);
-  // misc: [0] dead flag, [1] A entries, [2] K entries, [3] tau-partial start in A, [4] in K,
+  // misc: [0] dead flag, [1] A entries, [2] K entries, [4] tau-image start in K,
   //       [8 + u] offset of slot u's partials relative to the tau start, [12 + u] share mask of slot u
   int32_t* misc = poff + 2 * kPollMax;
   gu64* tb = (gu64*)a.xbuf + (int64_t)team * a.PT * kXSeg;  // the team's exchange area
@@ -268,9 +307,67 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
 
   if (tid == 0) misc[0] = 0;
   __syncthreads();
-  int wseq = 0;
-  for (int wi = team; wi < a.npos; wi += a.NT) {
-    ++wseq;
+  for (int wseq = 1;; ++wseq) {
+    // ---- the team's next window: segment 0 takes it from the launch-wide counter (after every segment has read
+    //      the previous hand-out) and hands it to the others; every segment acknowledges
+    if (wid == 0) {
+      auto poll1 = [&](int e0, int cnt, unsigned tag) -> bool {  // cnt <= 64 one-granule entries (C list area)
+        const bool act = lane < cnt;
+        gu64* p = tb + (act ? poff[e0 + lane] : 0);
+        bool ok = !act;
+        unsigned spins = 0;
+        while (!__all(ok)) {
+          if (!ok) {
+            const unsigned long long xv = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((unsigned)(xv >> 32) == tag) {
+              ok = true;
+              pval[e0 + lane] = (unsigned)xv;
+            }
+          }
+          if ((++spins & 1023u) == 0 &&
+              (spins > kSpinMax || __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+            if (lane == 0) {
+              __hip_atomic_store(abort_word + 16 + 8 * (int)blockIdx.x, spins > kSpinMax ? 3 : 2, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+              __hip_atomic_store(abort_word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            return false;
+          }
+        }
+        return true;
+      };
+      const unsigned wtag = chain_tag(wseq, 0x3FFFF);  // round field all ones: no exchange round reaches it
+      const int par = wseq & 1;
+      bool ok = true;
+      int wi = 0;
+      if (seg == 0) {
+        if (wseq > 1 && a.PT > 1) {  // acknowledgements of the previous hand-out
+          if (lane < a.PT - 1) poff[kPollC + lane] = (lane + 1) * kXSeg + kOffAck + (par ^ 1);
+          __builtin_amdgcn_wave_barrier();
+          ok = poll1(kPollC, a.PT - 1, chain_tag(wseq - 1, 0x3FFFF));
+        }
+        if (lane == 0) wi = __hip_atomic_fetch_add(abort_word + 8, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        wi = __builtin_amdgcn_readfirstlane(wi);
+        if (ok && lane == 0)
+          __hip_atomic_store(tb + kOffW + par, ((unsigned long long)wtag << 32) | (unsigned)wi, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        if (lane == 0) poff[kPollC] = kOffW + par;
+        __builtin_amdgcn_wave_barrier();
+        ok = poll1(kPollC, 1, wtag);
+        wi = (int)pval[kPollC];
+        if (ok && lane == 0)
+          __hip_atomic_store(mine + kOffAck + par, ((unsigned long long)wtag << 32), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (lane == 0) {
+        misc[5] = wi;
+        if (!ok) misc[0] = 1;
+      }
+    }
+    __syncthreads();
+    const int wi = misc[5];
+    if (misc[0] || wi >= a.npos) break;
     const int32_t* pl = a.plan + (int64_t)a.pos[wi] * kPlanInts;
     const int P = pl[0];
     if (seg >= P) continue;
@@ -297,27 +394,21 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
     const int32_t* dm = reinterpret_cast<const int32_t*>(w.vbuf + W.wn);
     double* xo_g = b.x + W.on;
     double* yo_g = b.y + W.om;
-    int cA = 0, cB = 0, cK = 0, cC = 0;  // rounds of each exchange kind (identical in every segment)
+    int cA = 0, cB = 0, cK = 0, cC = 0;  // rounds of each exchange kind (identical in every segment and wave)
 
-    // ---- poll lists (offset at parity 0 in the low 16 bits, parity stride above): A = {halo dual from s-1, tau
-    //      partials of the other segments sharing a slot}; K = {halo dual image from s-1, first-ene image from
-    //      s+1, tau image partials}; partials ordered by (slot, segment)
+    // ---- poll lists (offset at parity 0 in the low 16 bits, parity stride above): A = the tau partials of the
+    //      other segments sharing a slot (by slot, then segment); K = {first-ene image from s+1} + tau image
+    //      partials; up = ch, dis, ene of s-1's last step; down = s+1's first ene
     if (tid == 0) {
-      int e = 0;
-      if (!first) {
-        poff[e++] = ((seg - 1) * kXSeg + kOffA1) | (2 << 16);
-        poff[e++] = ((seg - 1) * kXSeg + kOffA1 + 1) | (2 << 16);
-      }
-      misc[3] = e;
-      int ek = kPollK;
-      if (!first) {
-        poff[ek++] = ((seg - 1) * kXSeg + kOffK) | (12 << 16);
-        poff[ek++] = ((seg - 1) * kXSeg + kOffK + 1) | (12 << 16);
-      }
+      int e = 0, ek = kPollK;
       if (!last) {
-        poff[ek++] = ((seg + 1) * kXSeg + kOffK + 2) | (12 << 16);
-        poff[ek++] = ((seg + 1) * kXSeg + kOffK + 3) | (12 << 16);
+        poff[ek++] = ((seg + 1) * kXSeg + kOffK) | (12 << 16);
+        poff[ek++] = ((seg + 1) * kXSeg + kOffK + 1) | (12 << 16);
+        poff[kPollD] = ((seg + 1) * kXSeg + kOffD) | (2 << 16);
+        poff[kPollD + 1] = ((seg + 1) * kXSeg + kOffD + 1) | (2 << 16);
       }
+      if (!first)
+        for (int g = 0; g < 6; ++g) poff[kPollU + g] = ((seg - 1) * kXSeg + kOffU + g) | (6 << 16);
       misc[4] = ek - kPollK;
       int rel = 0;
       for (int u = 0; u < nsl; ++u) {
@@ -330,8 +421,8 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
           while (ur < kJSeg - 1 && pl[24 + 4 * r + ur] != id) ++ur;
           poff[e++] = (r * kXSeg + kOffA2 + 2 * ur) | (8 << 16);
           poff[e++] = (r * kXSeg + kOffA2 + 2 * ur + 1) | (8 << 16);
-          poff[ek++] = (r * kXSeg + kOffK + 4 + 2 * ur) | (12 << 16);
-          poff[ek++] = (r * kXSeg + kOffK + 5 + 2 * ur) | (12 << 16);
+          poff[ek++] = (r * kXSeg + kOffK + 2 + 2 * ur) | (12 << 16);
+          poff[ek++] = (r * kXSeg + kOffK + 3 + 2 * ur) | (12 << 16);
           rel += 2;
         }
       }
@@ -339,7 +430,7 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
       misc[2] = ek - kPollK;
     }
     __syncthreads();
-    const int nA = misc[1], nK = misc[2], aTau = misc[3], kTau = misc[4];
+    const int nA = misc[1], nK = misc[2], kTau = misc[4];
 
     // polls entries [e0, e0 + cnt) for round c (tag, parity); the 32-bit halves land in pval[e0 ..]; false: the
     // spin expired or another workgroup aborted (the abort word is then set)
@@ -412,7 +503,7 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
     double loe = 0.0;
     double ks[4] = {0.0, 0.0, 0.0, 0.0};  // SOE row of step t: ch_t, dis_t, ene_t, ene_{t+1}
     double kd[3] = {0.0, 0.0, 0.0};       // DCM row of step t: ch_t, dis_t, tau
-    double kp = 0.0;                      // ene_t in row t (init row or the previous step's SOE row)
+    double kp = 0.0;                      // ene_t in row t (init row, or the previous step's SOE row)
     double y[NR], ya[NR], q[2];
     int drow = -1, jt = 0;
 #pragma unroll
@@ -471,11 +562,12 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
       }
     }
     const int xta = lds_addr(XT + jt);
-    // wave 0 special lanes: u < nsl the tau slots {x, xa, c, lo, hi, x+}; kInitLane (segment 0) the init row
-    // {y, ya, y+, q, coefficient, -}
-    constexpr int kInitLane = kWave - 1;
-    static_assert(kJSeg < kInitLane, "tau lanes and the init-row lane are distinct");
-    const bool tlane = wid == 0 && lane < nsl, ilane = first && wid == 0 && lane == kInitLane;
+    // wave 0 special lanes: u < nsl the tau slots {x, xa, c, lo, hi, x+}; the last lane the row of YS[0]: the
+    // init row (segment 0: {y, ya, y+, q, coefficient}) or the ghost boundary row ({y, ya, y+, q}, GK)
+    constexpr int kRowLane = kWave - 1;
+    static_assert(kJSeg < kRowLane, "tau lanes and the row lane are distinct");
+    const bool tlane = wid == 0 && lane < nsl, rlane = wid == 0 && lane == kRowLane;
+    const bool ilane = rlane && first, glane = rlane && !first;
     int jg0 = 0;
     bool town = false;  // this segment owns the slot (the lowest segment holding its rows): KKT / norm terms
     if (tlane) {
@@ -495,6 +587,21 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
       sp[3] = qs[0];
       sp[4] = gkv[gkp[0]];
       if (o.warm) sp[0] = sp[1] = sp[2] = yo_g[0] / drv[0];
+    }
+    if (glane) {  // row t0 = SOE row of step t0 - 1 (owned by segment s - 1)
+      double g4[4] = {0.0, 0.0, 0.0, 0.0};
+      for (int p = gkp[t0]; p < gkp[t0 + 1]; ++p) {
+        const int c = gkc[p];
+        const double av = gkv[p];
+        if (c == t0 - 1) g4[0] = av;
+        else if (c == T + t0 - 1) g4[1] = av;
+        else if (c == 2 * T + t0 - 1) g4[2] = av;
+        else g4[3] = av;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) GK[u] = g4[u];
+      sp[3] = qs[t0];
+      if (o.warm) sp[0] = sp[1] = yo_g[t0] / drv[t0];
     }
     if (tid < kJSeg) XT[tid] = XK[tid] = 0.0;
     if (tid == 0) XE[B] = YS[B] = 0.0;
@@ -520,6 +627,11 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
       os[0] = fma(ks[3], vnext, os[0]);
       os[1] = fma(kd[2], lds_ld(xta), os[1]);
     };
+    // the ghost row's K v from s-1's last step (polled, up) and v of ene_t0: the owner's kown + kfin, same order
+    auto kghost = [&]() -> double {
+      const double v0 = pv64(kPollU), v1 = pv64(kPollU + 2), v2 = pv64(kPollU + 4);
+      return fma(GK[3], XE[0], fma(GK[2], v2, fma(GK[1], v1, GK[0] * v0)));
+    };
     auto tau_parts = [&](double vd) {
       if (nsl == 1) {
         TP[tid] = kd[2] * vd;
@@ -539,41 +651,45 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
       }
       return res;
     };
-    // wave 0, start of a primal phase (after every wave advanced cA): publish this segment's tau partials (round
-    // cA), poll round cA (the halo dual of s-1 -> YS[0], the sharers' partials); returns the tau totals in lanes
-    // u < nsl; false in ok: abort
-    auto round_a = [&](bool& ok) -> double {
-      const unsigned tag = chain_tag(wseq, cA);
-      const double own = tau_own();
-      if (lane < nsl) put_f64(mine + kOffA2 + 8 * (cA & 1) + 2 * lane, tag, own);
+    // wave 0: publish this segment's tau partials for round cA (before its primal work) ...
+    auto publish_a = [&](double own) {
+      if (lane < nsl) put_f64(mine + kOffA2 + 8 * (cA & 1) + 2 * lane, chain_tag(wseq, cA), own);
+    };
+    // ... and, after it, collect the sharers' and return the totals (lanes u < nsl); false in ok: abort
+    auto collect_a = [&](double own, bool& ok) -> double {
       if (!poll(0, nA, cA)) {
         ok = false;
         return 0.0;
       }
-      if (!first && lane == 0) YS[0] = pv64(0);
       double tot = 0.0;
       for (int u = 0; u < nsl; ++u) {
-        const double tu = tau_total(u, readlane_f64(own, u), aTau);
+        const double tu = tau_total(u, readlane_f64(own, u), 0);
         if (lane == u) tot = tu;
       }
       return tot;
     };
-    auto publish_a1 = [&](double ylast) {  // lane L-1: dual of the last SOE row for s+1 (round cA + 1)
-      if (!last && tid == L - 1) put_f64(mine + kOffA1 + 2 * ((cA + 1) & 1), chain_tag(wseq, cA + 1), ylast);
-    };
-    auto publish_b = [&](double xe0) {  // lane 0: reflected first ene for s-1 (round cB)
-      if (!first && tid == 0) put_f64(mine + kOffB + 2 * (cB & 1), chain_tag(wseq, cB), xe0);
-    };
-    auto poll_b = [&]() -> bool {  // wave wl: the next segment's first ene (round cB) -> XE[L]
-      if (last) return true;
-      if (lane == 0) {
-        poff[kPollB] = ((seg + 1) * kXSeg + kOffB) | (2 << 16);
-        poff[kPollB + 1] = ((seg + 1) * kXSeg + kOffB + 1) | (2 << 16);
+    // after the primal half-step: the first ene goes down (lane 0), the last step's ch, dis, ene go up (lane L-1)
+    auto publish_b = [&](const double (&v)[NC]) {
+      const unsigned tag = chain_tag(wseq, cB);
+      if (!first && tid == 0) put_f64(mine + kOffD + 2 * (cB & 1), tag, v[2]);
+      if (!last && tid == L - 1) {
+        gu64* g = mine + kOffU + 6 * (cB & 1);
+        put_f64(g, tag, v[0]);
+        put_f64(g + 2, tag, v[1]);
+        put_f64(g + 4, tag, v[2]);
       }
-      __builtin_amdgcn_wave_barrier();
-      if (!poll(kPollB, 2, cB)) return false;
-      if (lane == 0) XE[L] = pv64(kPollB);
-      return true;
+    };
+    // before the dual half-step: wave wl takes the next segment's first ene into XE[L]; wave 0 the previous
+    // segment's last step (for the ghost row, in pval[kPollU ..]).  Sets the dead flag on an abort.
+    auto poll_b = [&]() {
+      if (!last && wid == wl) {
+        if (poll(kPollD, 2, cB)) {
+          if (lane == 0) XE[L] = pv64(kPollD);
+        } else if (lane == 0) {
+          misc[0] = 1;
+        }
+      }
+      if (!first && wid == 0 && !poll(kPollU, 6, cB) && lane == 0) misc[0] = 1;
     };
     // check reduction: this segment's NV partials (identical in every lane on entry) -> the sums over all segments
     // in segment order, in every lane; false: abort
@@ -630,15 +746,16 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
       double wr[NR] = {0.0, 0.0};
       for (int pi = 0; pi <= PI; ++pi) {
         if (pi > 0) {
-          double kt = 0.0;
-          ++cA;  // every wave: publish_a1 (wave wl) names the next round by it
+          ++cA;
           if (wid == 0) {
+            const double own = tau_own();
+            publish_a(own);
             bool ok = true;
-            kt = round_a(ok);
+            const double kt = collect_a(own, ok);
             if (!ok && lane == 0) misc[0] = 1;
+            if (tlane) vtau = kt;
           }
           ktr(wr, YS[tid], vc);
-          if (tlane) vtau = kt;
         }
         if (pi >= PI - 1) {
           double s = town ? vtau * vtau : 0.0;
@@ -650,18 +767,18 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
         XE[tid] = vc[2];
         if (tlane) XT[lane] = vtau;
         ++cB;
-        publish_b(vc[2]);
+        publish_b(vc);
         lds_barrier();
         if (misc[0]) {
           alive = false;
           break;
         }
-        if (wid == wl && !poll_b() && lane == 0) misc[0] = 1;
+        poll_b();
         kown(vc, wr);
         kfin(wr, XE[tid + 1]);
         YS[tid + 1] = wr[0];
-        publish_a1(wr[0]);
         if (ilane) YS[0] = sp[4] * XE[0];
+        if (glane) YS[0] = kghost();
         if (nsl > 0) tau_parts(wr[1]);
         lds_barrier();
         if (misc[0]) {
@@ -684,11 +801,10 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
       __syncthreads();
     }
     if (!alive) break;
-    // y images of the starting point (YS, TP), and the halo dual for the first primal phase
+    // y images of the starting point (YS, TP)
     if (val) YS[tid + 1] = y[0];
-    if (ilane) YS[0] = sp[0];
+    if (rlane) YS[0] = sp[0];
     if (nsl > 0) tau_parts(y[1]);
-    publish_a1(y[0]);
     __syncthreads();
 
     eta = uniform(eta);
@@ -718,14 +834,14 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
       }
       const double cb = readlane_f64(hw, kin - kbase), ca = 1.0 - cb;
       mv0 = mv1 = mv2 = mv3 = 0.0;
+      ++cA;
+      ++cB;
       // ---------------- primal half-step (reflected Halpern, rho = 1)
       {
-        double kt = 0.0;
-        ++cA;
+        double own = 0.0;
         if (wid == 0) {
-          bool ok = true;
-          kt = round_a(ok);
-          if (!ok && lane == 0) misc[0] = 1;
+          own = tau_own();
+          publish_a(own);
         }
         double kty[NC], xb[NC];
         ktr(y, YS[tid], kty);
@@ -743,29 +859,33 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
           x[v] = fma(ca, xb[v], cb * xa[v]);
         }
         XE[tid] = xb[2];
-        ++cB;
-        publish_b(xb[2]);
-        if (tlane) {
-          const double xo = sp[0], xan = sp[1];
-          const double p1 = vmin(vmax(fma(-tau, sp[2] - kt, xo), sp[3]), sp[4]);
-          const double xbt = fma(2.0, p1, -xo);
-          XT[lane] = xbt;
-          sp[0] = fma(ca, xbt, cb * xan);
-          if (CHECK) {
-            if (town) {
-              const double d = xo - p1, da = p1 - xan;
-              mv0 += d * d;
-              mv1 += da * da;
+        publish_b(xb);
+        kown(xb, kx);
+        if (wid == 0) {  // tau columns: the sharers' partials arrived while the wave did its own columns
+          bool ok = true;
+          const double kt = collect_a(own, ok);
+          if (!ok && lane == 0) misc[0] = 1;
+          if (tlane) {
+            const double xo = sp[0], xan = sp[1];
+            const double p1 = vmin(vmax(fma(-tau, sp[2] - kt, xo), sp[3]), sp[4]);
+            const double xbt = fma(2.0, p1, -xo);
+            XT[lane] = xbt;
+            sp[0] = fma(ca, xbt, cb * xan);
+            if (CHECK) {
+              if (town) {
+                const double d = xo - p1, da = p1 - xan;
+                mv0 += d * d;
+                mv1 += da * da;
+              }
+              sp[5] = p1;
             }
-            sp[5] = p1;
           }
         }
-        kown(xb, kx);
       }
       lds_barrier();
       // ---------------- dual half-step
       {
-        if (wid == wl && !poll_b() && lane == 0) misc[0] = 1;
+        poll_b();
         kfin(kx, XE[tid + 1]);
 #pragma unroll
         for (int r = 0; r < NR; ++r) {  // row 0 (SOE) is an equality; the DCM row is >=: its dual stays >= 0
@@ -780,15 +900,16 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
           y[r] = fma(ca, fma(2.0, p1, -y[r]), cb * ya[r]);
         }
         YS[tid + 1] = y[0];
-        if (!CHECK) publish_a1(y[0]);
         if (nsl > 0) tau_parts(y[1]);
-        if (ilane) {  // init row (segment 0): ene_0 = target
+        if (rlane) {  // init row (segment 0: ene_0 = target) or the ghost boundary row (counted by its owner)
           const double y0 = sp[0], ya0 = sp[1];
-          const double q1 = fma(sigma, sp[3] - sp[4] * XE[0], y0);
+          const double q1 = first ? fma(sigma, sp[3] - sp[4] * XE[0], y0) : fma(sigma, sp[3] - kghost(), y0);
           if (CHECK) {
-            const double d = y0 - q1, da = q1 - ya0;
-            mv2 += d * d;
-            mv3 += da * da;
+            if (first) {
+              const double d = y0 - q1, da = q1 - ya0;
+              mv2 += d * d;
+              mv3 += da * da;
+            }
             sp[2] = q1;
           }
           const double yn = fma(ca, fma(2.0, q1, -y0), cb * ya0);
@@ -823,7 +944,8 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
 #pragma unroll
       for (int u = 4; u < kNRed; ++u) acc[u] = 0.0;
       if (kkt) {
-        // images of T(z_k); the boundary images and the tau image totals come from the neighbours / sharers
+        // images of T(z_k); the next segment's first-ene image and the tau image totals come by exchange (the
+        // ghost row's image is local)
         double xp[NC], yp[NR];
 #pragma unroll
         for (int v = 0; v < NC; ++v) xp[v] = XP[v * B + tid];
@@ -831,7 +953,7 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
         for (int r = 0; r < NR; ++r) yp[r] = YP[r * B + tid];
         XE[tid] = xp[2];
         YS[tid + 1] = yp[0];
-        if (ilane) YS[0] = sp[2];
+        if (rlane) YS[0] = sp[2];
         if (tlane) XT[lane] = sp[5];
         if (nsl > 0) tau_parts(yp[1]);
         lds_barrier();
@@ -840,18 +962,12 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
           const unsigned tag = chain_tag(wseq, cK);
           gu64* g = mine + kOffK + 12 * (cK & 1);
           const double own = tau_own();
-          if (lane == 0 && !last) put_f64(g, tag, YS[L]);
-          if (lane == 1 && !first) put_f64(g + 2, tag, XE[0]);
-          if (lane < nsl) put_f64(g + 4 + 2 * lane, tag, own);
+          if (lane == 0 && !first) put_f64(g, tag, XE[0]);
+          if (lane < nsl) put_f64(g + 2 + 2 * lane, tag, own);
           if (!poll(kPollK, nK, cK)) {
             if (lane == 0) misc[0] = 1;
           } else {
-            int e = kPollK;
-            if (!first) {
-              if (lane == 0) YS[0] = pv64(e);
-              e += 2;
-            }
-            if (!last && lane == 0) XE[L] = pv64(e);
+            if (!last && lane == 0) XE[L] = pv64(kPollK);
             double tot = 0.0;
             for (int u = 0; u < nsl; ++u) {
               const double tu = tau_total(u, readlane_f64(own, u), kPollK + kTau);
@@ -928,7 +1044,7 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
         for (int v = 0; v < NC; ++v) x[v] = xa[v] = XP[v * B + tid];
 #pragma unroll
         for (int rr = 0; rr < NR; ++rr) y[rr] = ya[rr] = YP[rr * B + tid];
-        if (ilane) sp[0] = sp[1] = sp[2];
+        if (rlane) sp[0] = sp[1] = sp[2];
         if (tlane) sp[0] = sp[1] = sp[5];
         kin = 0;
         kbase = 0;
@@ -940,10 +1056,9 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
       }
       if (restart || kkt) {  // the y images must hold z again (after a restart z = T(z_k))
         YS[tid + 1] = y[0];
-        if (ilane) YS[0] = sp[0];
+        if (rlane) YS[0] = sp[0];
         if (nsl > 0) tau_parts(y[1]);
       }
-      publish_a1(y[0]);  // the halo dual for the next primal phase, after the check (restart included)
       lds_barrier();
     }
     if (misc[0]) break;
@@ -969,7 +1084,8 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
 
 hipError_t launch_chain_plan(const Batch& b, const Work& w, const Chunk& ch, const int32_t* list, int nlist,
                              int max_T, int32_t* plan, hipStream_t s) {
-  const size_t lds = sizeof(int32_t) * (size_t)std::max(max_T, 1);
+  (void)max_T;
+  const size_t lds = 2 * sizeof(int32_t) * (size_t)kPMax * kCB;  // tau ids and run ends
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   hipError_t e = hipFuncSetAttribute((const void*)chain_plan_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds);
@@ -992,26 +1108,29 @@ hipError_t chain_capacity(int device, int* blocks) {
   return hipSuccess;
 }
 
-size_t chain_abort_bytes(int NT, int PT) { return sizeof(int32_t) * (16 + 8 * (size_t)NT * PT); }
+size_t chain_abort_bytes(int S) { return sizeof(int32_t) * (16 + 64 * (size_t)S); }
 size_t chain_xbuf_bytes(int NT, int PT) { return sizeof(unsigned long long) * (size_t)NT * PT * kXSeg; }
 
+int chain_team_count(int S, int PT) { return chain_teams(S, PT); }
+
 hipError_t launch_chain(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, const int32_t* pos, int npos,
-                        const int32_t* plan, int PT, int NT, void* xbuf, int32_t* abort_word, hipStream_t s) {
+                        const int32_t* plan, int PT, int S, void* xbuf, int32_t* abort_word, hipStream_t s) {
+  const int NT = chain_teams(S, PT);
   const size_t lds = chain_lds_bytes();
   hipError_t e = hipFuncSetAttribute((const void*)pdhg_chain_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds);
   if (e != hipSuccess) return e;
   e = hipMemsetAsync(xbuf, 0, chain_xbuf_bytes(NT, PT), s);
   if (e != hipSuccess) return e;
-  e = hipMemsetAsync(abort_word, 0, chain_abort_bytes(NT, PT), s);
+  e = hipMemsetAsync(abort_word, 0, chain_abort_bytes(S), s);
   if (e != hipSuccess) return e;
-  ChainArgs a{pos, npos, plan, static_cast<unsigned long long*>(xbuf), abort_word, PT, NT};
+  ChainArgs a{pos, npos, plan, static_cast<unsigned long long*>(xbuf), abort_word, PT, NT, S};
   Batch bb = b;
   Work ww = w;
   Chunk cc = ch;
   Opts oo = o;
   void* args[] = {&bb, &ww, &cc, &oo, &a};
-  return hipLaunchCooperativeKernel((const void*)pdhg_chain_kernel, dim3(NT * PT), dim3(kCB), args, (unsigned)lds, s);
+  return hipLaunchCooperativeKernel((const void*)pdhg_chain_kernel, dim3(8 * S), dim3(kCB), args, (unsigned)lds, s);
 }
 
 }  // namespace dvh

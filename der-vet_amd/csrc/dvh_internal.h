@@ -107,9 +107,11 @@ hipError_t launch_chain_plan(const Batch& b, const Work& w, const Chunk& ch, con
                              int max_T, int32_t* plan, hipStream_t s);
 hipError_t chain_capacity(int device, int* blocks);
 size_t chain_xbuf_bytes(int NT, int PT);
-size_t chain_abort_bytes(int NT, int PT);  // abort word + per-workgroup diagnostics
+size_t chain_abort_bytes(int S);  // abort word, window counter, per-workgroup diagnostics (grid 8 S)
+// S: resident workgroup slots per XCD (grid = 8 S); teams of PT workgroups, chain_team_count(S, PT) of them
+int chain_team_count(int S, int PT);
 hipError_t launch_chain(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, const int32_t* pos, int npos,
-                        const int32_t* plan, int PT, int NT, void* xbuf, int32_t* abort_word, hipStream_t s);
+                        const int32_t* plan, int PT, int S, void* xbuf, int32_t* abort_word, hipStream_t s);
 // Power iteration for ||Kt||_2 of the listed windows (generic path; the ELL kernel does its own on chip).
 hipError_t launch_power(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, const int32_t* list, int nlist,
                         hipStream_t s);
