@@ -42,12 +42,14 @@ __host__ __device__ inline size_t band_lds_bytes(int B, bool ice) {
 }
 
 // KKT pieces of one column / one row (out of line: the KKT check runs every 128 iterations, and inlined it
-// would raise the whole kernel's register allocation)
+// would raise the whole kernel's register allocation).  d / dr: the column / row scaling, id / idr: their
+// reciprocals from the setup kernel (the unscaling is a multiplication, not a division)
 struct ColKkt {
   double rd2, cx, bt;
 };
-__device__ __noinline__ ColKkt col_kkt_fn(double kt, double cj, double loj, double hij, double xj, double d) {
-  const double rc = (cj - kt) / d;
+__device__ __noinline__ ColKkt col_kkt_fn(double kt, double cj, double loj, double hij, double xj, double d,
+                                          double id) {
+  const double rc = (cj - kt) * id;
   const bool fl = isfinite(loj), fh = isfinite(hij);
   const double lam = (fl && fh) ? rc : (fl ? fmax(rc, 0.0) : (fh ? fmin(rc, 0.0) : 0.0));
   const double rd = rc - lam;
@@ -56,8 +58,8 @@ __device__ __noinline__ ColKkt col_kkt_fn(double kt, double cj, double loj, doub
 struct RowKkt {
   double rp2, y2;
 };
-__device__ __noinline__ RowKkt row_kkt_fn(double kv, double qi, double yi, double dr, int ge) {
-  double r = (qi - kv) / dr;
+__device__ __noinline__ RowKkt row_kkt_fn(double kv, double qi, double yi, double dr, double idr, int ge) {
+  double r = (qi - kv) * idr;
   if (ge) r = fmax(r, 0.0);
   return {r * r, (yi * dr) * (yi * dr)};
 }
@@ -347,6 +349,27 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
     os[0] = fma(ks[3], vnext, os[0]);
     os[1] = fma(kd[2], lds_ld(xta), os[1]);
   };
+  // The iteration's forms with the objective / right-hand side folded into the FMA chains: K^T y - c for the
+  // primal half-step (x + tau (K^T y - c) = x - tau (c - K^T y)) and K x - q for the dual one (y - sigma (K x - q)):
+  // one FP64 operation fewer per column and per row than forming the difference afterwards.
+  auto ktr_c = [&](const double (&vr)[NR], double vprev, double (&out)[NC]) {
+    out[0] = fma(kd[0], vr[1], fma(ks[0], vr[0], -cof(0)));
+    out[1] = fma(kd[1], vr[1], fma(ks[1], vr[0], -cof(1)));
+    out[2] = fma(ks[2], vr[0], fma(kp, vprev, -cof(2)));
+    if constexpr (ICE) {
+      out[3] = fma(kb[0], vr[3], fma(ka[0], vr[2], fma(kd[3], vr[1], -cof(3))));
+      out[4] = fma(kb[1], vr[3], fma(ka[1], vr[2], -cof(4)));
+    }
+  };
+  auto kown_q = [&](const double (&v)[NC], double (&os)[NR]) {
+    os[0] = fma(ks[2], v[2], fma(ks[1], v[1], fma(ks[0], v[0], -q[0])));
+    os[1] = fma(kd[1], v[1], fma(kd[0], v[0], -q[1]));
+    if constexpr (ICE) {
+      os[1] = fma(kd[3], v[3], os[1]);
+      os[2] = fma(ka[1], v[4], fma(ka[0], v[3], -rhs(2)));
+      os[3] = fma(kb[1], v[4], fma(kb[0], v[3], -rhs(3)));
+    }
+  };
   // per-lane partial K'y of the tau columns from the DCM row's value
   auto tau_parts = [&](double vd) {
     if (J == 1) {
@@ -479,11 +502,11 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
         }
       }
       double kty[NC], xb[NC];
-      ktr(y, YS[tid], kty);
+      ktr_c(y, YS[tid], kty);
 #pragma unroll
       for (int v = 0; v < NC; ++v) {  // branch-free: padding steps have c = lo = hi = 0 and stay at 0
         const double lo = v == 2 ? loe : 0.0;
-        const double p1 = vmin(vmax(fma(-tau, cof(v) - kty[v], x[v]), lo), hib(v));
+        const double p1 = vmin(vmax(fma(tau, kty[v], x[v]), lo), hib(v));
         xb[v] = fma(2.0, p1, -x[v]);
         if (CHECK) {
           const double d = x[v] - p1, da = p1 - xa[v];
@@ -494,7 +517,7 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
         x[v] = fma(ca, xb[v], cb * xa[v]);
       }
       XE[tid] = xb[2];
-      kown(xb, kx);
+      kown_q(xb, kx);
       if constexpr (W0) {
         tau_update(uniform(wave_sum_dpp(ta0 + ta1)), ca, cb, chk_tag);
       } else {
@@ -507,7 +530,7 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
       kfin(kx, XE[tid + 1]);
 #pragma unroll
       for (int r = 0; r < NR; ++r) {  // row 0 (SOE) is an equality; DCM / ICE rows are >=: duals stay >= 0
-        double p1 = fma(sigma, rhs(r) - kx[r], y[r]);
+        double p1 = fma(-sigma, kx[r], y[r]);
         if (r > 0) p1 = vmax(p1, 0.0);
         if (CHECK) {
           const double d = y[r] - p1, da = p1 - ya[r];
@@ -580,13 +603,15 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
       if (J > 0) tau_parts(yp[1]);
       lds_barrier();
       auto col_kkt = [&](int j, double kt, double cj, double loj, double hij, double xj) {
-        const ColKkt r = col_kkt_fn(kt, cj, loj, hij, xj, dcv[opaque(j)]);
+        const int jj = opaque(j);
+        const ColKkt r = col_kkt_fn(kt, cj, loj, hij, xj, dcv[jj], w.tmpc[W.wn + jj]);
         acc[5] += r.rd2;
         acc[6] += r.cx;
         acc[8] += r.bt;
       };
       auto row_kkt = [&](int i, double kv, double qi, double yi, bool ge) {
-        const RowKkt r = row_kkt_fn(kv, qi, yi, drv[opaque(i)], ge);
+        const int ii = opaque(i);
+        const RowKkt r = row_kkt_fn(kv, qi, yi, drv[ii], w.tmpr[W.wm + ii], ge);
         acc[4] += r.rp2;
         acc[7] += qi * yi;
         acc[9] += r.y2;

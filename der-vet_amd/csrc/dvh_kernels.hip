@@ -291,6 +291,10 @@ __global__ __launch_bounds__(kSetupB) void setup_kernel(const Batch b, const Wor
     nrm[1] += qi * d * qi * d;
     nrm[3] += qi * qi;
   }
+  // reciprocal scalings for the band kernel's KKT checks (multiplications instead of divisions); the same thread
+  // owns index j / i in the Ruiz update above, so these overwrite factors nobody reads any more
+  for (int j = tid; j < n; j += kSetupB) tmpc[j] = 1.0 / Dc[j];
+  for (int i = tid; i < m; i += kSetupB) tmpr[i] = 1.0 / Dr[i];
   if (!MED) {
     for (int j = tid; j < n; j += kSetupB) gDc[j] = Dc[j];
     for (int i = tid; i < m; i += kSetupB) gDr[i] = Dr[i];

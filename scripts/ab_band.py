@@ -22,7 +22,8 @@ pb = builder.pack_groups(scenarios.config4(range(%d)))
 dev = pb.to_torch("cuda:0").alloc_outputs()
 s = BatchSolver(0)
 out = {}
-for label, kw in (("plain", dict(check_every=1000000, kkt_every=1)), ("checks", dict(check_every=32, kkt_every=4))):
+for label, kw in (("plain", dict(check_every=1000000, kkt_every=1)), ("checks", dict(check_every=32, kkt_every=4)),
+                  ("warm64_2", dict(check_every=64, kkt_every=2)), ("kkt32_1", dict(check_every=32, kkt_every=1))):
     s.set_options(eps=1e-30, eps_obj=0.0, max_iters=%d, **kw)
     best = None
     for rep in range(3):
@@ -62,7 +63,8 @@ def main():
         if ref is None:
             ref = obj
         d = float(np.max(np.abs(obj - ref) / np.maximum(np.abs(ref), 1.0)))
-        print(f"{os.path.basename(lib):22s} plain {res['plain']:.3f} checks {res['checks']:.3f} us/iter/CU | solve "
+        print(f"{os.path.basename(lib):22s} plain {res['plain']:.3f} checks {res['checks']:.3f} 64/2 {res['warm64_2']:.3f} "
+              f"32/1 {res['kkt32_1']:.3f} us/iter/CU | solve "
               f"{res['solve_ms']:.1f} ms, iters {res['iters']:.1f}, optimal {res['optimal']:.4f}, max obj diff vs "
               f"first {d:.2e}, band {res['paths']['band_windows']}", flush=True)
 
