@@ -26,7 +26,11 @@ def main():
     ap.add_argument("--eps", type=float, default=0.0)
     ap.add_argument("--opt", action="append", default=[], help="dvh_options field=value (repeatable)")
     ap.add_argument("--no-cold", action="store_true")
+    ap.add_argument("--lib", default=None, help="alternative libdervet_hip.so (A/B builds)")
     args = ap.parse_args()
+    if args.lib:
+        from dervet_hip import _lib
+        _lib.LIB_PATH = os.path.abspath(args.lib)
     from dervet_hip import BatchSolver
     from dervet_hip.lp import scenarios
     from dervet_hip.sweep import SeededSweep
