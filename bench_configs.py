@@ -15,6 +15,9 @@ config-4 slice for comparison).
   medium    (`--only 7`) windows above the on-chip limit of 4,096 columns / rows as a batch: --med-scenarios
             config-4 scenarios with n = "year" (annual hourly windows, T = 8,760, n = 26,292) and with dt = 0.25
             (15-minute monthly windows, T = 2,688..2,976, n <= 8,929)
+  degradation (`--only 8`) --deg-scenarios config-4 scenarios with cycle + calendar degradation: window
+            position k of every scenario in one batch, capacities updated from the solved SOE profiles before
+            position k + 1 (dervet_hip/degradation.py; parity unpinned: storagevet's degradation module is absent)
   market    (`--only 6`) Usecase 3 daily DA + FR windows of the three golden cases (3 x 365), and
             the same days with load following + spinning / non-spinning reserve added (synthetic LF / SR / NSR
             prices from the fixture's Reg Up / Down prices; parity unpinned beyond HiGHS on the same LP)
@@ -120,6 +123,7 @@ def main():
     ap.add_argument("--c5-scenarios", type=int, default=1000)
     ap.add_argument("--c5-years", type=int, default=20)
     ap.add_argument("--med-scenarios", type=int, default=1000)
+    ap.add_argument("--deg-scenarios", type=int, default=1000)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--sample", type=int, default=48)
     ap.add_argument("--procs", type=int, default=16)
@@ -195,6 +199,8 @@ def main():
             P(groups), s, args.reps, args.sample, args.procs)
     if 5 in only:
         config5_horizon(s, range(args.c5_scenarios), args.c5_years, args)
+    if 8 in only:
+        degradation_sweep(s, range(args.deg_scenarios), args)
     if 7 in only:
         ids = range(args.med_scenarios)
         run("medium-annual", f"{args.med_scenarios} config-4 scenarios x 1 annual hourly window (n = 'year', T = 8,760)",
@@ -202,6 +208,41 @@ def main():
         ids = range(max(1, args.med_scenarios // 12))
         run("medium-15min", f"{len(ids)} config-4 scenarios x 12 monthly windows at dt = 0.25 h",
             P(scenarios.config4(ids, dt=0.25)), s, args.reps, min(args.sample, 8), args.procs)
+
+
+def degradation_sweep(s, ids, args):
+    """Degradation-coupled config-4 sweep: 12 window positions in order, each one batched solve over every
+    scenario; wall time of the whole loop (host builds, solves, capacity updates) and of the GPU solves alone."""
+    from dervet_hip import degradation
+    from dervet_hip.lp import scenarios
+    ids = list(ids)
+    P = scenarios.sweep_parameters(ids)
+    deg = degradation.Degradation(P["E"], yearly_degrade=2.0)
+    solve_ms = []
+
+    class Timed:
+        def solve_packed(self, dev):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            s.solve_packed(dev)
+            torch.cuda.synchronize()
+            solve_ms.append(1e3 * (time.perf_counter() - t))
+
+    sw = degradation.DegradationSweep(lambda k, cap: scenarios.config4(ids, E=cap, only=[k]), range(12), deg)
+    t = time.perf_counter()
+    out = sw.run(Timed())
+    wall = time.perf_counter() - t
+    windows = 12 * len(ids)
+    it = np.concatenate([p["iters"] for p in out])
+    line = {"config": "degradation", "workload": f"{len(ids)} config-4 scenarios x 12 monthly windows, cycle + calendar "
+                                                 "degradation coupling the months (2 %/yr, default cycle-life table)",
+            "windows": windows, "schedule": "cold, window position by window position",
+            "solve_ms_total": round(sum(solve_ms), 1), "windows_per_s_solve": round(windows / (sum(solve_ms) / 1e3), 1),
+            "wall_s_total": round(wall, 2), "windows_per_s_end_to_end": round(windows / wall, 1),
+            "iters_mean": round(float(it.mean()), 1), "optimal": int(sum((p["status"] == 0).sum() for p in out)),
+            "mean_capacity_lost_pct": round(float(100 * (1 - deg.capacity() / P["E"]).mean()), 3),
+            "replacements": int(deg.replacements.sum())}
+    print(json.dumps(line), flush=True)
 
 
 def config5_horizon(s, ids, years, args):

@@ -33,11 +33,12 @@ def tariff(name="data_tariff"):
 
 def windows_by_period(year, dt, load, gen, bat, tariff_def=None, da_price=None, n="month", ene_min=None,
                       ene_max=None, demand_price_override=None, price_scale=None, tags_prefix=None,
-                      pv_curtail_max=None, ice=None, poi=None, grid_charge=True):
+                      pv_curtail_max=None, ice=None, poi=None, grid_charge=True, only=None):
     """Split S scenarios' series [S, Tall] into windows; returns a list of WindowGroup (one per window id).
 
     demand_price_override [S] replaces every demand charge's $/kW (sweep); price_scale [S] scales energy prices.
     poi / grid_charge: POI interconnection limits and PV grid_charge (builder.battery_group; parity unpinned).
+    only: window ids to build (None: all), e.g. one window position of a degradation-coupled sweep.
     """
     load = np.atleast_2d(np.asarray(load, np.float64))
     S, Tall = load.shape
@@ -58,6 +59,8 @@ def windows_by_period(year, dt, load, gen, bat, tariff_def=None, da_price=None, 
         wid = np.arange(Tall) // int(n)
     groups = []
     for w in np.unique(wid):
+        if only is not None and int(w) not in only:
+            continue
         sel = np.nonzero(wid == w)[0]
         T = len(sel)
         masks, prices = [], []
@@ -146,10 +149,12 @@ def sweep_features(P):
     return np.stack([np.log(P["E"] / P["load_scale"]), P["duration"], P["pv_rated"] / P["load_scale"]], axis=1)
 
 
-def config4(scenarios, n="month", dt=1.0):
+def config4(scenarios, n="month", dt=1.0, E=None, only=None):
     """Synthetic sweep windows for the given scenario ids (12 monthly windows each).  n: the optimisation window
     (Model_Parameters_Template_DER.csv:8 `n`: "month", "year" or a step count); dt < 1: sub-hourly steps, the hourly
-    series held constant within each hour (Model_Parameters_Template_DER.csv:4 `dt`)."""
+    series held constant within each hour (Model_Parameters_Template_DER.csv:4 `dt`).  E [S]: the batteries'
+    current energy capacity (a degraded battery, dervet_hip.degradation; power ratings stay at the rated E /
+    duration); only: window ids to build."""
     from scipy.signal import lfilter
     ri = reference_inputs()
     P = sweep_parameters(scenarios)
@@ -159,14 +164,14 @@ def config4(scenarios, n="month", dt=1.0):
     a = lfilter([1.0], [1.0, -phi], e, axis=1)
     load = ri["multi_der_site_load"][None, :] * P["load_scale"][:, None] * (1.0 + 0.05 * a)
     gen = P["pv_rated"][:, None] * np.nan_to_num(ri["multi_der_pv_profile"])[None, :]
-    E = P["E"]
-    bat = dict(E=E, Pch=E / P["duration"], Pdis=E / P["duration"], rte=P["rte"], sdr=0.0, soc_target=1.0,
-               ulsoc=1.0, llsoc=0.0, fixedOM=10.0, OMexpenses=0.0, hp=0.0)
+    Eb = P["E"] if E is None else np.asarray(E, np.float64)
+    bat = dict(E=Eb, Pch=P["E"] / P["duration"], Pdis=P["E"] / P["duration"], rte=P["rte"], sdr=0.0,
+               soc_target=1.0, ulsoc=1.0, llsoc=0.0, fixedOM=10.0, OMexpenses=0.0, hp=0.0)
     rep = int(round(1.0 / dt))
     if rep > 1:
         load, gen = np.repeat(load, rep, axis=1), np.repeat(gen, rep, axis=1)
     return windows_by_period(2017, dt, load, gen, bat, tariff_def=tariff(), n=n, demand_price_override=P["demand"],
-                             price_scale=P["price_scale"], tags_prefix=list(scenarios))
+                             price_scale=P["price_scale"], tags_prefix=list(scenarios), only=only)
 
 
 def reliability_min_soe(critical_load, hours=4.0, dt=1.0, cap=None):
