@@ -18,6 +18,8 @@ config-4 slice for comparison).
   degradation (`--only 8`) --deg-scenarios config-4 scenarios with cycle + calendar degradation: window
             position k of every scenario in one batch, capacities updated from the solved SOE profiles before
             position k + 1 (dervet_hip/degradation.py; parity unpinned: storagevet's degradation module is absent)
+  build     (`--only 9`) window expansion of --c4-scenarios config-4 scenarios: host builder + upload of the
+            expanded LPs vs the device builder (lp/gpu_builder.py, bit-identical output)
   market    (`--only 6`) Usecase 3 daily DA + FR windows of the three golden cases (3 x 365), and
             the same days with load following + spinning / non-spinning reserve added (synthetic LF / SR / NSR
             prices from the fixture's Reg Up / Down prices; parity unpinned beyond HiGHS on the same LP)
@@ -201,6 +203,9 @@ def main():
         config5_horizon(s, range(args.c5_scenarios), args.c5_years, args)
     if 8 in only:
         degradation_sweep(s, range(args.deg_scenarios), args)
+        degradation_sweep(s, range(args.deg_scenarios), args, spec=True)
+    if 9 in only:
+        device_build(s, range(args.c4_scenarios), args.reps)
     if 7 in only:
         ids = range(args.med_scenarios)
         run("medium-annual", f"{args.med_scenarios} config-4 scenarios x 1 annual hourly window (n = 'year', T = 8,760)",
@@ -210,9 +215,10 @@ def main():
             P(scenarios.config4(ids, dt=0.25)), s, args.reps, min(args.sample, 8), args.procs)
 
 
-def degradation_sweep(s, ids, args):
+def degradation_sweep(s, ids, args, spec=False):
     """Degradation-coupled config-4 sweep: 12 window positions in order, each one batched solve over every
-    scenario; wall time of the whole loop (host builds, solves, capacity updates) and of the GPU solves alone."""
+    scenario; wall time of the whole loop (builds, solves, capacity updates) and of the GPU solves alone.  spec: the
+    windows are expanded on the GPU (lp/gpu_builder.py) instead of by the host builder."""
     from dervet_hip import degradation
     from dervet_hip.lp import scenarios
     ids = list(ids)
@@ -228,20 +234,69 @@ def degradation_sweep(s, ids, args):
             torch.cuda.synchronize()
             solve_ms.append(1e3 * (time.perf_counter() - t))
 
-    sw = degradation.DegradationSweep(lambda k, cap: scenarios.config4(ids, E=cap, only=[k]), range(12), deg)
+    sw = degradation.DegradationSweep(lambda k, cap: scenarios.config4(ids, E=cap, only=[k], spec=spec), range(12), deg,
+                                      builder=s)
     t = time.perf_counter()
     out = sw.run(Timed())
     wall = time.perf_counter() - t
     windows = 12 * len(ids)
     it = np.concatenate([p["iters"] for p in out])
-    line = {"config": "degradation", "workload": f"{len(ids)} config-4 scenarios x 12 monthly windows, cycle + calendar "
-                                                 "degradation coupling the months (2 %/yr, default cycle-life table)",
+    line = {"config": "degradation" + ("+device-build" if spec else ""),
+            "workload": f"{len(ids)} config-4 scenarios x 12 monthly windows, cycle + calendar degradation coupling "
+                        "the months (2 %/yr, default cycle-life table)",
             "windows": windows, "schedule": "cold, window position by window position",
             "solve_ms_total": round(sum(solve_ms), 1), "windows_per_s_solve": round(windows / (sum(solve_ms) / 1e3), 1),
             "wall_s_total": round(wall, 2), "windows_per_s_end_to_end": round(windows / wall, 1),
             "iters_mean": round(float(it.mean()), 1), "optimal": int(sum((p["status"] == 0).sum() for p in out)),
             "mean_capacity_lost_pct": round(float(100 * (1 - deg.capacity() / P["E"]).mean()), 3),
             "replacements": int(deg.replacements.sum())}
+    print(json.dumps(line), flush=True)
+
+
+def device_build(s, ids, reps):
+    """Window expansion for a config-4 batch: host builder (numpy) + upload of the expanded LP, against the device
+    builder (numpy for the compact inputs, upload of those, expansion on the GPU); both give the same bytes
+    (tests/test_gpu_builder.py).  Best of reps after one warm-up; the solve of the same batch for scale."""
+    from dervet_hip.lp import builder, gpu_builder, scenarios
+    ids = list(ids)
+    tm = {"host": [], "device": [], "host_build_only": [], "spec_only": []}
+    for r in range(reps + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        pb = builder.pack_groups(scenarios.config4(ids))
+        t1 = time.perf_counter()
+        dh = pb.to_torch("cuda:0").alloc_outputs()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        specs = scenarios.config4(ids, spec=True)
+        t3 = time.perf_counter()
+        dd = gpu_builder.pack_specs_device(specs, s)
+        t4 = time.perf_counter()
+        if r:
+            tm["host"].append(t2 - t0)
+            tm["host_build_only"].append(t1 - t0)
+            tm["device"].append(t4 - t2)
+            tm["spec_only"].append(t3 - t2)
+        same = all(torch.equal(getattr(dh, f), getattr(dd, f)) for f in ("indptr", "indices", "data", "c", "c0", "q",
+                                                                         "l", "u"))
+        if r < reps:
+            del dh, dd
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    s.solve_packed(dd)
+    torch.cuda.synchronize()
+    solve = time.perf_counter() - t
+    w = len(ids) * 12
+    best = {k: min(v) for k, v in tm.items()}
+    line = {"config": "device-build", "workload": f"{len(ids)} config-4 scenarios x 12 monthly windows: window "
+                                                  "expansion + upload, host builder vs device builder",
+            "windows": w, "bit_identical": bool(same),
+            "host_build_ms": round(1e3 * best["host_build_only"], 1),
+            "host_build_upload_ms": round(1e3 * best["host"], 1),
+            "device_spec_ms": round(1e3 * best["spec_only"], 1),
+            "device_build_total_ms": round(1e3 * best["device"], 1),
+            "host_windows_per_s": round(w / best["host"], 1), "device_windows_per_s": round(w / best["device"], 1),
+            "solve_ms": round(1e3 * solve, 1)}
     print(json.dumps(line), flush=True)
 
 

@@ -442,6 +442,44 @@ int dvh_last_timing(const dvh_handle* h, double* ms3) {
 
 }  // extern "C"
 
+namespace dvh {
+hipError_t launch_build_battery(const dvh_battery_group& g, const dvh_packed& b, int first, hipStream_t s);
+}
+
+extern "C" int dvh_build_battery_group(dvh_handle* h, const dvh_battery_group* g, const dvh_packed* b,
+                                       int32_t first) {
+  if (!h) return DVH_ERR_ARG;
+  if (!g || !b) return fail(h, DVH_ERR_ARG, "null group or batch");
+  if (g->G == 0) return DVH_OK;
+  if (g->T < 1 || g->J < 0 || g->G < 0 || g->mI < 0 || !(g->dt > 0.0) || first < 0 || first + g->G > b->count)
+    return fail(h, DVH_ERR_ARG, "battery group: bad sizes or window range");
+  if ((g->mI > 0 && (!g->dcm_t || !g->dcm_j)) || !g->base || (g->J > 0 && !g->demand) || !g->E || !g->pch ||
+      !g->pdis || !g->rte || !g->sdr || !g->soc_target || !g->ulsoc || !g->llsoc || !g->om || !g->c0 ||
+      (g->has_retail && !g->retail) || (g->has_da && !g->da) || (g->has_emin && !g->emin) ||
+      (g->has_emax && !g->emax))
+    return fail(h, DVH_ERR_ARG, "battery group: null input array");
+  if (!b->desc || !b->indptr || !b->indices || !b->data || !b->c || !b->c0 || !b->q || !b->l || !b->u)
+    return fail(h, DVH_ERR_ARG, "null device array in packed batch");
+  DVH_HIP(h, hipSetDevice(h->device));
+  hipStream_t s = h->stream;
+  // the windows' descriptors must describe exactly this LP shape, inside the arrays (the kernel writes through them)
+  std::vector<int64_t> desc(8 * (size_t)g->G);
+  DVH_HIP(h, hipMemcpyAsync(desc.data(), b->desc + 8 * (int64_t)first, desc.size() * sizeof(int64_t),
+                            hipMemcpyDeviceToHost, s));
+  DVH_HIP(h, hipStreamSynchronize(s));
+  const int64_t T = g->T, n = 3 * T + g->J, m = T + 1 + g->mI, nnz = 4 * T + 3 * (int64_t)g->mI;
+  for (int w = 0; w < g->G; ++w) {
+    const int64_t* d = &desc[8 * (size_t)w];
+    if (d[0] != n || d[1] != m || d[2] != T + 1 || d[3] != nnz || d[4] < 0 || d[5] < 0 || d[6] < 0 || d[7] < 0 ||
+        d[4] + m + 1 > b->total_rows || d[5] + nnz > b->total_nnz || d[6] + n > b->total_n || d[7] + m > b->total_m)
+      return fail(h, DVH_ERR_ARG, "battery group: descriptor of window " + std::to_string(first + w) +
+                                      " does not match the group's LP shape or the arrays");
+  }
+  hipError_t e = dvh::launch_build_battery(*g, *b, first, s);
+  if (e != hipSuccess) return hip_fail(h, e, "launch_build_battery");
+  return DVH_OK;
+}
+
 // Medium tier over the candidates of one chunk (setup already run): plan, then the team kernel over the windows the
 // plan accepts; med_done[k] = 1 for the windows it solved or that the setup reported infeasible.  The others stay
 // with the grid-wide path.

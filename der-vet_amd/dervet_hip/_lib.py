@@ -61,6 +61,16 @@ class OutageCase(ctypes.Structure):
 
 
 # symbol -> (restype, argtypes); every symbol declared in include/dervet_hip.h
+class BatteryGroup(ctypes.Structure):
+    """dvh_battery_group (device-side window builder inputs; pointers are device addresses)."""
+    _fields_ = [("T", ctypes.c_int32), ("J", ctypes.c_int32), ("G", ctypes.c_int32), ("mI", ctypes.c_int32),
+                ("dt", ctypes.c_double), ("has_retail", ctypes.c_int32), ("has_da", ctypes.c_int32),
+                ("has_emin", ctypes.c_int32), ("has_emax", ctypes.c_int32)] + \
+               [(f, ctypes.c_void_p) for f in ("dcm_t", "dcm_j", "base", "retail", "da", "demand", "emin", "emax", "E",
+                                               "pch", "pdis", "rte", "sdr", "soc_target", "ulsoc", "llsoc", "om",
+                                               "c0")]
+
+
 SYMBOLS = {
     "dvh_version": (ctypes.c_char_p, []),
     "dvh_default_options": (None, [ctypes.POINTER(Options)]),
@@ -73,6 +83,8 @@ SYMBOLS = {
     "dvh_set_options": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Options)]),
     "dvh_solve_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(LP), ctypes.c_int32, ctypes.POINTER(Result)]),
     "dvh_solve_packed_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Packed), ctypes.c_void_p]),
+    "dvh_build_battery_group": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(BatteryGroup), ctypes.POINTER(Packed),
+                                               ctypes.c_int32]),
     "dvh_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
     "dvh_last_timing": (ctypes.c_int, [ctypes.c_void_p, c_double_p]),
     "dvh_last_stats": (ctypes.c_int, [ctypes.c_void_p, c_int32_p]),

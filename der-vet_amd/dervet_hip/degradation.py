@@ -157,28 +157,35 @@ class DegradationSweep:
     e.g. ``lambda k, E: scenarios.config4(ids, E=E, only=[k])``); positions: the window ids in time order; dt: hours
     per step."""
 
-    def __init__(self, build, positions, degradation, dt=1.0):
+    def __init__(self, build, positions, degradation, dt=1.0, builder=None):
         self.build, self.positions, self.deg, self.dt = build, list(positions), degradation, float(dt)
+        self.builder = builder
 
     def run(self, solver, device="cuda:0"):
         """Returns per position {k, iters [S], status [S], obj [S], degradation [S], capacity_before [S], ene [S, T]}.
         A solver with ``solve_packed`` (BatchSolver) gets the position's batch resident in HBM; any other solver
-        with ``solve(lps)`` (e.g. the CPU restatement) gets WindowLPs."""
-        from .lp import builder
+        with ``solve(lps)`` (e.g. the CPU restatement) gets WindowLPs.  When build returns device-builder specs
+        (``scenarios.config4(..., spec=True)``) the windows are expanded on the GPU (lp/gpu_builder.py; ``builder``
+        then names the BatchSolver whose handle builds them, default: solver)."""
+        from .lp import builder, gpu_builder
         out = []
         for k in self.positions:
             cap = self.deg.capacity()
             groups = self.build(k, cap)
             if hasattr(solver, "solve_packed") and device is not None:
                 import torch
-                pb = builder.pack_groups(groups)
-                dev = pb.to_torch(device).alloc_outputs()
+                if groups and isinstance(groups[0], gpu_builder.BatteryGroupSpec):
+                    dev = gpu_builder.pack_specs_device(groups, self.builder or solver, device)
+                    d = gpu_builder.desc_of(groups)[0]
+                else:
+                    pb = builder.pack_groups(groups)
+                    dev = pb.to_torch(device).alloc_outputs()
+                    d = np.asarray(pb.desc)
                 solver.solve_packed(dev)
                 torch.cuda.synchronize()
                 x = dev.x.cpu().numpy()
                 ist = dev.istats.cpu().numpy()
                 obj = dev.stats.cpu().numpy()[:, 0]
-                d = np.asarray(pb.desc)
                 del dev
                 T = int(d[0, 2]) - 1
                 ene = np.stack([x[int(r[6]) + 2 * T:int(r[6]) + 3 * T] for r in d])

@@ -12,6 +12,7 @@ Generator (numpy PCG64), per scenario s with seed 20250217 + s, draws in this or
   (P = E / duration); rte ~ U[0.80, 0.95].
   load_t = base_t * scale * (1 + 0.05 a_t),  a_t = 0.9 a_{t-1} + sqrt(1 - 0.81) e_t,  a_0 = e_0.
 """
+import functools
 import os
 
 import numpy as np
@@ -33,12 +34,13 @@ def tariff(name="data_tariff"):
 
 def windows_by_period(year, dt, load, gen, bat, tariff_def=None, da_price=None, n="month", ene_min=None,
                       ene_max=None, demand_price_override=None, price_scale=None, tags_prefix=None,
-                      pv_curtail_max=None, ice=None, poi=None, grid_charge=True, only=None):
+                      pv_curtail_max=None, ice=None, poi=None, grid_charge=True, only=None, spec=False):
     """Split S scenarios' series [S, Tall] into windows; returns a list of WindowGroup (one per window id).
 
     demand_price_override [S] replaces every demand charge's $/kW (sweep); price_scale [S] scales energy prices.
     poi / grid_charge: POI interconnection limits and PV grid_charge (builder.battery_group; parity unpinned).
     only: window ids to build (None: all), e.g. one window position of a degradation-coupled sweep.
+    spec: return the device builder's inputs (gpu_builder.BatteryGroupSpec) instead of host-built groups.
     """
     load = np.atleast_2d(np.asarray(load, np.float64))
     S, Tall = load.shape
@@ -73,7 +75,10 @@ def windows_by_period(year, dt, load, gen, bat, tariff_def=None, da_price=None, 
                     prices.append(dp)
         masks = np.array(masks, bool).reshape(-1, T)
         prices = np.stack(prices, axis=1) if prices else np.zeros((S, 0))
-        g = battery_group(
+        make = battery_group
+        if spec:
+            from .gpu_builder import battery_group_spec as make
+        g = make(
             T, dt, load[:, sel] - gen[:, sel], bat,
             retail_price=None if price is None else price[:, sel],
             da_price=None if da_price is None else np.broadcast_to(np.asarray(da_price, np.float64), (S, Tall))[:, sel],
@@ -149,21 +154,32 @@ def sweep_features(P):
     return np.stack([np.log(P["E"] / P["load_scale"]), P["duration"], P["pv_rated"] / P["load_scale"]], axis=1)
 
 
-def config4(scenarios, n="month", dt=1.0, E=None, only=None):
-    """Synthetic sweep windows for the given scenario ids (12 monthly windows each).  n: the optimisation window
-    (Model_Parameters_Template_DER.csv:8 `n`: "month", "year" or a step count); dt < 1: sub-hourly steps, the hourly
-    series held constant within each hour (Model_Parameters_Template_DER.csv:4 `dt`).  E [S]: the batteries'
-    current energy capacity (a degraded battery, dervet_hip.degradation; power ratings stay at the rated E /
-    duration); only: window ids to build."""
+@functools.lru_cache(maxsize=1)
+def _config4_series(scenarios):
+    """The scenarios' draws and hourly load / PV series (kept for the next call: a degradation-coupled sweep builds
+    one window position per call from the same series; read-only)."""
     from scipy.signal import lfilter
     ri = reference_inputs()
     P = sweep_parameters(scenarios)
     phi = 0.9
-    e = P["eps"].copy()
+    e = P.pop("eps")
     e[:, 1:] *= np.sqrt(1.0 - phi * phi)
     a = lfilter([1.0], [1.0, -phi], e, axis=1)
+    del e
     load = ri["multi_der_site_load"][None, :] * P["load_scale"][:, None] * (1.0 + 0.05 * a)
     gen = P["pv_rated"][:, None] * np.nan_to_num(ri["multi_der_pv_profile"])[None, :]
+    for v in list(P.values()) + [load, gen]:
+        v.flags.writeable = False
+    return P, load, gen
+
+
+def config4(scenarios, n="month", dt=1.0, E=None, only=None, spec=False):
+    """Synthetic sweep windows for the given scenario ids (12 monthly windows each).  n: the optimisation window
+    (Model_Parameters_Template_DER.csv:8 `n`: "month", "year" or a step count); dt < 1: sub-hourly steps, the hourly
+    series held constant within each hour (Model_Parameters_Template_DER.csv:4 `dt`).  E [S]: the batteries'
+    current energy capacity (a degraded battery, dervet_hip.degradation; power ratings stay at the rated E /
+    duration); only: window ids to build; spec: the device builder's inputs instead of host-built groups."""
+    P, load, gen = _config4_series(tuple(int(s) for s in scenarios))
     Eb = P["E"] if E is None else np.asarray(E, np.float64)
     bat = dict(E=Eb, Pch=P["E"] / P["duration"], Pdis=P["E"] / P["duration"], rte=P["rte"], sdr=0.0,
                soc_target=1.0, ulsoc=1.0, llsoc=0.0, fixedOM=10.0, OMexpenses=0.0, hp=0.0)
@@ -171,7 +187,7 @@ def config4(scenarios, n="month", dt=1.0, E=None, only=None):
     if rep > 1:
         load, gen = np.repeat(load, rep, axis=1), np.repeat(gen, rep, axis=1)
     return windows_by_period(2017, dt, load, gen, bat, tariff_def=tariff(), n=n, demand_price_override=P["demand"],
-                             price_scale=P["price_scale"], tags_prefix=list(scenarios), only=only)
+                             price_scale=P["price_scale"], tags_prefix=list(scenarios), only=only, spec=spec)
 
 
 def reliability_min_soe(critical_load, hours=4.0, dt=1.0, cap=None):

@@ -151,6 +151,39 @@ int dvh_solve_batch(dvh_handle* h, const dvh_lp* lps, int32_t count, dvh_result*
 /* Device-resident batch; `stream` is a hipStream_t (NULL = the handle's own stream).  Asynchronous
  * w.r.t. the host when stream != NULL; call dvh_synchronize / hipStreamSynchronize before reading. */
 int dvh_solve_packed_device(dvh_handle* h, const dvh_packed* batch, void* stream);
+
+/* ---- Device-side window builder (the LP that storagevet's
+ * set_up_optimization builds for a battery + demand-charge + retail / DA window, MicrogridScenario.py:322-346).
+ * Expands G windows' inputs (device pointers) into the packed batch's LP arrays, windows first .. first + G - 1,
+ * whose descriptors the caller has set (n = 3T + J, m = T + 1 + mI, nnz = 4T + 3 mI, any offsets).  The values are
+ * exactly those of dervet_hip/lp/builder.py battery_group (same formulas, same summation order; bit-identical,
+ * tests/test_gpu_builder.py), so a sweep ships its compact inputs to HBM instead of the expanded LPs.
+ * Asynchronous on the handle's stream. */
+typedef struct dvh_battery_group {
+  int32_t T, J, G, mI;             /* steps, demand-charge (tau) columns, windows, demand-charge rows           */
+  double dt;                       /* hours per step                                                             */
+  int32_t has_retail, has_da;      /* price inputs present                                                       */
+  int32_t has_emin, has_emax;      /* aggregate-SOE limits present                                               */
+  const int32_t* dcm_t;            /* [mI] step of each demand-charge row (rows in builder order)                */
+  const int32_t* dcm_j;            /* [mI] its tau column                                                        */
+  const double* base;              /* [G*T] net load + housekeeping power, kW (load - fixed PV + hp)             */
+  const double* retail;            /* [G*T] $/kWh or NULL                                                        */
+  const double* da;                /* [G*T] $/kWh or NULL                                                        */
+  const double* demand;            /* [G*J] $/kW                                                                 */
+  const double* emin;              /* [G*T] kWh or NULL                                                          */
+  const double* emax;              /* [G*T] kWh or NULL                                                          */
+  const double* E;                 /* [G] energy capacity, kWh                                                   */
+  const double* pch;               /* [G] kW                                                                     */
+  const double* pdis;              /* [G] kW                                                                     */
+  const double* rte;               /* [G] round-trip efficiency, fraction                                        */
+  const double* sdr;               /* [G] self-discharge, fraction per hour (sdr % / 100)                        */
+  const double* soc_target;        /* [G] fraction                                                               */
+  const double* ulsoc;             /* [G] fraction                                                               */
+  const double* llsoc;             /* [G] fraction                                                               */
+  const double* om;                /* [G] variable O&M, $/MWh                                                    */
+  const double* c0;                /* [G] objective constant (the terms' constants, summed on the host)          */
+} dvh_battery_group;
+int dvh_build_battery_group(dvh_handle* h, const dvh_battery_group* group, const dvh_packed* batch, int32_t first);
 int dvh_synchronize(dvh_handle* h);
 
 /* Timing of the most recent solve on the handle's stream (HIP events, milliseconds):

@@ -38,3 +38,17 @@ def test_lockstep_sweep_matches_serial_and_highs(gpu_solver):
                  c0=float(g.c0[i]), l=g.l[i], u=g.u[i], m_eq=g.m_eq)
         h = window_lp.solve_highs(o)
         assert abs(out[6]["obj"][i] - h["obj"]) <= 1e-5 * abs(h["obj"])
+
+
+def test_device_built_sweep_equals_host_built(gpu_solver):
+    """The same sweep with every position's windows expanded on the GPU (lp/gpu_builder.py): identical results."""
+    ids = list(range(6))
+    P = scenarios.sweep_parameters(ids)
+    host, dh = _sweep(ids, P["E"], gpu_solver, range(4))
+    deg = degradation.Degradation(P["E"], yearly_degrade=2.0)
+    sw = degradation.DegradationSweep(lambda k, cap: scenarios.config4(ids, E=cap, only=[k], spec=True), range(4), deg)
+    dev = sw.run(gpu_solver)
+    for a, b in zip(host, dev):
+        for f in ("ene", "iters", "status", "obj", "degradation", "capacity_before"):
+            assert np.array_equal(a[f], b[f]), f
+    assert np.array_equal(dh.capacity(), deg.capacity())
