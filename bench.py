@@ -22,6 +22,7 @@ the restated LP + HiGHS on a process pool (oracle/cpu_baseline.py), which is als
 objectives on its sample.
 """
 import argparse
+import functools
 import json
 import os
 import sys
@@ -151,6 +152,9 @@ def main():
                          "from their nearest seed (dervet_hip/sweep.py); cold: every window from zero")
     ap.add_argument("--seed-stride", type=int, default=32)
     ap.add_argument("--no-cold-ref", action="store_true", help="skip the untimed all-cold reference solve")
+    ap.add_argument("--build", choices=("device", "host"), default="device",
+                    help="window expansion: on the GPU from compact inputs (lp/gpu_builder.py) or by the host "
+                         "builder + upload (bit-identical batches; untimed by the contract, reported as build)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -175,21 +179,35 @@ def main():
 
     S = args.scenarios
     scen = range(*parallel.weak_shard(S, rank))
+    solver = BatchSolver(local)
     t0 = time.time()
     sweep = None
+    make = functools.partial(scenarios.config4, spec=args.build == "device")
     if args.schedule == "seeded":
         P = scenarios.sweep_parameters(scen)
-        sweep = SeededSweep(scenarios.config4, scen, P["E"], stride=args.seed_stride,
-                            features=scenarios.sweep_features(P))
-        pb = sweep.packed
+        sweep = SeededSweep(make, scen, P["E"], stride=args.seed_stride, features=scenarios.sweep_features(P))
+        t1 = time.time()
+        dev = sweep.to_device(solver, f"cuda:{local}")
+        desc = sweep.desc
+    elif args.build == "device":
+        from dervet_hip.lp import gpu_builder
+        specs = make(scen)
+        t1 = time.time()
+        dev = gpu_builder.pack_specs_device(specs, solver, f"cuda:{local}")
+        desc = gpu_builder.desc_of(specs)[0]
+        del specs
     else:
-        groups = scenarios.config4(scen)
-        pb = builder.pack_groups(groups)
-        del groups
-    dev = pb.to_torch(f"cuda:{local}").alloc_outputs()
+        hb = builder.pack_groups(make(scen))
+        t1 = time.time()
+        dev = hb.to_torch(f"cuda:{local}").alloc_outputs()
+        desc = np.asarray(hb.desc)
+        del hb
+    torch.cuda.synchronize()
     build_s = time.time() - t0
-    count = pb.count
-    solver = BatchSolver(local)
+    build = {"kind": args.build, "s": round(build_s, 2), "host_inputs_s": round(t1 - t0, 2),
+             "expand_upload_s": round(time.time() - t1, 3)}
+    pb = dev  # windows are read back from the device for the CPU legs
+    count = len(desc)
     opts = {k: v for k, v in (("check_every", args.check_every), ("kkt_every", args.kkt_every)) if v > 0}
     if opts:
         solver.set_options(**opts)
@@ -201,7 +219,7 @@ def main():
 
     gathered = None
     phase = {}
-    runs = parallel.dispatch_runs(pb.desc) if dist is not None else None
+    runs = parallel.dispatch_runs(desc) if dist is not None else None
     tmax = max(r[4] for r in runs) if runs else 0
     gather = {}
 
@@ -216,7 +234,7 @@ def main():
             # the ch / dis / ene dispatch (fixed stride 3 * tmax); equal window counts per rank (weak scaling)
             torch.cuda.synchronize()
             tg = time.perf_counter()
-            rows = parallel.result_rows(dev.stats, dev.istats, dev.x, pb.desc, tmax, runs)
+            rows = parallel.result_rows(dev.stats, dev.istats, dev.x, desc, tmax, runs)
             gathered = parallel.gather_rows(rows, counts=[count] * world)
             torch.cuda.synchronize()
             gather.update(ms=round(1e3 * (time.perf_counter() - tg), 2), bytes_per_rank=int(rows.numel() * 8),
@@ -248,7 +266,7 @@ def main():
     kname = ("pdhg_band_kernel (battery-banded)" if ks["band_windows"] == count else
              "pdhg_ell_kernel" if ks["ell_windows"] == count else "mixed band / ELL / generic kernels")
     iters = ist[:, 1].astype(np.float64)
-    alg = float((alg_bytes_per_iter(pb.desc) * iters).sum())
+    alg = float((alg_bytes_per_iter(desc) * iters).sum())
     pdhg_s = tm["pdhg_ms"] * 1e-3
     achieved = alg / pdhg_s / 1e9 if pdhg_s > 0 else None
     status_counts = np.bincount(ist[:, 0] + 1, minlength=6)[1:].tolist()  # OPTIMAL..NUMERICAL
@@ -365,7 +383,7 @@ def main():
         "cpu_baseline": cpu,
         "gather": gather or None,
         "parity": parity,
-        "build_s": round(build_s, 1),
+        "build": build,
     }
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -82,14 +82,16 @@ class PackedBatch:
             setattr(p, f, t.data_ptr())
         return p
 
-    # ---- per-window views (host)
+    # ---- per-window views (host; slices of a device batch are copied to the host)
     def window(self, k):
-        d = np.asarray(self.desc[k])
+        h = lambda v: v.detach().cpu().numpy() if hasattr(v, "detach") else v  # noqa: E731
+        d = h(self.desc[k])
         n, m, meq, nnz, orow, onz, on, om = (int(v) for v in d)
-        return dict(n=n, m=m, m_eq=meq, nnz=nnz, indptr=self.indptr[orow:orow + m + 1],
-                    indices=self.indices[onz:onz + nnz], data=self.data[onz:onz + nnz], c=self.c[on:on + n],
-                    l=self.l[on:on + n], u=self.u[on:on + n], q=self.q[om:om + m], c0=float(self.c0[k]),
-                    x=None if self.x is None else self.x[on:on + n], y=None if self.y is None else self.y[om:om + m])
+        return dict(n=n, m=m, m_eq=meq, nnz=nnz, indptr=h(self.indptr[orow:orow + m + 1]),
+                    indices=h(self.indices[onz:onz + nnz]), data=h(self.data[onz:onz + nnz]), c=h(self.c[on:on + n]),
+                    l=h(self.l[on:on + n]), u=h(self.u[on:on + n]), q=h(self.q[om:om + m]), c0=float(self.c0[k]),
+                    x=None if self.x is None else h(self.x[on:on + n]),
+                    y=None if self.y is None else h(self.y[om:om + m]))
 
     def window_lp(self, k):
         """Window k as a solver.WindowLP (host copies)."""

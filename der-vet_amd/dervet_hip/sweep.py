@@ -95,6 +95,15 @@ def _window_id(tag):
     return tag[1] if isinstance(tag, tuple) and len(tag) > 1 else tag
 
 
+def _same_pattern(a, b):
+    """Same CSR pattern: host-built groups compare their CSR, device-builder specs the inputs that fix it."""
+    if a.n != b.n or a.m != b.m:
+        return False
+    if hasattr(a, "indices"):
+        return np.array_equal(a.indices, b.indices) and np.array_equal(a.indptr, b.indptr)
+    return a.T == b.T and np.array_equal(a.dcm_t, b.dcm_t) and np.array_equal(a.dcm_j, b.dcm_j)
+
+
 def plan(seed_groups, rest_groups, partner_of):
     """Transfers from the packed seed windows (packed first) to the rest windows (packed after them).
 
@@ -112,8 +121,7 @@ def plan(seed_groups, rest_groups, partner_of):
         if wid not in seed_at:
             raise ValueError(f"no seed group for window {wid!r}")
         sg, son, som = seed_at[wid]
-        if sg.n != g.n or sg.m != g.m or not np.array_equal(sg.indices, g.indices) or \
-                not np.array_equal(sg.indptr, g.indptr):
+        if not _same_pattern(sg, g):
             raise ValueError(f"seed and rest groups of window {wid!r} differ in pattern")
         col = {t[0]: i for i, t in enumerate(sg.tags)}
         local = np.array([col[partner_of[t[0]]] for t in g.tags], np.int64)
@@ -158,8 +166,9 @@ def sub_batch(pb, a, b):
 class SeededSweep:
     """Packs a scenario sweep seed-first and solves it in the two phases of the module docstring.
 
-    make_groups(scenario_ids) -> list of WindowGroup (e.g. ``scenarios.config4``); keys: similarity key per
-    scenario (same order as `scenario_ids`)."""
+    make_groups(scenario_ids) -> list of WindowGroup (e.g. ``scenarios.config4``) or of device-builder specs
+    (``functools.partial(scenarios.config4, spec=True)``: then ``packed`` is None and ``to_device`` expands the
+    windows on the GPU, lp/gpu_builder.py); keys: similarity key per scenario (same order as `scenario_ids`)."""
 
     def __init__(self, make_groups, scenario_ids, keys, stride=8, features=None, cover=False):
         from .lp import builder
@@ -171,8 +180,22 @@ class SeededSweep:
         rg = make_groups(self.rest_ids) if len(self.rest_ids) else []
         self.transfers = plan(sg, rg, partner_of)
         self.n_seed = sum(g.G for g in sg)
-        self.packed = builder.pack_groups(sg + rg)
         self.tags = [t for g in sg + rg for t in g.tags]
+        self.specs = None
+        if sg and not hasattr(sg[0], "indices"):
+            from .lp import gpu_builder
+            self.specs, self.packed = sg + rg, None
+            self.desc = gpu_builder.desc_of(self.specs)[0]
+        else:
+            self.packed = builder.pack_groups(sg + rg)
+            self.desc = np.asarray(self.packed.desc)
+
+    def to_device(self, solver, device):
+        """The sweep's packed batch on the device, outputs allocated (specs: built there by solver's handle)."""
+        if self.specs is not None:
+            from .lp import gpu_builder
+            return gpu_builder.pack_specs_device(self.specs, solver, device)
+        return self.packed.to_torch(device).alloc_outputs()
 
     def solve(self, solver, dev, warm_options=None):
         """dev: this sweep's packed batch on the device (``self.packed.to_torch(..).alloc_outputs()``).

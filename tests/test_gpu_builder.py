@@ -62,3 +62,26 @@ def test_solving_device_built_windows_equals_host_built(gpu_solver):
     for f in ("x", "y", "stats", "istats"):
         assert torch.equal(getattr(hd, f), getattr(dd, f)), f
     assert (dd.istats[:, 0] == 0).all()
+
+
+def test_seeded_sweep_on_device_built_windows_equals_host_built(gpu_solver):
+    """bench.py's default: the seeded sweep over windows expanded on the GPU gives the host-built sweep's results
+    bit for bit (same seeds, same warm-start transfers)."""
+    import functools
+
+    from dervet_hip.sweep import SeededSweep
+    ids = range(40)
+    P = scenarios.sweep_parameters(ids)
+    out = []
+    for make in (scenarios.config4, functools.partial(scenarios.config4, spec=True)):
+        sw = SeededSweep(make, ids, P["E"], stride=8, features=scenarios.sweep_features(P))
+        dev = sw.to_device(gpu_solver, "cuda:0")
+        sw.solve(gpu_solver, dev)
+        torch.cuda.synchronize()
+        out.append((sw, dev))
+    (sh, dh), (sd, dd) = out
+    assert sd.packed is None and np.array_equal(sh.desc, sd.desc) and sh.n_seed == sd.n_seed
+    for f in FIELDS[1:] + ("x", "y", "stats", "istats"):
+        assert torch.equal(getattr(dh, f), getattr(dd, f)), f
+    w = dd.window(5)
+    assert np.array_equal(w["c"], sh.packed.window(5)["c"])
