@@ -68,7 +68,8 @@ struct dvh_handle {
   double timing[3] = {0, 0, 0};
   int last_variant = -1;
   int n_ell = 0, n_generic = 0, n_large = 0, n_band = 0, n_chain = 0;
-  int kernel_path = 0;  // 0 band -> ELL -> generic, 1 generic only, 2 ELL -> generic (no band kernel)
+  int kernel_path = 0;  // 0 band -> ELL -> generic, 1 generic only, 2 ELL -> generic (no band kernel), 3 as 0 with
+                        // the one-step-per-lane battery band kernel
   dvh::LargeSolver* large = nullptr;  // grid-wide path for windows above dvh::kSmallMax (created on first use)
   float large_ms[2] = {0, 0};         // setup, PDHG time of the large windows of the last solve
   // Further devices of this handle (device_mask bits after the first, or dvh_create_devices): same options; a
@@ -269,7 +270,7 @@ int dvh_last_path_counts4(const dvh_handle* h, int32_t* out4) {
 }
 
 int dvh_set_kernel_path(dvh_handle* h, int mode) {
-  if (!h || mode < 0 || mode > 2) return DVH_ERR_ARG;
+  if (!h || mode < 0 || mode > 3) return DVH_ERR_ARG;
   h->kernel_path = mode;
   for (dvh_handle* p : h->peers) p->kernel_path = mode;
   return DVH_OK;
@@ -584,7 +585,7 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
   };
   // medium tier candidates: battery-shaped sizes (n = 3T + J, m <= 2T + 1) up to kPMax segments of kChainB steps;
   // the plan kernel verifies the pattern, anything else goes to the grid-wide path
-  const bool chain_on = h->kernel_path == 0 && o.rho == 1.0 && o.max_iters + o.power_iters < (1 << 17);
+  const bool chain_on = (h->kernel_path == 0 || h->kernel_path == 3) && o.rho == 1.0 && o.max_iters + o.power_iters < (1 << 17);
   auto is_medium = [&](int k) {
     const int64_t* d = &desc[8 * (size_t)k];
     const int64_t T = d[2] - 1;
@@ -700,16 +701,19 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
     const bool fast = h->kernel_path != 1 && o.rho == 1.0;
     std::vector<int32_t> ell_list;  // empty + ell_all: the whole chunk
     bool ell_all = true;
-    if (fast && h->kernel_path == 0) {
+    if (fast && (h->kernel_path == 0 || h->kernel_path == 3)) {
+      const int band_form = h->kernel_path == 3 ? 1 : 3;
       // pass 1: battery (+ DCM) windows over the whole chunk; pass 2: the ICE variant over what pass 1 returned
       auto band_pass = [&](bool ice, const std::vector<int32_t>* in, std::vector<int32_t>& out) -> hipError_t {
         hipError_t r;
+        int bvar = -1;
         if (in) {
           r = hipMemcpyAsync(h->d_list.p, in->data(), I * in->size(), hipMemcpyHostToDevice, s);
           if (r != hipSuccess) return r;
-          r = dvh::launch_pdhg_band(b, w, c.ch, o, s, ice, h->d_list.as<int32_t>(), (int)in->size());
+          r = dvh::launch_pdhg_band(b, w, c.ch, o, s, ice, band_form, h->d_list.as<int32_t>(), (int)in->size(),
+                                    &bvar);
         } else {
-          r = dvh::launch_pdhg_band(b, w, c.ch, o, s, ice, nullptr, 0);
+          r = dvh::launch_pdhg_band(b, w, c.ch, o, s, ice, band_form, nullptr, 0, &bvar);
         }
         if (r != hipSuccess) return r;
         ist.resize(2 * (size_t)c.ch.count);
@@ -733,7 +737,7 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
           for (int k = 0; k < c.ch.count; ++k) visit(c.ch.first + k);
         }
         h->n_band += nb;
-        if (nb > 0 && variant < 0) variant = 9000000 + 12 + (ice ? 100 : 0);  // band kernel, 768 threads
+        if (nb > 0 && variant < 0) variant = bvar;  // band kernel (steps per lane, ICE, waves per window)
         return hipSuccess;
       };
       ell_all = false;

@@ -14,11 +14,16 @@
 // The structure is detected and verified on the device from the CSR pattern (any values, any entry order
 // within a row, >= rows in any order); a window that does not match comes back with status kNeedsEll.
 //
-// Mapping: lane t owns time step t -- its columns, its SOE / DCM (/ ICE) rows -- with every coefficient, bound,
-// objective, iterate and anchor in VGPRs.  An SpMV needs only the next step's ene (K x) and the previous SOE
-// row's dual (K^T y): one LDS store + one LDS load per lane and half-step instead of per-entry gathers.  The
-// dense tau columns are summed by wave 0 from per-lane partials (no per-wave reduction).  768 threads per
-// window, 12 waves, <= 168 VGPRs.
+// Mapping: B lanes per window, lane l owns the S consecutive time steps S l .. S l + S - 1 -- their columns, their
+// SOE / DCM (/ ICE) rows -- with every coefficient, bound, objective, iterate and anchor in VGPRs.  An SpMV needs
+// only the next step's ene (K x) and the previous SOE row's dual (K^T y); inside a lane those are registers, across
+// lanes one LDS store + one LDS load per lane and half-step.  The dense tau columns are summed by wave 0 from
+// per-lane partials.  Instantiations: <768, 1> (one step per lane, 12 waves, one window per CU) and <384, 2> (two
+// steps per lane, 6 waves: two windows share a CU, so one window's barrier waits are filled by the other's work,
+// and every lane carries two independent FMA chains).  <= 168 VGPRs (3 waves per SIMD) either way.
+#include <stdio.h>
+#include <stdlib.h>
+
 #include <type_traits>
 
 #include "dvh_device.h"
@@ -26,19 +31,33 @@
 namespace dvh {
 namespace {
 
-constexpr int kBandB = 768;   // threads per window (T <= kBandB steps)
-constexpr int kJMax = 4;      // tau (demand-period) columns per window
+constexpr int kBandSteps = 768;  // steps per window (T <= kBandSteps)
+constexpr int kJMax = 4;         // tau (demand-period) columns per window
 constexpr int kNeedsEll = -2;
 
-// LDS layout in doubles (then ints): XE[B+1] YS[B+1] XT[kJMax] red[kNRed(NW+1)+4] TP[kJMax][B] XP[NC][B] YP[NR][B]
-// (ICE: RO[6][B]) | ints: dcm[B] ice_a[B] ice_b[B] ice_n[B] flag[4]
-__host__ __device__ inline size_t band_lds_doubles(int B, bool ice) {
+// LDS layout (B lanes, S steps per lane, SB = S B steps), doubles then ints:
+//   XE[B+1] YS[B+1] XT[kJMax] red[kNRed(NW+1)+4] TP[kJMax][B] XP[NC S][B] YP[NR S][B] (ICE: RO[6 S][B])
+//   | ints: dcm[SB] ice_a[SB] ice_b[SB] ice_n[SB] flag[4]
+// Register-relief flags LF (forms with several steps per lane): kLfAnchors -- the Halpern anchors XA[NC S][B] /
+// YA[NR S][B] live in LDS (one FMA operand per iteration, written at restarts; the ints, read only while the lane
+// state is loaded, share their space); kLfCosts -- CQ[5 S][B] = c of ch / dis / ene and q of the SOE / DCM rows in
+// LDS (one FMA addend per iteration); kLfImages -- the check iteration's T(z_k) goes to the window's global workspace
+// instead of XP / YP (read back by the same lane at the check).  Layout after TP: [XP YP] (no kLfImages) [XA YA]
+// (kLfAnchors) [RO] (ICE) [CQ] (kLfCosts).
+constexpr int kLfAnchors = 1, kLfCosts = 2, kLfImages = 4;
+__host__ __device__ inline size_t band_lds_doubles(int B, int S, bool ice, int LF) {
   const int NW = B / kWave, NC = ice ? 5 : 3, NR = ice ? 4 : 2;
-  return 2 * (size_t)(B + 1) + kJMax + (size_t)kNRed * (NW + 1) + 4 + (size_t)kJMax * B + (size_t)(NC + NR) * B +
-         (ice ? 6 * (size_t)B : 0);
+  const size_t SB = (size_t)S * B;
+  return 2 * (size_t)(B + 1) + kJMax + (size_t)kNRed * (NW + 1) + 4 + (size_t)kJMax * B +
+         ((LF & kLfImages) ? 0 : (NC + NR) * SB) + ((LF & kLfAnchors) ? (NC + NR) * SB : 0) +
+         ((LF & kLfCosts) ? 5 * SB : 0) + (ice ? 6 * SB : 0);
 }
-__host__ __device__ inline size_t band_lds_bytes(int B, bool ice) {
-  return align16(sizeof(double) * band_lds_doubles(B, ice)) + align16(sizeof(int32_t) * (4 * (size_t)B + 4));
+__host__ __device__ inline size_t band_ints_bytes(int B, int S) { return sizeof(int32_t) * (4 * (size_t)S * B + 4); }
+// The ints share the anchors' (kLfAnchors) or, in the other relieved forms, the check images' space
+__host__ __device__ inline bool band_ints_shared(int LF) { return (LF & kLfAnchors) || (LF && !(LF & kLfImages)); }
+__host__ __device__ inline size_t band_lds_bytes(int B, int S, bool ice, int LF) {
+  const size_t d = align16(sizeof(double) * band_lds_doubles(B, S, ice, LF));
+  return band_ints_shared(LF) ? d : d + align16(band_ints_bytes(B, S));
 }
 
 // KKT pieces of one column / one row (out of line: the KKT check runs every 128 iterations, and inlined it
@@ -64,10 +83,11 @@ __device__ __noinline__ RowKkt row_kkt_fn(double kv, double qi, double yi, doubl
   return {r * r, (yi * dr) * (yi * dr)};
 }
 
-template <int B, bool ICE>
-__global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Work w, const Chunk ch, const Opts o,
+template <int B, int S, bool ICE, int LF, int WPS>
+__global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const Work w, const Chunk ch, const Opts o,
                                                         const int32_t* list) {
   constexpr int NW = B / kWave;
+  constexpr int SB = S * B;        // step capacity
   constexpr int NC = ICE ? 5 : 3;  // columns per step: ch, dis, ene (, elec, on)
   constexpr int NR = ICE ? 4 : 2;  // rows per step: SOE, DCM (, ICE rated, ICE minimum)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -86,28 +106,37 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
     }
   };
   if (scal[6] == 3.0) return;  // reported infeasible by the setup kernel
-  if (scal[6] != 0.0 || T < 1 || T > B || J < 0 || J > kJMax || MD < 0 || MD > T || (J == 0 && MD > 0)) {
+  if (scal[6] != 0.0 || T < 1 || T > SB || J < 0 || J > kJMax || MD < 0 || MD > T || (J == 0 && MD > 0)) {
     bail();
     return;
   }
   const int CE = 3 * T + J, CO = 4 * T + J;  // first elec / on column (ICE)
   // ---- LDS carve
-  double* XE = reinterpret_cast<double*>(smem);  // x-bar (x+) of ene_t at [t]; [T..B] stay 0
-  double* YS = XE + (B + 1);                     // y (y+) of row t at [t]: the init row (t = 0), SOE row of step t-1
-  double* XT = YS + (B + 1);                     // x-bar (x+) of the tau columns
+  double* XE = reinterpret_cast<double*>(smem);  // x-bar (x+) of ene of lane l's first step at [l]; [B] stays 0
+  double* YS = XE + (B + 1);  // y (y+) of the init row at [0], of the SOE row of lane l's last step at [l + 1]
+  double* XT = YS + (B + 1);  // x-bar (x+) of the tau columns
   double* red = XT + kJMax;
-  double* TP = red + kNRed * (NW + 1) + 4;       // [kJMax][B] per-lane partial K'y of the tau columns
-  double* XP = TP + kJMax * B;                   // [NC][B] T(z) of the lane's columns (check iterations)
-  double* YP = XP + NC * B;                      // [NR][B] T(z) of the lane's rows
+  double* TP = red + kNRed * (NW + 1) + 4;  // [kJMax][B] per-lane partial K'y of the tau columns
+  constexpr bool LA = LF & kLfAnchors, LC = LF & kLfCosts, LI = LF & kLfImages;
+  double* XP = TP + kJMax * B;                  // [NC S][B] T(z) of the lane's columns (check iterations)
+  double* YP = XP + (LI ? 0 : NC * SB);         // [NR S][B] T(z) of the lane's rows
+  double* XA = YP + (LI ? 0 : NR * SB);         // [NC S][B] Halpern anchors of the columns (kLfAnchors)
+  double* YA = XA + (LA ? NC * SB : 0);         // [NR S][B] and of the rows
   // ICE: read-only data of the ICE columns / rows in LDS instead of VGPRs (the register budget at 3 waves per
-  // SIMD is 168): RO[0..1][.] = c of elec / on, RO[2..3][.] = upper bound of elec / on, RO[4..5][.] = q of the
-  // two ICE rows
-  double* RO = YP + NR * B;
-  int32_t* dcm = reinterpret_cast<int32_t*>(smem + align16(sizeof(double) * band_lds_doubles(B, ICE)));  // [B]
-  int32_t* ice_a = dcm + B;   // [B] ICE rows of each step (lower / higher row index), and their count
-  int32_t* ice_b = ice_a + B;
-  int32_t* ice_n = ice_b + B;
-  int32_t* flag = ice_n + B;
+  // SIMD is 168): RO[0..1] = c of elec / on, RO[2..3] = upper bound of elec / on, RO[4..5] = q of the two ICE rows,
+  // each [S][B]
+  double* RO = YA + (LA ? NR * SB : 0);
+  double* CQ = RO + (ICE ? 6 * SB : 0);  // [5 S][B] (kLfCosts)
+  static_assert(!(LF && ICE), "register relief is for the battery (+ DCM) kernel");
+  static_assert(!LA || sizeof(double) * (NC + NR) * SB >= sizeof(int32_t) * (4 * SB + 4), "ints fit the anchors");
+  constexpr bool IS = (LF & kLfAnchors) || (LF && !(LF & kLfImages));  // band_ints_shared(LF)
+  int32_t* dcm = LA   ? reinterpret_cast<int32_t*>(XA)
+                 : IS ? reinterpret_cast<int32_t*>(XP)
+                      : reinterpret_cast<int32_t*>(smem + align16(sizeof(double) * band_lds_doubles(B, S, ICE, LF)));
+  int32_t* ice_a = dcm + SB;  // [SB] ICE rows of each step (lower / higher row index), and their count
+  int32_t* ice_b = ice_a + SB;
+  int32_t* ice_n = ice_b + SB;
+  int32_t* flag = ice_n + SB;
 
   const int32_t* gkp = b.indptr + W.row;
   const int32_t* gkc = b.indices + W.nz;
@@ -122,10 +151,12 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
   double* yo_g = b.y + W.om;
 
   // ---- structure check (every entry of every row accounted for) and the step -> row maps
-  dcm[tid] = -1;
-  ice_a[tid] = 0x7fffffff;
-  ice_b[tid] = -1;
-  ice_n[tid] = 0;
+  for (int u = tid; u < SB; u += B) {
+    dcm[u] = -1;
+    ice_a[u] = 0x7fffffff;
+    ice_b[u] = -1;
+    ice_n[u] = 0;
+  }
   if (tid == 0) flag[0] = 0;
   __syncthreads();
   int bad = 0;
@@ -200,99 +231,134 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
   }
   if (bad) flag[0] = 1;
   __syncthreads();
-  if (ICE && tid < T && ice_n[tid] != 2) flag[0] = 1;  // exactly two ICE rows per step
+  if (ICE)
+    for (int u = tid; u < T; u += B)
+      if (ice_n[u] != 2) flag[0] = 1;  // exactly two ICE rows per step
   __syncthreads();
   if (flag[0] != 0) {
     bail();
     return;
   }
 
-  // ---- the lane's step t: columns (v) ch, dis, ene (, elec, on), rows (r) SOE, DCM (, ICE a, ICE b) -- VGPRs
-  const int t = tid;
-  const bool val = t < T;
-  auto col = [&](int v) { return v < 3 ? v * T + t : (v == 3 ? CE : CO) + t; };
-  double x[NC], xa[NC], cc[3], hi[3];
-  double loe = 0.0;                        // lower bound of ene (the others are 0)
-  double ks[4] = {0.0, 0.0, 0.0, 0.0};     // SOE row: coefficients of ch_t, dis_t, ene_t, ene_{t+1}
-  double kd[4] = {0.0, 0.0, 0.0, 0.0};     // DCM row: coefficients of ch_t, dis_t, tau_j, elec_t
-  double ka[2] = {0.0, 0.0}, kb[2] = {0.0, 0.0};  // ICE rows: coefficients of elec_t, on_t
-  double kp = 0.0;                         // coefficient of ene_t in row t (init row or SOE row of step t-1)
-  double y[NR], ya[NR], q[2];
-  int drow = -1, jt = 0, ra = -1, rb = -1;
+  // ---- the lane's steps t = S tid + s: columns (v) ch, dis, ene (, elec, on), rows (r) SOE, DCM (, ICE a, ICE b)
+  const int t0 = S * tid;
+  bool val[S];
+  double x[S][NC], xa[S][NC], cc[S][3], hi[S][3];
+  double loe[S];                     // lower bound of ene (the others are 0)
+  double ks[S][4];                   // SOE row: coefficients of ch_t, dis_t, ene_t, ene_{t+1}
+  double kd[S][4];                   // DCM row: coefficients of ch_t, dis_t, tau_j, elec_t
+  double ka[S][2], kb[S][2];         // ICE rows: coefficients of elec_t, on_t
+  double kp0 = 0.0;                  // coefficient of ene_{t0} in row t0 (the init row or the previous lane's SOE
+                                     // row); for s > 0 the coefficient of ene_t in row t is ks[s - 1][3]
+  double y[S][NR], ya[S][NR], q[S][2];
+  int drow[S], jt[S], ra[S], rb[S];
+  auto col = [&](int s, int v) { return v < 3 ? v * T + t0 + s : (v == 3 ? CE : CO) + t0 + s; };
+  auto ro = [&](int u, int s) -> double& { return RO[(u * S + s) * B + tid]; };
+  auto cqa = [&](int u, int s) -> double& { return CQ[(u * S + s) * B + tid]; };
 #pragma unroll
-  for (int v = 0; v < NC; ++v) x[v] = xa[v] = 0.0;
+  for (int s = 0; s < S; ++s) {
+    const int t = t0 + s;
+    val[s] = t < T;
 #pragma unroll
-  for (int v = 0; v < 3; ++v) cc[v] = hi[v] = 0.0;
+    for (int v = 0; v < NC; ++v) x[s][v] = xa[s][v] = 0.0;
 #pragma unroll
-  for (int r = 0; r < NR; ++r) y[r] = ya[r] = 0.0;
-  q[0] = q[1] = 0.0;
-  if (ICE)
-    for (int u = 0; u < 6; ++u) RO[u * B + tid] = 0.0;
-  auto cof = [&](int v) -> double { return v < 3 ? cc[v] : RO[(v - 3) * B + tid]; };
-  auto hib = [&](int v) -> double { return v < 3 ? hi[v] : RO[(v - 1) * B + tid]; };
-  auto rhs = [&](int r) -> double { return r < 2 ? q[r] : RO[(r + 2) * B + tid]; };
-  if (val) {
+    for (int v = 0; v < 3; ++v) cc[s][v] = hi[s][v] = 0.0;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) y[s][r] = ya[s][r] = 0.0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) ks[s][u] = kd[s][u] = 0.0;
+    ka[s][0] = ka[s][1] = kb[s][0] = kb[s][1] = 0.0;
+    q[s][0] = q[s][1] = 0.0;
+    loe[s] = 0.0;
+    drow[s] = -1;
+    jt[s] = 0;
+    ra[s] = rb[s] = -1;
+    if (ICE)
+      for (int u = 0; u < 6; ++u) ro(u, s) = 0.0;
+    if (LC)
+      for (int u = 0; u < 5; ++u) cqa(u, s) = 0.0;
+  }
+  auto cof = [&](int s, int v) -> double { return v < 3 ? (LC ? cqa(v, s) : cc[s][v]) : ro(v - 3, s); };
+  auto qv = [&](int s, int r) -> double { return LC ? cqa(3 + r, s) : q[s][r]; };
+  auto hib = [&](int s, int v) -> double { return v < 3 ? hi[s][v] : ro(v - 1, s); };
+  auto rhs = [&](int s, int r) -> double { return r < 2 ? qv(s, r) : ro(r + 2, s); };
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    if (!val[s]) continue;
+    const int t = t0 + s;
 #pragma unroll
     for (int v = 0; v < NC; ++v) {
-      const int j = col(v);
+      const int j = col(s, v);
       if (v < 3) {
-        hi[v] = us[j];
-        cc[v] = cs[j];
+        hi[s][v] = us[j];
+        if (LC)
+          cqa(v, s) = cs[j];
+        else
+          cc[s][v] = cs[j];
       } else {
-        RO[(v - 1) * B + tid] = us[j];
-        RO[(v - 3) * B + tid] = cs[j];
+        ro(v - 1, s) = us[j];
+        ro(v - 3, s) = cs[j];
       }
-      x[v] = xa[v] = fmin(fmax(0.0, ls[j]), us[j]);
+      x[s][v] = xa[s][v] = fmin(fmax(0.0, ls[j]), us[j]);
     }
-    loe = ls[2 * T + t];
+    loe[s] = ls[2 * T + t];
     for (int p = gkp[t + 1]; p < gkp[t + 2]; ++p) {
       const int c = gkc[p];
       const double a = gkv[p];
-      if (c == t) ks[0] = a;
-      else if (c == T + t) ks[1] = a;
-      else if (c == 2 * T + t) ks[2] = a;
-      else ks[3] = a;
+      if (c == t) ks[s][0] = a;
+      else if (c == T + t) ks[s][1] = a;
+      else if (c == 2 * T + t) ks[s][2] = a;
+      else ks[s][3] = a;
     }
-    for (int p = gkp[t]; p < gkp[t + 1]; ++p)
-      if (gkc[p] == 2 * T + t) kp = gkv[p];
-    q[0] = qs[t + 1];
+    if (s == 0)
+      for (int p = gkp[t]; p < gkp[t + 1]; ++p)
+        if (gkc[p] == 2 * T + t) kp0 = gkv[p];
+    if (LC)
+      cqa(3, s) = qs[t + 1];
+    else
+      q[s][0] = qs[t + 1];
     const int dv = dcm[t];
     if (dv >= 0) {
-      drow = dv >> 3;
-      jt = dv & 7;
-      for (int p = gkp[drow]; p < gkp[drow + 1]; ++p) {
+      drow[s] = dv >> 3;
+      jt[s] = dv & 7;
+      for (int p = gkp[drow[s]]; p < gkp[drow[s] + 1]; ++p) {
         const int c = gkc[p];
         const double a = gkv[p];
-        if (c < T) kd[0] = a;
-        else if (c < 2 * T) kd[1] = a;
-        else if (c < 3 * T + J) kd[2] = a;
-        else kd[3] = a;
+        if (c < T) kd[s][0] = a;
+        else if (c < 2 * T) kd[s][1] = a;
+        else if (c < 3 * T + J) kd[s][2] = a;
+        else kd[s][3] = a;
       }
-      q[1] = qs[drow];
+      if (LC)
+        cqa(4, s) = qs[drow[s]];
+      else
+        q[s][1] = qs[drow[s]];
     }
     if (ICE) {
-      ra = ice_a[t];
-      rb = ice_b[t];
-      for (int p = gkp[ra]; p < gkp[ra + 1]; ++p) (gkc[p] < CO ? ka[0] : ka[1]) = gkv[p];
-      for (int p = gkp[rb]; p < gkp[rb + 1]; ++p) (gkc[p] < CO ? kb[0] : kb[1]) = gkv[p];
-      RO[4 * B + tid] = qs[ra];
-      RO[5 * B + tid] = qs[rb];
+      ra[s] = ice_a[t];
+      rb[s] = ice_b[t];
+      for (int p = gkp[ra[s]]; p < gkp[ra[s] + 1]; ++p) (gkc[p] < CO ? ka[s][0] : ka[s][1]) = gkv[p];
+      for (int p = gkp[rb[s]]; p < gkp[rb[s] + 1]; ++p) (gkc[p] < CO ? kb[s][0] : kb[s][1]) = gkv[p];
+      ro(4, s) = qs[ra[s]];
+      ro(5, s) = qs[rb[s]];
     }
     if (o.warm) {  // warm start from the unscaled x / y in the output buffers
 #pragma unroll
       for (int v = 0; v < NC; ++v) {
-        const int j = col(v);
-        x[v] = xa[v] = fmin(fmax(xo_g[j] / dcv[j], ls[j]), us[j]);
+        const int j = col(s, v);
+        x[s][v] = xa[s][v] = fmin(fmax(xo_g[j] / dcv[j], ls[j]), us[j]);
       }
-      y[0] = ya[0] = yo_g[t + 1] / drv[t + 1];
-      if (drow >= 0) y[1] = ya[1] = fmax(yo_g[drow] / drv[drow], 0.0);
+      y[s][0] = ya[s][0] = yo_g[t + 1] / drv[t + 1];
+      if (drow[s] >= 0) y[s][1] = ya[s][1] = fmax(yo_g[drow[s]] / drv[drow[s]], 0.0);
       if (ICE) {
-        y[2] = ya[2] = fmax(yo_g[ra] / drv[ra], 0.0);
-        y[3] = ya[3] = fmax(yo_g[rb] / drv[rb], 0.0);
+        y[s][2] = ya[s][2] = fmax(yo_g[ra[s]] / drv[ra[s]], 0.0);
+        y[s][3] = ya[s][3] = fmax(yo_g[rb[s]] / drv[rb[s]], 0.0);
       }
     }
   }
-  const int xta = lds_addr(XT + jt);
+  int xta[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) xta[s] = lds_addr(XT + jt[s]);
   // Special state in wave 0 (registers sp[], meaning by lane): lane j < J holds tau column j {x, xa, c, lo, hi, x+};
   // lane kInitLane holds the init row (row 0: ene_0 = target) {y, ya, y+, q, coefficient, -}.
   constexpr int kInitLane = kWave - 1;
@@ -314,69 +380,107 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
     if (tlane) sp[0] = sp[1] = sp[5] = fmin(fmax(xo_g[3 * T + lane] / dcv[3 * T + lane], sp[3]), sp[4]);
     if (ilane) sp[0] = sp[1] = sp[2] = yo_g[0] / drv[0];
   }
+  if constexpr (IS) __syncthreads();  // anchors / images overwrite the step -> row maps: every lane has read them
+  if constexpr (LA) {
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+#pragma unroll
+      for (int v = 0; v < NC; ++v) XA[(v * S + s) * B + tid] = xa[s][v];
+#pragma unroll
+      for (int r = 0; r < NR; ++r) YA[(r * S + s) * B + tid] = ya[s][r];
+    }
+  }
+  auto axv = [&](int s, int v) -> double { return LA ? XA[(v * S + s) * B + tid] : xa[s][v]; };
+  auto ayv = [&](int s, int r) -> double { return LA ? YA[(r * S + s) * B + tid] : ya[s][r]; };
   if (tid < kJMax) XT[tid] = 0.0;
   if (tid == 0) XE[B] = YS[B] = 0.0;
   XE[tid] = YS[tid] = 0.0;
   for (int u = tid; u < kJMax * B; u += B) TP[u] = 0.0;
 #pragma unroll
-  for (int v = 0; v < NC; ++v) XP[v * B + tid] = x[v];
+  for (int s = 0; s < S; ++s) {
+    if constexpr (LI) {  // the outputs hold the last KKT check's T(z_k): the starting point until the first one
+      if (val[s]) {
+        const int t = t0 + s;
 #pragma unroll
-  for (int r = 0; r < NR; ++r) YP[r * B + tid] = y[r];
+        for (int v = 0; v < NC; ++v) xo_g[col(s, v)] = x[s][v] * dcv[col(s, v)];
+        yo_g[t + 1] = y[s][0] * drv[t + 1];
+        if (drow[s] >= 0) yo_g[drow[s]] = y[s][1] * drv[drow[s]];
+      }
+    } else {
+#pragma unroll
+      for (int v = 0; v < NC; ++v) XP[(v * S + s) * B + tid] = x[s][v];
+#pragma unroll
+      for (int r = 0; r < NR; ++r) YP[(r * S + s) * B + tid] = y[s][r];
+    }
+  }
   __syncthreads();
 
   // ---- SpMV pieces (fixed summation order)
-  // K^T of the lane's columns from its rows' values vr and vprev = the value of row t
-  auto ktr = [&](const double (&vr)[NR], double vprev, double (&out)[NC]) {
-    out[0] = fma(kd[0], vr[1], ks[0] * vr[0]);
-    out[1] = fma(kd[1], vr[1], ks[1] * vr[0]);
-    out[2] = fma(ks[2], vr[0], kp * vprev);
+  auto kpv = [&](int s) { return s == 0 ? kp0 : ks[s > 0 ? s - 1 : 0][3]; };
+  // K^T of step s's columns from its rows' values vr and vprev = the value of row t (the previous SOE row)
+  auto ktr = [&](int s, const double (&vr)[NR], double vprev, double (&out)[NC]) {
+    out[0] = fma(kd[s][0], vr[1], ks[s][0] * vr[0]);
+    out[1] = fma(kd[s][1], vr[1], ks[s][1] * vr[0]);
+    out[2] = fma(ks[s][2], vr[0], kpv(s) * vprev);
     if constexpr (ICE) {
-      out[3] = fma(kb[0], vr[3], fma(ka[0], vr[2], kd[3] * vr[1]));
-      out[4] = fma(kb[1], vr[3], ka[1] * vr[2]);
+      out[3] = fma(kb[s][0], vr[3], fma(ka[s][0], vr[2], kd[s][3] * vr[1]));
+      out[4] = fma(kb[s][1], vr[3], ka[s][1] * vr[2]);
     }
   };
-  // K of the lane's rows, own-column part (kfin adds the next step's ene and the tau term)
-  auto kown = [&](const double (&v)[NC], double (&os)[NR]) {
-    os[0] = fma(ks[2], v[2], fma(ks[1], v[1], ks[0] * v[0]));
-    os[1] = fma(kd[1], v[1], kd[0] * v[0]);
+  // K of step s's rows, own-column part (kfin_next adds the next step's ene, kfin_tau the tau term)
+  auto kown = [&](int s, const double (&v)[NC], double (&os)[NR]) {
+    os[0] = fma(ks[s][2], v[2], fma(ks[s][1], v[1], ks[s][0] * v[0]));
+    os[1] = fma(kd[s][1], v[1], kd[s][0] * v[0]);
     if constexpr (ICE) {
-      os[1] = fma(kd[3], v[3], os[1]);
-      os[2] = fma(ka[1], v[4], ka[0] * v[3]);
-      os[3] = fma(kb[1], v[4], kb[0] * v[3]);
+      os[1] = fma(kd[s][3], v[3], os[1]);
+      os[2] = fma(ka[s][1], v[4], ka[s][0] * v[3]);
+      os[3] = fma(kb[s][1], v[4], kb[s][0] * v[3]);
     }
   };
-  auto kfin = [&](double (&os)[NR], double vnext) {
-    os[0] = fma(ks[3], vnext, os[0]);
-    os[1] = fma(kd[2], lds_ld(xta), os[1]);
-  };
+  auto kfin_next = [&](int s, double (&os)[NR], double vnext) { os[0] = fma(ks[s][3], vnext, os[0]); };
+  auto kfin_tau = [&](int s, double (&os)[NR]) { os[1] = fma(kd[s][2], lds_ld(xta[s]), os[1]); };
   // The iteration's forms with the objective / right-hand side folded into the FMA chains: K^T y - c for the
   // primal half-step (x + tau (K^T y - c) = x - tau (c - K^T y)) and K x - q for the dual one (y - sigma (K x - q)):
   // one FP64 operation fewer per column and per row than forming the difference afterwards.
-  auto ktr_c = [&](const double (&vr)[NR], double vprev, double (&out)[NC]) {
-    out[0] = fma(kd[0], vr[1], fma(ks[0], vr[0], -cof(0)));
-    out[1] = fma(kd[1], vr[1], fma(ks[1], vr[0], -cof(1)));
-    out[2] = fma(ks[2], vr[0], fma(kp, vprev, -cof(2)));
+  auto ktr_c = [&](int s, const double (&vr)[NR], double vprev, double (&out)[NC]) {
+    out[0] = fma(kd[s][0], vr[1], fma(ks[s][0], vr[0], -cof(s, 0)));
+    out[1] = fma(kd[s][1], vr[1], fma(ks[s][1], vr[0], -cof(s, 1)));
+    out[2] = fma(ks[s][2], vr[0], fma(kpv(s), vprev, -cof(s, 2)));
     if constexpr (ICE) {
-      out[3] = fma(kb[0], vr[3], fma(ka[0], vr[2], fma(kd[3], vr[1], -cof(3))));
-      out[4] = fma(kb[1], vr[3], fma(ka[1], vr[2], -cof(4)));
+      out[3] = fma(kb[s][0], vr[3], fma(ka[s][0], vr[2], fma(kd[s][3], vr[1], -cof(s, 3))));
+      out[4] = fma(kb[s][1], vr[3], fma(ka[s][1], vr[2], -cof(s, 4)));
     }
   };
-  auto kown_q = [&](const double (&v)[NC], double (&os)[NR]) {
-    os[0] = fma(ks[2], v[2], fma(ks[1], v[1], fma(ks[0], v[0], -q[0])));
-    os[1] = fma(kd[1], v[1], fma(kd[0], v[0], -q[1]));
+  auto kown_q = [&](int s, const double (&v)[NC], double (&os)[NR]) {
+    os[0] = fma(ks[s][2], v[2], fma(ks[s][1], v[1], fma(ks[s][0], v[0], -qv(s, 0))));
+    os[1] = fma(kd[s][1], v[1], fma(kd[s][0], v[0], -qv(s, 1)));
     if constexpr (ICE) {
-      os[1] = fma(kd[3], v[3], os[1]);
-      os[2] = fma(ka[1], v[4], fma(ka[0], v[3], -rhs(2)));
-      os[3] = fma(kb[1], v[4], fma(kb[0], v[3], -rhs(3)));
+      os[1] = fma(kd[s][3], v[3], os[1]);
+      os[2] = fma(ka[s][1], v[4], fma(ka[s][0], v[3], -rhs(s, 2)));
+      os[3] = fma(kb[s][1], v[4], fma(kb[s][0], v[3], -rhs(s, 3)));
     }
   };
-  // per-lane partial K'y of the tau columns from the DCM row's value
-  auto tau_parts = [&](double vd) {
+  // per-lane partial K'y of the tau columns from the DCM rows' values vd[s] (steps summed in order)
+  auto tau_parts = [&](const double (&vd)[S]) {
     if (J == 1) {
-      TP[tid] = kd[2] * vd;
+      double a = kd[0][2] * vd[0];
+#pragma unroll
+      for (int s = 1; s < S; ++s) a = fma(kd[s][2], vd[s], a);
+      TP[tid] = a;
     } else {
-      for (int j = 0; j < J; ++j) TP[j * B + tid] = (jt == j ? kd[2] : 0.0) * vd;
+      for (int j = 0; j < J; ++j) {
+        double a = (jt[0] == j ? kd[0][2] : 0.0) * vd[0];
+#pragma unroll
+        for (int s = 1; s < S; ++s) a = fma(jt[s] == j ? kd[s][2] : 0.0, vd[s], a);
+        TP[j * B + tid] = a;
+      }
     }
+  };
+  auto tau_parts_of = [&](const double (&vr)[S][NR]) {
+    double vd[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) vd[s] = vr[s][1];
+    tau_parts(vd);
   };
   // wave 0: lane j < J gets the sum over all lanes of TP[j][.] (fixed order; uniform per column)
   auto tau_kt = [&]() {
@@ -396,17 +500,23 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
   if (o.power_iters > 0) {
     const int P = o.power_iters;
     const double v0 = 1.0 / sqrt((double)n);
-    double vc[NC];
+    double vc[S][NC];
 #pragma unroll
-    for (int v = 0; v < NC; ++v) vc[v] = val ? v0 : 0.0;
+    for (int s = 0; s < S; ++s)
+#pragma unroll
+      for (int v = 0; v < NC; ++v) vc[s][v] = val[s] ? v0 : 0.0;
     double vtau = (wid == 0 && lane < J) ? v0 : 0.0;
     double nv[2] = {0.0, 0.0};
-    double wr[NR];
+    double wr[S][NR];
 #pragma unroll
-    for (int r = 0; r < NR; ++r) wr[r] = 0.0;
+    for (int s = 0; s < S; ++s)
+#pragma unroll
+      for (int r = 0; r < NR; ++r) wr[s][r] = 0.0;
     for (int pi = 0; pi <= P; ++pi) {
       if (pi > 0) {
-        ktr(wr, YS[tid], vc);
+        const double ysp = YS[tid];
+#pragma unroll
+        for (int s = 0; s < S; ++s) ktr(s, wr[s], s == 0 ? ysp : wr[s > 0 ? s - 1 : 0][0], vc[s]);
         if (wid == 0) {
           const double kt = tau_kt();
           vtau = lane < J ? kt : 0.0;
@@ -415,18 +525,25 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
       if (pi >= P - 1) {
         double a = vtau * vtau;
 #pragma unroll
-        for (int v = 0; v < NC; ++v) a = fma(vc[v], vc[v], a);
+        for (int s = 0; s < S; ++s)
+#pragma unroll
+          for (int v = 0; v < NC; ++v) a = fma(vc[s][v], vc[s][v], a);
         nv[pi - (P - 1)] = a;
       }
       if (pi == P) break;
-      XE[tid] = vc[2];
+      XE[tid] = vc[0][2];
       if (wid == 0 && lane < J) XT[lane] = vtau;
       __syncthreads();
-      kown(vc, wr);
-      kfin(wr, XE[tid + 1]);
-      YS[tid + 1] = wr[0];
+      const double xen = XE[tid + 1];
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        kown(s, vc[s], wr[s]);
+        kfin_next(s, wr[s], s == S - 1 ? xen : vc[s < S - 1 ? s + 1 : s][2]);
+        kfin_tau(s, wr[s]);
+      }
+      YS[tid + 1] = wr[S - 1][0];
       if (ilane) YS[0] = sp[4] * XE[0];
-      tau_parts(wr[1]);
+      tau_parts_of(wr);
       __syncthreads();
     }
     block_sum<B, 2>(nv, red);
@@ -437,9 +554,9 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
     __syncthreads();
   }
   if (o.warm) {  // y images of the starting point
-    YS[tid + 1] = y[0];
+    YS[tid + 1] = y[S - 1][0];
     if (ilane) YS[0] = sp[0];
-    if (J > 0) tau_parts(y[1]);
+    if (J > 0) tau_parts_of(y);
     __syncthreads();
   }
   eta = uniform(eta);
@@ -481,6 +598,26 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
       }
     }
   };
+  // Lean form: the check iteration's T(z_k) (scaled) goes to the window's global workspace (the lane reads back only
+  // its own entries, at the check); padding steps write nothing
+  double* xim = w.vbuf + W.wn;
+  double* yim = w.wbuf + W.wm;
+  auto load_images = [&](double (&xp)[S][NC], double (&yp)[S][NR]) {
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      if constexpr (LI) {
+#pragma unroll
+        for (int v = 0; v < NC; ++v) xp[s][v] = val[s] ? xim[opaque(col(s, v))] : 0.0;
+        yp[s][0] = val[s] ? yim[opaque(t0 + s + 1)] : 0.0;
+        yp[s][1] = drow[s] >= 0 ? yim[opaque(drow[s])] : 0.0;
+      } else {
+#pragma unroll
+        for (int v = 0; v < NC; ++v) xp[s][v] = XP[(v * S + s) * B + tid];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) yp[s][r] = YP[(r * S + s) * B + tid];
+      }
+    }
+  };
   auto iterate = [&](auto chk_tag, auto w0_tag) __attribute__((always_inline)) {
     constexpr bool CHECK = decltype(chk_tag)::value;
     constexpr bool W0 = decltype(w0_tag)::value;
@@ -491,33 +628,48 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
     const double cb = readlane_f64(hw, kin - kbase), ca = 1.0 - cb;
     mv0 = mv1 = mv2 = mv3 = 0.0;
     // ---------------- primal half-step (reflected Halpern, rho = 1)
-    double kx[NR];  // own-column part of K x-bar for the dual half-step
+    double kx[S][NR];  // own-lane part of K x-bar for the dual half-step
     {
       double ta0 = 0.0, ta1 = 0.0;
-      if constexpr (W0) {
+      if constexpr (W0) {  // (0 + a == a: the first partials start the two chains)
+        ta0 = TP[lane];
+        if (NW > 1) ta1 = TP[kWave + lane];
 #pragma unroll
-        for (int r = 0; r < NW; r += 2) {
+        for (int r = 2; r < NW; r += 2) {
           ta0 += TP[r * kWave + lane];
           if (r + 1 < NW) ta1 += TP[(r + 1) * kWave + lane];
         }
       }
-      double kty[NC], xb[NC];
-      ktr_c(y, YS[tid], kty);
+      double kty[S][NC], xb[S][NC];
+      const double ysp = YS[tid];
 #pragma unroll
-      for (int v = 0; v < NC; ++v) {  // branch-free: padding steps have c = lo = hi = 0 and stay at 0
-        const double lo = v == 2 ? loe : 0.0;
-        const double p1 = vmin(vmax(fma(tau, kty[v], x[v]), lo), hib(v));
-        xb[v] = fma(2.0, p1, -x[v]);
-        if (CHECK) {
-          const double d = x[v] - p1, da = p1 - xa[v];
-          mv0 += d * d;
-          mv1 += da * da;
-          XP[v * B + tid] = p1;
+      for (int s = 0; s < S; ++s) ktr_c(s, y[s], s == 0 ? ysp : y[s > 0 ? s - 1 : 0][0], kty[s]);
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+#pragma unroll
+        for (int v = 0; v < NC; ++v) {  // branch-free: padding steps have c = lo = hi = 0 and stay at 0
+          const double lo = v == 2 ? loe[s] : 0.0;
+          const double p1 = vmin(vmax(fma(tau, kty[s][v], x[s][v]), lo), hib(s, v));
+          xb[s][v] = fma(2.0, p1, -x[s][v]);
+          if (CHECK) {
+            const double d = x[s][v] - p1, da = p1 - axv(s, v);
+            mv0 += d * d;
+            mv1 += da * da;
+            if constexpr (LI) {
+              if (val[s]) xim[opaque(col(s, v))] = p1;
+            } else {
+              XP[(v * S + s) * B + tid] = p1;
+            }
+          }
+          x[s][v] = fma(ca, xb[s][v], cb * axv(s, v));
         }
-        x[v] = fma(ca, xb[v], cb * xa[v]);
       }
-      XE[tid] = xb[2];
-      kown_q(xb, kx);
+      XE[tid] = xb[0][2];
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        kown_q(s, xb[s], kx[s]);
+        if (s < S - 1) kfin_next(s, kx[s], xb[s < S - 1 ? s + 1 : s][2]);  // the next step is the lane's own
+      }
       if constexpr (W0) {
         tau_update(uniform(wave_sum_dpp(ta0 + ta1)), ca, cb, chk_tag);
       } else {
@@ -527,21 +679,30 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
     lds_barrier();
     // ---------------- dual half-step
     {
-      kfin(kx, XE[tid + 1]);
+      kfin_next(S - 1, kx[S - 1], XE[tid + 1]);
 #pragma unroll
-      for (int r = 0; r < NR; ++r) {  // row 0 (SOE) is an equality; DCM / ICE rows are >=: duals stay >= 0
-        double p1 = fma(-sigma, kx[r], y[r]);
-        if (r > 0) p1 = vmax(p1, 0.0);
-        if (CHECK) {
-          const double d = y[r] - p1, da = p1 - ya[r];
-          mv2 += d * d;
-          mv3 += da * da;
-          YP[r * B + tid] = p1;
+      for (int s = 0; s < S; ++s) {
+        kfin_tau(s, kx[s]);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {  // row 0 (SOE) is an equality; DCM / ICE rows are >=: duals stay >= 0
+          double p1 = fma(-sigma, kx[s][r], y[s][r]);
+          if (r > 0) p1 = vmax(p1, 0.0);
+          if (CHECK) {
+            const double d = y[s][r] - p1, da = p1 - ayv(s, r);
+            mv2 += d * d;
+            mv3 += da * da;
+            if constexpr (LI) {
+              if (r == 0 && val[s]) yim[opaque(t0 + s + 1)] = p1;
+              else if (drow[s] >= 0) yim[opaque(drow[s])] = p1;
+            } else {
+              YP[(r * S + s) * B + tid] = p1;
+            }
+          }
+          y[s][r] = fma(ca, fma(2.0, p1, -y[s][r]), cb * ayv(s, r));
         }
-        y[r] = fma(ca, fma(2.0, p1, -y[r]), cb * ya[r]);
       }
-      YS[tid + 1] = y[0];
-      if (J > 0) tau_parts(y[1]);
+      YS[tid + 1] = y[S - 1][0];
+      if (J > 0) tau_parts_of(y);
       if (W0 || wid == 0) {  // init row (lane kInitLane): ene_0 = target
         if (ilane) {
           const double y0 = sp[0], ya0 = sp[1];
@@ -591,16 +752,13 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
     for (int u = 4; u < kNRed; ++u) acc[u] = 0.0;
     if (kkt) {
       // images of T(z_k) in XE / XT / YS / TP (rewritten from z after the check)
-      double xp[NC], yp[NR];
-#pragma unroll
-      for (int v = 0; v < NC; ++v) xp[v] = XP[v * B + tid];
-#pragma unroll
-      for (int r = 0; r < NR; ++r) yp[r] = YP[r * B + tid];
-      XE[tid] = xp[2];
-      YS[tid + 1] = yp[0];
+      double xp[S][NC], yp[S][NR];
+      load_images(xp, yp);
+      XE[tid] = xp[0][2];
+      YS[tid + 1] = yp[S - 1][0];
       if (ilane) YS[0] = sp[2];
       if (tlane) XT[lane] = sp[5];
-      if (J > 0) tau_parts(yp[1]);
+      if (J > 0) tau_parts_of(yp);
       lds_barrier();
       auto col_kkt = [&](int j, double kt, double cj, double loj, double hij, double xj) {
         const int jj = opaque(j);
@@ -616,24 +774,50 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
         acc[7] += qi * yi;
         acc[9] += r.y2;
       };
-      double kt[NC];
-      ktr(yp, YS[tid], kt);
-      if (val) {
+      const double ysp = YS[tid];
 #pragma unroll
-        for (int v = 0; v < NC; ++v) col_kkt(col(v), kt[v], cof(v), v == 2 ? loe : 0.0, hib(v), xp[v]);
+      for (int s = 0; s < S; ++s) {
+        double kt[NC];
+        ktr(s, yp[s], s == 0 ? ysp : yp[s > 0 ? s - 1 : 0][0], kt);
+        if (val[s]) {
+#pragma unroll
+          for (int v = 0; v < NC; ++v)
+            col_kkt(col(s, v), kt[v], cof(s, v), v == 2 ? loe[s] : 0.0, hib(s, v), xp[s][v]);
+        }
       }
       if (wid == 0 && J > 0) {
         const double ktt = tau_kt();
         if (tlane) col_kkt(3 * T + lane, ktt, sp[2], sp[3], sp[4], sp[5]);
       }
-      double kv[NR];
-      kown(xp, kv);
-      kfin(kv, XE[tid + 1]);
-      if (val) row_kkt(t + 1, kv[0], q[0], yp[0], false);
-      if (drow >= 0) row_kkt(drow, kv[1], q[1], yp[1], true);
-      if (ICE && val) {
-        row_kkt(ra, kv[2], rhs(2), yp[2], true);
-        row_kkt(rb, kv[3], rhs(3), yp[3], true);
+      const double xen = XE[tid + 1];
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        double kv[NR];
+        kown(s, xp[s], kv);
+        kfin_next(s, kv, s == S - 1 ? xen : xp[s < S - 1 ? s + 1 : s][2]);
+        kfin_tau(s, kv);
+        const int t = t0 + s;
+        if (val[s]) row_kkt(t + 1, kv[0], qv(s, 0), yp[s][0], false);
+        if (drow[s] >= 0) row_kkt(drow[s], kv[1], qv(s, 1), yp[s][1], true);
+        if constexpr (LI) {  // this check's T(z_k), unscaled, as the outputs
+          if (val[s]) {
+#pragma unroll
+            for (int v = 0; v < NC; ++v) {
+              const int j = opaque(col(s, v));
+              xo_g[j] = xp[s][v] * dcv[j];
+            }
+            const int i0 = opaque(t + 1);
+            yo_g[i0] = yp[s][0] * drv[i0];
+          }
+          if (drow[s] >= 0) {
+            const int i1 = opaque(drow[s]);
+            yo_g[i1] = yp[s][1] * drv[i1];
+          }
+        }
+        if (ICE && val[s]) {
+          row_kkt(ra[s], kv[2], rhs(s, 2), yp[s][2], true);
+          row_kkt(rb[s], kv[3], rhs(s, 3), yp[s][3], true);
+        }
       }
       if (ilane) row_kkt(0, sp[4] * XE[0], sp[3], sp[2], false);
     }
@@ -673,10 +857,27 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
       if (ddx > 1e-10 && ddy > 1e-10) pw = uniform(pw_update(ddy / ddx, pw, o.theta));
       tau = uniform(eta / pw);
       sigma = uniform(eta * pw);
+      double xp[S][NC], yp[S][NR];
+      load_images(xp, yp);
 #pragma unroll
-      for (int v = 0; v < NC; ++v) x[v] = xa[v] = XP[v * B + tid];
+      for (int s = 0; s < S; ++s) {
 #pragma unroll
-      for (int rr = 0; rr < NR; ++rr) y[rr] = ya[rr] = YP[rr * B + tid];
+        for (int v = 0; v < NC; ++v) {
+          x[s][v] = xp[s][v];
+          if constexpr (LA)
+            XA[(v * S + s) * B + tid] = x[s][v];
+          else
+            xa[s][v] = x[s][v];
+        }
+#pragma unroll
+        for (int rr = 0; rr < NR; ++rr) {
+          y[s][rr] = yp[s][rr];
+          if constexpr (LA)
+            YA[(rr * S + s) * B + tid] = y[s][rr];
+          else
+            ya[s][rr] = y[s][rr];
+        }
+      }
       if (ilane) sp[0] = sp[1] = sp[2];
       if (tlane) sp[0] = sp[1] = sp[5];
       kin = 0;
@@ -688,21 +889,24 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
       rprev = r;
     }
     if (restart || kkt) {  // the y images must hold z again (after a restart z = T(z_k))
-      YS[tid + 1] = y[0];
+      YS[tid + 1] = y[S - 1][0];
       if (ilane) YS[0] = sp[0];
-      if (J > 0) tau_parts(y[1]);
+      if (J > 0) tau_parts_of(y);
     }
     lds_barrier();
   }
-  // outputs: the last check's T(z_k), unscaled
-  if (val) {
+  // outputs: the last check's T(z_k), unscaled (the lean form wrote them at that check)
 #pragma unroll
-    for (int v = 0; v < NC; ++v) xo_g[col(v)] = XP[v * B + tid] * dcv[col(v)];
-    yo_g[t + 1] = YP[tid] * drv[t + 1];
-    if (drow >= 0) yo_g[drow] = YP[B + tid] * drv[drow];
+  for (int s = 0; s < S; ++s) {
+    if (LI || !val[s]) continue;
+    const int t = t0 + s;
+#pragma unroll
+    for (int v = 0; v < NC; ++v) xo_g[col(s, v)] = XP[(v * S + s) * B + tid] * dcv[col(s, v)];
+    yo_g[t + 1] = YP[s * B + tid] * drv[t + 1];
+    if (drow[s] >= 0) yo_g[drow[s]] = YP[(S + s) * B + tid] * drv[drow[s]];
     if (ICE) {
-      yo_g[ra] = YP[2 * B + tid] * drv[ra];
-      yo_g[rb] = YP[3 * B + tid] * drv[rb];
+      yo_g[ra[s]] = YP[(2 * S + s) * B + tid] * drv[ra[s]];
+      yo_g[rb[s]] = YP[(3 * S + s) * B + tid] * drv[rb[s]];
     }
   }
   if (tlane) xo_g[3 * T + lane] = sp[5] * dcv[3 * T + lane];
@@ -714,23 +918,49 @@ __global__ __launch_bounds__(B, 3) void pdhg_band_kernel(const Batch b, const Wo
   }
 }
 
-template <bool ICE>
+template <int B, int S, bool ICE, int LF, int WPS>
 hipError_t launch_band_one(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, hipStream_t s,
-                           const int32_t* list, int nlist) {
-  constexpr int B = kBandB;
-  const size_t lds = band_lds_bytes(B, ICE);
-  auto kern = pdhg_band_kernel<B, ICE>;
+                           const int32_t* list, int nlist, int* variant_out) {
+  static_assert(B * S == kBandSteps, "every form covers T <= kBandSteps");
+  const size_t lds = band_lds_bytes(B, S, ICE, LF);
+  auto kern = pdhg_band_kernel<B, S, ICE, LF, WPS>;
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
+  if (getenv("DVH_BAND_OCC")) {  // residency diagnostics (A/B helper)
+    int nb = -1, dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceProp_t pr;
+    hipGetDeviceProperties(&pr, dev);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kern, B, lds);
+    hipFuncAttributes fa;
+    hipFuncGetAttributes(&fa, (const void*)kern);
+    fprintf(stderr, "band<%d,%d,%d,%d>: lds %zu B, blocks/CU %d, lds/CU %zu, regs %d, local %zu\n", B, S, (int)ICE, LF,
+            lds, nb, (size_t)pr.maxSharedMemoryPerMultiProcessor, fa.numRegs, (size_t)fa.localSizeBytes);
+  }
   hipLaunchKernelGGL(kern, dim3(list ? nlist : ch.count), dim3(B), lds, s, b, w, ch, o, list);
+  if (variant_out) *variant_out = 9000000 + 1000 * (S - 1) + (ICE ? 100 : 0) + B / kWave;
   return hipGetLastError();
 }
 
 }  // namespace
 
+// Forms of the battery (non-ICE) band kernel.  form 3 (default): 256 threads = one wave per SIMD, three steps per
+// lane, <= 256 VGPRs = 2 waves per SIMD, so two windows share every CU (a 384-thread, two-step form with 3 waves
+// per SIMD was measured to run one window per CU in practice: its 6 waves cannot be placed 3 / 3 / 3 / 3); the
+// costs / right-hand sides in LDS keep its three steps' state in 256 VGPRs without spills in the iteration, and the
+// setup-only ints share the check images' LDS so that two windows fit one CU's LDS (74 KB each).  Measured
+// (profiles/r02x_band_forms.log): 0.51 vs 0.69 us per window-iteration per CU; with the images in the global
+// workspace (kLfImages) 5 % slower and 10x the HBM writes, with the anchors in LDS too (kLfAnchors) 8 % slower.
+// form 1: 768 threads, one step per lane, 12 waves, one window per CU (A/B, dvh_set_kernel_path 3).  The LP-relaxed
+// ICE windows keep the one-step form (twice the per-step state).
+#ifndef DVH_BAND3_LF
+#define DVH_BAND3_LF kLfCosts
+#endif
 hipError_t launch_pdhg_band(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, hipStream_t s, bool ice,
-                            const int32_t* list, int nlist) {
-  return ice ? launch_band_one<true>(b, w, ch, o, s, list, nlist) : launch_band_one<false>(b, w, ch, o, s, list, nlist);
+                            int form, const int32_t* list, int nlist, int* variant_out) {
+  if (ice) return launch_band_one<kBandSteps, 1, true, 0, 3>(b, w, ch, o, s, list, nlist, variant_out);
+  if (form == 1) return launch_band_one<kBandSteps, 1, false, 0, 3>(b, w, ch, o, s, list, nlist, variant_out);
+  return launch_band_one<kBandSteps / 3, 3, false, DVH_BAND3_LF, 2>(b, w, ch, o, s, list, nlist, variant_out);
 }
 
 }  // namespace dvh

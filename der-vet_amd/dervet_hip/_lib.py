@@ -7,7 +7,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libdervet_hip.so")
+# DVH_LIB: an alternative build of the same library (kernel A/B helpers under scripts/)
+LIB_PATH = os.environ.get("DVH_LIB") or os.path.join(HERE, "libdervet_hip.so")
 
 DVH_OK, DVH_ERR_ARG, DVH_ERR_HIP, DVH_ERR_UNSUPPORTED = 0, -1, -2, -3
 OPTIMAL, PRIMAL_INFEASIBLE, DUAL_INFEASIBLE, ITER_LIMIT, NUMERICAL = 0, 1, 2, 3, 4

@@ -108,6 +108,42 @@ def test_band_ell_and_generic_kernels_agree():
         assert abs(ra.iters - rc.iters) <= 32 and abs(rb.iters - rc.iters) <= 32
 
 
+@pytest.mark.parametrize("T", [743, 745, 768, 100, 2])
+def test_band_kernel_forms_agree(T):
+    """The battery band kernel's default form (3 steps per lane, 256 threads, two windows per CU) and its
+    one-step-per-lane form (768 threads) run the same iteration; only the tau partial sums are grouped differently.
+    Step counts T = 3k + 2 / 3k + 1 leave padding steps inside a lane; T = 768 fills every lane; two demand periods
+    (J = 2) take the per-column tau path.  Objectives within 1e-7 of each other (as the other cross-kernel checks;
+    the realistic lengths agree to 1e-9) and 1e-5 of HiGHS; iteration counts within two check periods except on the
+    degenerate two-step window, where the grouping of the sums moves the restart decisions."""
+    rng = np.random.default_rng(T)
+    G = 3
+    load = 400 + 200 * rng.random((G, T))
+    masks = np.zeros((2, T), bool)
+    masks[0, : (T + 1) // 2] = True
+    masks[1, (T + 1) // 2:] = True
+    bat = dict(E=rng.uniform(500, 2000, G), Pch=rng.uniform(100, 400, G), Pdis=rng.uniform(100, 400, G),
+               rte=rng.uniform(0.8, 0.95, G), sdr=rng.uniform(0, 1, G), soc_target=rng.uniform(0.3, 0.9, G),
+               ulsoc=0.95, llsoc=0.05, fixedOM=10.0, OMexpenses=rng.uniform(0, 5, G))
+    groups = [builder.battery_group(T, 1.0, load, bat, retail_price=rng.uniform(0.03, 0.2, (G, T)),
+                                    demand_masks=masks[:1], demand_prices=rng.uniform(5, 20, (G, 1))),
+              builder.battery_group(T, 1.0, load, bat, retail_price=rng.uniform(0.03, 0.2, (G, T)),
+                                    demand_masks=masks, demand_prices=rng.uniform(5, 20, (G, 2)))]
+    lps = _lps(groups)
+    out = {}
+    with BatchSolver(0) as s:
+        for path, variant in (("default", 9002004), ("band1", 9000012)):
+            s.set_kernel_path(path)
+            out[path] = s.solve(lps)
+            st = s.kernel_stats()
+            assert st["band_windows"] == len(lps) and st["variant"] == variant, (path, st)
+    for ra, rb in zip(out["default"], out["band1"]):
+        assert ra.status == rb.status == 0
+        assert abs(ra.obj - rb.obj) <= (1e-9 if T >= 100 else 1e-7) * max(1.0, abs(rb.obj))
+        assert T < 100 or abs(ra.iters - rb.iters) <= 64
+    _check(lps, out["default"], f"band form 3, T={T}")
+
+
 def test_band_kernel_config1_no_dcm(gpu_solver):
     """Config 1 (DA arbitrage, no demand charge: J = 0, no >= rows) takes the battery-banded kernel."""
     lps = _lps(scenarios.config1())
