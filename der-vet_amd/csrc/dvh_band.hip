@@ -679,10 +679,16 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
     lds_barrier();
     // ---------------- dual half-step
     {
-      kfin_next(S - 1, kx[S - 1], XE[tid + 1]);
+      // every LDS read of the half-step first (the next lane's ene, the tau columns' x-bar), before any LDS store:
+      // issued together, one wait instead of one per read
+      const double xen = XE[tid + 1];
+      double xtv[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s) xtv[s] = lds_ld(xta[s]);
+      kfin_next(S - 1, kx[S - 1], xen);
 #pragma unroll
       for (int s = 0; s < S; ++s) {
-        kfin_tau(s, kx[s]);
+        kx[s][1] = fma(kd[s][2], xtv[s], kx[s][1]);  // kfin_tau
 #pragma unroll
         for (int r = 0; r < NR; ++r) {  // row 0 (SOE) is an equality; DCM / ICE rows are >=: duals stay >= 0
           double p1 = fma(-sigma, kx[s][r], y[s][r]);
