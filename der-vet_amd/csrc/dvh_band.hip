@@ -127,7 +127,6 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
   // each [S][B]
   double* RO = YA + (LA ? NR * SB : 0);
   double* CQ = RO + (ICE ? 6 * SB : 0);  // [5 S][B] (kLfCosts)
-  static_assert(!(LF && ICE), "register relief is for the battery (+ DCM) kernel");
   static_assert(!LA || sizeof(double) * (NC + NR) * SB >= sizeof(int32_t) * (4 * SB + 4), "ints fit the anchors");
   constexpr bool IS = (LF & kLfAnchors) || (LF && !(LF & kLfImages));  // band_ints_shared(LF)
   int32_t* dcm = LA   ? reinterpret_cast<int32_t*>(XA)
@@ -359,6 +358,10 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
   int xta[S];
 #pragma unroll
   for (int s = 0; s < S; ++s) xta[s] = lds_addr(XT + jt[s]);
+  // row of step s's r-th row (SOE, DCM, ICE a, ICE b), or -1 where the step has none
+  auto row_of = [&](int s, int r) -> int {
+    return r == 0 ? (val[s] ? t0 + s + 1 : -1) : r == 1 ? drow[s] : (val[s] ? (r == 2 ? ra[s] : rb[s]) : -1);
+  };
   // Special state in wave 0 (registers sp[], meaning by lane): lane j < J holds tau column j {x, xa, c, lo, hi, x+};
   // lane kInitLane holds the init row (row 0: ene_0 = target) {y, ya, y+, q, coefficient, -}.
   constexpr int kInitLane = kWave - 1;
@@ -400,11 +403,13 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
   for (int s = 0; s < S; ++s) {
     if constexpr (LI) {  // the outputs hold the last KKT check's T(z_k): the starting point until the first one
       if (val[s]) {
-        const int t = t0 + s;
 #pragma unroll
         for (int v = 0; v < NC; ++v) xo_g[col(s, v)] = x[s][v] * dcv[col(s, v)];
-        yo_g[t + 1] = y[s][0] * drv[t + 1];
-        if (drow[s] >= 0) yo_g[drow[s]] = y[s][1] * drv[drow[s]];
+      }
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        const int i = row_of(s, r);
+        if (i >= 0) yo_g[i] = y[s][r] * drv[i];
       }
     } else {
 #pragma unroll
@@ -608,8 +613,11 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
       if constexpr (LI) {
 #pragma unroll
         for (int v = 0; v < NC; ++v) xp[s][v] = val[s] ? xim[opaque(col(s, v))] : 0.0;
-        yp[s][0] = val[s] ? yim[opaque(t0 + s + 1)] : 0.0;
-        yp[s][1] = drow[s] >= 0 ? yim[opaque(drow[s])] : 0.0;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          const int i = row_of(s, r);
+          yp[s][r] = i >= 0 ? yim[opaque(i)] : 0.0;
+        }
       } else {
 #pragma unroll
         for (int v = 0; v < NC; ++v) xp[s][v] = XP[(v * S + s) * B + tid];
@@ -698,8 +706,8 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
             mv2 += d * d;
             mv3 += da * da;
             if constexpr (LI) {
-              if (r == 0 && val[s]) yim[opaque(t0 + s + 1)] = p1;
-              else if (drow[s] >= 0) yim[opaque(drow[s])] = p1;
+              const int i = row_of(s, r);
+              if (i >= 0) yim[opaque(i)] = p1;
             } else {
               YP[(r * S + s) * B + tid] = p1;
             }
@@ -812,12 +820,11 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
               const int j = opaque(col(s, v));
               xo_g[j] = xp[s][v] * dcv[j];
             }
-            const int i0 = opaque(t + 1);
-            yo_g[i0] = yp[s][0] * drv[i0];
           }
-          if (drow[s] >= 0) {
-            const int i1 = opaque(drow[s]);
-            yo_g[i1] = yp[s][1] * drv[i1];
+#pragma unroll
+          for (int r = 0; r < NR; ++r) {
+            const int i = row_of(s, r);
+            if (i >= 0) yo_g[opaque(i)] = yp[s][r] * drv[opaque(i)];
           }
         }
         if (ICE && val[s]) {
@@ -959,12 +966,15 @@ hipError_t launch_band_one(const Batch& b, const Work& w, const Chunk& ch, const
 // workspace (kLfImages) 5 % slower and 10x the HBM writes, with the anchors in LDS too (kLfAnchors) 8 % slower.
 // form 1: 768 threads, one step per lane, 12 waves, one window per CU (A/B, dvh_set_kernel_path 3).  The LP-relaxed
 // ICE windows keep the one-step form (twice the per-step state).
+#ifndef DVH_BANDI_LF
+#define DVH_BANDI_LF 0
+#endif
 #ifndef DVH_BAND3_LF
 #define DVH_BAND3_LF kLfCosts
 #endif
 hipError_t launch_pdhg_band(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, hipStream_t s, bool ice,
                             int form, const int32_t* list, int nlist, int* variant_out) {
-  if (ice) return launch_band_one<kBandSteps, 1, true, 0, 3>(b, w, ch, o, s, list, nlist, variant_out);
+  if (ice) return launch_band_one<kBandSteps, 1, true, DVH_BANDI_LF, 3>(b, w, ch, o, s, list, nlist, variant_out);
   if (form == 1) return launch_band_one<kBandSteps, 1, false, 0, 3>(b, w, ch, o, s, list, nlist, variant_out);
   return launch_band_one<kBandSteps / 3, 3, false, DVH_BAND3_LF, 2>(b, w, ch, o, s, list, nlist, variant_out);
 }

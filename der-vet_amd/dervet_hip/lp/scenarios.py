@@ -272,9 +272,13 @@ def config5(scenarios, years=20, start_year=2017, min_soe=None, cap_min_soe=Fals
             emin = np.minimum(emin, (bat["ulsoc"] * E)[:, None])
     groups = []
     for y in range(years):
-        groups += windows_by_period(start_year + y, 1.0, load, gen, bat, tariff_def=tariff(),
-                                    demand_price_override=P["demand"], price_scale=P["price_scale"],
-                                    ene_min=emin, ice=ice, tags_prefix=scen)
+        gy = windows_by_period(start_year + y, 1.0, load, gen, bat, tariff_def=tariff(),
+                               demand_price_override=P["demand"], price_scale=P["price_scale"],
+                               ene_min=emin, ice=ice, tags_prefix=scen)
+        if y > 0:  # window ids unique over the horizon (12 y + month): several opt years can share one sweep batch
+            for g in gy:
+                g.tags = [(t[0], 12 * y + t[1]) for t in g.tags]
+        groups += gy
     return groups
 
 
