@@ -1,8 +1,9 @@
 """Warm-phase parameter sweep (dev helper): the seeded config-4 schedule with different dvh_options for the warm
 phase only.  Prints warm-phase iterations and kernel time per variant.
 
-Usage: python scripts/warm_params.py <scenarios>
+Usage: python scripts/warm_params.py <scenarios> ['<json list of warm-option dicts>']
 """
+import json
 import os
 import sys
 
@@ -26,6 +27,7 @@ VARIANTS = [
 
 def main():
     S = int(sys.argv[1]) if len(sys.argv) > 1 else 4000
+    variants = json.loads(sys.argv[2]) if len(sys.argv) > 2 else VARIANTS
     ids = np.arange(S)
     P = scenarios.sweep_parameters(ids)
     sw = SeededSweep(scenarios.config4, ids, P["E"], stride=32, features=scenarios.sweep_features(P))
@@ -33,7 +35,7 @@ def main():
     s = BatchSolver(0)
     ns = sw.n_seed
     base = None
-    for v in VARIANTS:
+    for v in variants:
         tms = []
         for rep in range(2):
             tm, _ = sw.solve(s, dev, warm_options=v)

@@ -70,6 +70,25 @@ def test_seeded_packing_and_transfer_on_host():
     assert sb.c0.shape[0] == sb.count and sb.stats.shape[0] == sb.count
 
 
+def test_multi_year_config5_sweep_pairs_windows_of_the_same_year_and_month():
+    """Config 5 is solved several opt years per batch (bench_configs.py --c5-batch-years): window ids run 12 y +
+    month over the horizon, so every warm window starts from its seed's window of the same year and month."""
+    ids = np.arange(8)
+    keys = scenarios.sweep_parameters(ids)["E"]
+    sw = SeededSweep(lambda v: scenarios.config5(v, years=2), ids, keys, stride=4)
+    assert sorted(sw.tags) == sorted((int(s), w) for s in ids for w in range(24))
+    desc = np.asarray(sw.packed.desc)
+    tag_at = {int(desc[k, 6]): sw.tags[k] for k in range(sw.packed.count)}
+    checked = 0
+    for tr in sw.transfers:
+        for i in range(tr.g_rest):
+            rest = tag_at[tr.on_rest + i * tr.n]
+            seed = tag_at[tr.on_seed + int(tr.local[i]) * tr.n]
+            assert rest[1] == seed[1] and seed[0] in set(int(s) for s in sw.seed_ids)
+            checked += 1
+    assert checked == sw.packed.count - sw.n_seed
+
+
 @pytest.mark.gpu
 def test_seeded_sweep_on_gpu_matches_cold_and_highs():
     from dervet_hip import BatchSolver
