@@ -113,7 +113,7 @@ def test_band_kernel_forms_agree(T):
     """The battery band kernel's default form (3 steps per lane, 256 threads, two windows per CU) and its
     one-step-per-lane form (768 threads) run the same iteration; only the tau partial sums are grouped differently.
     Step counts T = 3k + 2 / 3k + 1 leave padding steps inside a lane; T = 768 fills every lane; two demand periods
-    (J = 2) take the per-column tau path.  Objectives within 1e-7 of each other (as the other cross-kernel checks;
+    (J = 2, 4) take the per-column tau path.  Objectives within 1e-7 of each other (as the other cross-kernel checks;
     the realistic lengths agree to 1e-9) and 1e-5 of HiGHS; iteration counts within two check periods except on the
     degenerate two-step window, where the grouping of the sums moves the restart decisions."""
     rng = np.random.default_rng(T)
@@ -129,6 +129,12 @@ def test_band_kernel_forms_agree(T):
                                     demand_masks=masks[:1], demand_prices=rng.uniform(5, 20, (G, 1))),
               builder.battery_group(T, 1.0, load, bat, retail_price=rng.uniform(0.03, 0.2, (G, T)),
                                     demand_masks=masks, demand_prices=rng.uniform(5, 20, (G, 2)))]
+    if T >= 4:  # J = 4 (the kernel's limit): four interleaved demand periods, every step in one of them
+        m4 = np.zeros((4, T), bool)
+        for j in range(4):
+            m4[j, j::4] = True
+        groups.append(builder.battery_group(T, 1.0, load, bat, retail_price=rng.uniform(0.03, 0.2, (G, T)),
+                                            demand_masks=m4, demand_prices=rng.uniform(5, 20, (G, 4))))
     lps = _lps(groups)
     out = {}
     with BatchSolver(0) as s:
