@@ -62,6 +62,7 @@ struct dvh_handle {
   DevBuf m_list, m_plan, m_pos, m_xbuf, m_abort;  // medium tier (dvh_chain.hip)
   int chain_cap = -1;                             // resident 768-thread workgroups (cooperative limit)
   DevBuf o_data, o_cases, o_len, o_hist, o_soe;  // reliability sweep
+  DevBuf s_pairs, s_bad;                          // seeded-sweep warm transfer (dvh_sweep.hip)
   double outage_ms = 0.0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<std::array<hipEvent_t, 3>> chunk_events;
@@ -215,7 +216,8 @@ int dvh_destroy(dvh_handle* h) {
                     &h->d_u, &h->d_list, &h->d_hinv, &h->d_x, &h->d_y, &h->d_stats, &h->d_istats, &h->w_tptr, &h->w_tind, &h->w_tval,
                     &h->w_kval, &h->w_rowof, &h->w_perm, &h->w_dr, &h->w_dc, &h->w_cs, &h->w_ls, &h->w_us,
                     &h->w_qs, &h->w_vbuf, &h->w_wbuf, &h->w_tmpc, &h->w_tmpr, &h->w_longk, &h->w_longt, &h->w_scal,
-                    &h->m_list, &h->m_plan, &h->m_pos, &h->m_xbuf, &h->m_abort, &h->o_data, &h->o_cases, &h->o_len, &h->o_hist, &h->o_soe};
+                    &h->m_list, &h->m_plan, &h->m_pos, &h->m_xbuf, &h->m_abort, &h->o_data, &h->o_cases, &h->o_len, &h->o_hist, &h->o_soe,
+                    &h->s_pairs, &h->s_bad};
   for (DevBuf* b : bufs) b->release();
   for (auto& e : h->ev)
     if (e) hipEventDestroy(e);
@@ -226,6 +228,32 @@ int dvh_destroy(dvh_handle* h) {
 }
 
 const char* dvh_last_error(const dvh_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
+int dvh_warm_transfer(dvh_handle* h, const dvh_packed* b, const int32_t* pairs, int32_t count) {
+  if (!h) return DVH_ERR_ARG;
+  if (count < 0 || (count > 0 && (!b || !pairs))) return fail(h, DVH_ERR_ARG, "warm transfer: bad arguments");
+  if (count == 0) return DVH_OK;
+  if (!b->desc || !b->c || !b->u || !b->x || !b->y) return fail(h, DVH_ERR_ARG, "null device array in packed batch");
+  for (int32_t i = 0; i < count; ++i) {
+    const int32_t w = pairs[3 * (size_t)i], p = pairs[3 * (size_t)i + 1];
+    if (w < 0 || w >= b->count || p < 0 || p >= b->count || w == p)
+      return fail(h, DVH_ERR_ARG, "warm transfer: pair " + std::to_string(i) + " names no window / itself");
+  }
+  DVH_HIP(h, hipSetDevice(h->device));
+  hipStream_t s = h->stream;
+  DVH_HIP(h, h->s_pairs.ensure(sizeof(int32_t) * 3 * (size_t)count));
+  DVH_HIP(h, h->s_bad.ensure(sizeof(int32_t)));
+  DVH_HIP(h, hipMemcpyAsync(h->s_pairs.p, pairs, sizeof(int32_t) * 3 * (size_t)count, hipMemcpyHostToDevice, s));
+  DVH_HIP(h, hipMemsetAsync(h->s_bad.p, 0, sizeof(int32_t), s));
+  hipError_t e = dvh::launch_warm_transfer(b->desc, b->c, b->u, b->x, b->y, h->s_pairs.as<int32_t>(), count,
+                                           h->s_bad.as<int32_t>(), s);
+  if (e != hipSuccess) return hip_fail(h, e, "launch_warm_transfer");
+  int32_t bad = 0;
+  DVH_HIP(h, hipMemcpyAsync(&bad, h->s_bad.p, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  DVH_HIP(h, hipStreamSynchronize(s));
+  if (bad) return fail(h, DVH_ERR_ARG, "warm transfer: " + std::to_string(bad) + " pair(s) of different LP shape");
+  return DVH_OK;
+}
 
 int dvh_synchronize(dvh_handle* h) {
   if (!h) return DVH_ERR_ARG;

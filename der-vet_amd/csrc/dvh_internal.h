@@ -113,6 +113,10 @@ size_t chain_abort_bytes(int S);  // abort word, window counter, per-workgroup d
 int chain_team_count(int S, int PT);
 hipError_t launch_chain(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, const int32_t* pos, int npos,
                         const int32_t* plan, int PT, int S, void* xbuf, int32_t* abort_word, hipStream_t s);
+// Seeded-sweep warm starts (dvh_sweep.hip): pairs[count][3] = {window, partner window, T (> 0: battery + DCM dual
+// scaling) }; bad counts pairs whose windows differ in shape (skipped).
+hipError_t launch_warm_transfer(const int64_t* desc, const double* c, const double* u, double* x, double* y,
+                                const int32_t* pairs, int count, int32_t* bad, hipStream_t s);
 // Power iteration for ||Kt||_2 of the listed windows (generic path; the ELL kernel does its own on chip).
 hipError_t launch_power(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, const int32_t* list, int nlist,
                         hipStream_t s);

@@ -17,6 +17,7 @@ point changes (``scripts/warm_study.py``: 3,351 -> 2,316 mean iterations on conf
 neighbour).  The two phases are two ``dvh_solve_packed_device`` calls on sub-ranges of ONE packed batch (seed
 windows packed first), and the transfer between them is a device-side gather on the solver's stream.
 """
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -89,6 +90,8 @@ class _Transfer:
     local: object        # [g_rest] index into the seed group
     battery_dcm: bool    # x = [ch, dis, ene, tau (1)]: scale the duals too
     T: int
+    w_rest: int = 0      # window index of the rest group's first window (packing order)
+    w_seed: int = 0      # and of the seed group's
 
 
 def _window_id(tag):
@@ -110,26 +113,51 @@ def plan(seed_groups, rest_groups, partner_of):
     partner_of: dict rest scenario id -> seed scenario id.  Groups are matched by window id (tag[1]) and must
     share the CSR pattern."""
     out = []
-    on = om = 0
+    on = om = wk = 0
     seed_at = {}
     for g in seed_groups:
-        seed_at[_window_id(g.tags[0])] = (g, on, om)
+        seed_at[_window_id(g.tags[0])] = (g, on, om, wk)
         on += g.G * g.n
         om += g.G * g.m
+        wk += g.G
     for g in rest_groups:
         wid = _window_id(g.tags[0])
         if wid not in seed_at:
             raise ValueError(f"no seed group for window {wid!r}")
-        sg, son, som = seed_at[wid]
+        sg, son, som, swk = seed_at[wid]
         if not _same_pattern(sg, g):
             raise ValueError(f"seed and rest groups of window {wid!r} differ in pattern")
         col = {t[0]: i for i, t in enumerate(sg.tags)}
         local = np.array([col[partner_of[t[0]]] for t in g.tags], np.int64)
         out.append(_Transfer(on, om, son, som, g.n, g.m, g.G, sg.G, local,
-                             g.n == 3 * g.T + 1 and g.J == 1, g.T))
+                             g.n == 3 * g.T + 1 and g.J == 1, g.T, wk, swk))
         on += g.G * g.n
         om += g.G * g.m
+        wk += g.G
     return out
+
+
+def transfer_pairs(tr_list):
+    """int32 [windows][3] {window, partner window, T (> 0: battery + DCM dual scaling)} of the transfers, for
+    ``dvh_warm_transfer`` (the same warm starts as ``transfer``, in one launch on the solver's stream)."""
+    parts = []
+    for t in tr_list:
+        p = np.empty((t.g_rest, 3), np.int32)
+        p[:, 0] = t.w_rest + np.arange(t.g_rest)
+        p[:, 1] = t.w_seed + np.asarray(t.local, np.int64)
+        p[:, 2] = t.T if t.battery_dcm else 0
+        parts.append(p)
+    return np.ascontiguousarray(np.concatenate(parts)) if parts else np.zeros((0, 3), np.int32)
+
+
+def transfer_device(solver, tr_list, pb, pairs=None):
+    """``transfer`` for a device-resident batch through the library (``dvh_warm_transfer``): one launch on the
+    solver's stream, ordered after the seed solve and before the warm one; no host-side tensor work."""
+    import ctypes
+    pairs = transfer_pairs(tr_list) if pairs is None else pairs
+    p = pb.as_ctypes()
+    solver._check(solver._lib.dvh_warm_transfer(solver._h, ctypes.byref(p), pairs.ctypes.data_as(ctypes.c_void_p),
+                                                len(pairs)), "dvh_warm_transfer")
 
 
 def transfer(tr_list, x, y, c, u):
@@ -179,6 +207,7 @@ class SeededSweep:
         sg = make_groups(self.seed_ids)
         rg = make_groups(self.rest_ids) if len(self.rest_ids) else []
         self.transfers = plan(sg, rg, partner_of)
+        self.pairs = transfer_pairs(self.transfers)
         self.n_seed = sum(g.G for g in sg)
         self.tags = [t for g in sg + rg for t in g.tags]
         self.specs = None
@@ -202,7 +231,6 @@ class SeededSweep:
         warm_options: dvh_options fields for the warm phase only (restored afterwards; None: WARM_OPTIONS).
         Returns the kernel timings {setup_ms, pdhg_ms, total_ms} and the windows per kernel path, summed over
         the two phases."""
-        import torch
         cnt = dev.count
         o0 = solver.options()
         warm_options = dict(WARM_OPTIONS if warm_options is None else warm_options)
@@ -225,12 +253,14 @@ class SeededSweep:
             solver.set_options(warm_start=o0.warm_start)
         account()
         if cnt > self.n_seed:
-            stream = torch.cuda.current_stream(dev.x.device) if dev.x.is_cuda else None
-            if stream is not None:
-                torch.cuda.synchronize(dev.x.device)  # seeds solved (library stream) before the gather reads them
-            transfer(self.transfers, dev.x, dev.y, dev.c, dev.u)
-            if stream is not None:
-                torch.cuda.synchronize(dev.x.device)
+            if dev.x.is_cuda and not os.environ.get("DVH_SWEEP_TORCH_TRANSFER"):
+                # one launch on the library's stream (the seed solve has completed on it)
+                transfer_device(solver, self.transfers, dev, self.pairs)
+            else:  # host tensors (tests), or the torch formulation for A/B timing
+                transfer(self.transfers, dev.x, dev.y, dev.c, dev.u)
+                if dev.x.is_cuda:
+                    import torch
+                    torch.cuda.synchronize(dev.x.device)  # before the library's stream reads the warm starts
             solver.set_options(warm_start=1, **warm_options)
             try:
                 solver.solve_packed(sub_batch(dev, self.n_seed, cnt))

@@ -186,6 +186,17 @@ typedef struct dvh_battery_group {
 int dvh_build_battery_group(dvh_handle* h, const dvh_battery_group* group, const dvh_packed* batch, int32_t first);
 int dvh_synchronize(dvh_handle* h);
 
+/* ---- Seeded scenario sweeps (dervet_hip/sweep.py; the sensitivity cases of dervet/DERVET.py:75 solve the same
+ * windows for many perturbed scenarios; no reference counterpart: the reference solves every window cold).
+ * Warm starts for `count` windows of a device-resident packed batch from solved partner windows of the same LP
+ * shape, in one launch on the handle's stream (ordered with the solves; returns after it completed).
+ * pairs (host, int32 [count][3]): {window, partner window, T}.  x <- the partner's x scaled per column by
+ * u_window / u_partner where both are finite and u_partner > 0, else copied; T > 0 (battery + DCM shape,
+ * n = 3T + 1): the duals of rows 0..T scaled by mean|c_window[0:T]| / mean|c_partner[0:T]| and the others by
+ * c_window[3T] / c_partner[3T] (denominators clamped at 1e-12); T <= 0: duals copied.  DVH_ERR_ARG for a pair
+ * naming no window or windows of different shape. */
+int dvh_warm_transfer(dvh_handle* h, const dvh_packed* batch, const int32_t* pairs, int32_t count);
+
 /* Timing of the most recent solve on the handle's stream (HIP events, milliseconds):
  * [0] whole solve, [1] setup kernel (transpose + scaling + power iteration), [2] PDHG kernel. */
 int dvh_last_timing(const dvh_handle* h, double* ms3);

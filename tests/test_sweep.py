@@ -10,7 +10,7 @@ import pytest
 import torch
 
 from dervet_hip.lp import builder, scenarios
-from dervet_hip.sweep import SeededSweep, seed_split, sub_batch, transfer
+from dervet_hip.sweep import SeededSweep, seed_split, sub_batch, transfer, transfer_pairs
 
 
 def test_seed_split_partners_are_nearest_in_key_order():
@@ -68,6 +68,45 @@ def test_seeded_packing_and_transfer_on_host():
     sb = sub_batch(pb, sw.n_seed, pb.count)
     assert sb.count == pb.count - sw.n_seed and int(sb.desc[0, 6]) == ns_n
     assert sb.c0.shape[0] == sb.count and sb.stats.shape[0] == sb.count
+
+
+def test_transfer_pairs_name_each_rest_window_and_its_seed_partner():
+    ids = np.arange(12)
+    keys = scenarios.sweep_parameters(ids)["E"]
+    sw = SeededSweep(scenarios.config4, ids, keys, stride=4)
+    pairs = transfer_pairs(sw.transfers)
+    assert pairs.dtype == np.int32 and pairs.shape == (sw.packed.count - sw.n_seed, 3)
+    assert sorted(pairs[:, 0].tolist()) == list(range(sw.n_seed, sw.packed.count))
+    seeds = set(int(s) for s in sw.seed_ids)
+    for w, p, T in pairs:
+        assert p < sw.n_seed and sw.tags[p][0] in seeds and sw.tags[p][1] == sw.tags[w][1]
+        assert T == int(sw.desc[w, 2]) - 1  # battery + DCM windows: dual scaling with the window's T
+
+
+@pytest.mark.gpu
+def test_device_transfer_equals_host_transfer():
+    """dvh_warm_transfer (one launch) gives the torch transfer's warm starts: x bit for bit, y to rounding (the
+    mean |c| is summed in another order)."""
+    from dervet_hip import BatchSolver
+    from dervet_hip.sweep import transfer_device
+    ids = np.arange(40)
+    keys = scenarios.sweep_parameters(ids)["E"]
+    sw = SeededSweep(scenarios.config4, ids, keys, stride=8)
+    host = sw.packed.to_torch("cpu").alloc_outputs()
+    g = torch.Generator().manual_seed(1)
+    host.x.copy_(torch.randn(host.x.shape, generator=g, dtype=torch.float64))
+    host.y.copy_(torch.randn(host.y.shape, generator=g, dtype=torch.float64))
+    dev = sw.packed.to_torch("cuda:0").alloc_outputs()
+    dev.x.copy_(host.x)
+    dev.y.copy_(host.y)
+    transfer(sw.transfers, host.x, host.y, host.c, host.u)
+    with BatchSolver(0) as s:
+        transfer_device(s, sw.transfers, dev)
+        bad = np.array([[0, 0, 0]], np.int32)  # a window paired with itself
+        with pytest.raises(Exception):
+            transfer_device(s, sw.transfers, dev, bad)
+    assert torch.equal(dev.x.cpu(), host.x)
+    np.testing.assert_allclose(dev.y.cpu().numpy(), host.y.numpy(), rtol=1e-14, atol=0)
 
 
 def test_multi_year_config5_sweep_pairs_windows_of_the_same_year_and_month():
