@@ -1735,8 +1735,12 @@ hipError_t small_dispatch(int max_n, int max_m, int wx, int wy, const Batch& b, 
   // which the register-resident KR variants do not take)
   DVH_SMALL(5, 128, 3, 4, 6, 8, 0, 2)
   // ... with CombinedMarket load following (one more equality block: n = 17 T = 408, m ~ 22 T at T = 24; the LF
-  // columns sit in 5 rows, beyond the 512-thread kernels' K^T width 4)
-  DVH_SMALL(6, 256, 2, 3, 6, 8, 0, 2)
+  // columns sit in 5 rows, beyond the 512-thread kernels' K^T width 4).  Only for those: windows the 512-thread
+  // kernels take (K^T width <= 4, e.g. load following without CombinedMarket, m just above 512) run 2.9x faster
+  // there (profiles/r02zj_market_variants.log)
+  if (wx > 4 || sv == 6) {
+    DVH_SMALL(6, 256, 2, 3, 6, 8, 0, 2)
+  }
 #undef DVH_SMALL
   return hipErrorInvalidValue;
 }

@@ -113,7 +113,11 @@ def test_load_following_windows_match_highs(gpu_solver, combined):
     g = scenarios.market_days(sig, meta["params"], days=days, reserves=reserve_series(sig, pdis),
                               lf=_lf(sig, pdis, combined=combined))
     res = gpu_solver.solve(builder.group_window_lps(g))
-    assert gpu_solver.kernel_stats()["ell_windows"] == len(days), gpu_solver.kernel_stats()
+    st = gpu_solver.kernel_stats()
+    assert st["ell_windows"] == len(days), st
+    # CombinedMarket LF (K^T width 5) takes the 256-thread small variant 6; without it (width <= 4) the 512-thread
+    # ELL kernel, 2.9x faster on these days (profiles/r02zj_market_variants.log)
+    assert (st["variant"] == 2680423) == combined, st
     # the oracle's direct form (options written into the SOE rows, no aggregate columns; tests/test_market_reserves)
     from test_market_reserves import _oracle_window
     wins, _ = cases.market_windows("es")
