@@ -234,11 +234,18 @@ int dvh_warm_transfer(dvh_handle* h, const dvh_packed* b, const int32_t* pairs, 
   if (count < 0 || (count > 0 && (!b || !pairs))) return fail(h, DVH_ERR_ARG, "warm transfer: bad arguments");
   if (count == 0) return DVH_OK;
   if (!b->desc || !b->c || !b->u || !b->x || !b->y) return fail(h, DVH_ERR_ARG, "null device array in packed batch");
+  // every window written once, and no partner written (a workgroup would read it while another writes it)
+  std::vector<char> target((size_t)std::max(b->count, 0), 0);
   for (int32_t i = 0; i < count; ++i) {
     const int32_t w = pairs[3 * (size_t)i], p = pairs[3 * (size_t)i + 1];
     if (w < 0 || w >= b->count || p < 0 || p >= b->count || w == p)
       return fail(h, DVH_ERR_ARG, "warm transfer: pair " + std::to_string(i) + " names no window / itself");
+    if (target[w]) return fail(h, DVH_ERR_ARG, "warm transfer: window " + std::to_string(w) + " listed twice");
+    target[w] = 1;
   }
+  for (int32_t i = 0; i < count; ++i)
+    if (target[pairs[3 * (size_t)i + 1]])
+      return fail(h, DVH_ERR_ARG, "warm transfer: partner of pair " + std::to_string(i) + " is itself a listed window");
   DVH_HIP(h, hipSetDevice(h->device));
   hipStream_t s = h->stream;
   DVH_HIP(h, h->s_pairs.ensure(sizeof(int32_t) * 3 * (size_t)count));

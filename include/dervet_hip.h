@@ -194,7 +194,8 @@ int dvh_synchronize(dvh_handle* h);
  * u_window / u_partner where both are finite and u_partner > 0, else copied; T > 0 (battery + DCM shape,
  * n = 3T + 1): the duals of rows 0..T scaled by mean|c_window[0:T]| / mean|c_partner[0:T]| and the others by
  * c_window[3T] / c_partner[3T] (denominators clamped at 1e-12); T <= 0: duals copied.  DVH_ERR_ARG for a pair
- * naming no window or windows of different shape. */
+ * naming no window, a window listed twice, a partner that is itself listed (checked before the launch), or windows
+ * of different shape (those pairs are skipped, the others applied). */
 int dvh_warm_transfer(dvh_handle* h, const dvh_packed* batch, const int32_t* pairs, int32_t count);
 
 /* Timing of the most recent solve on the handle's stream (HIP events, milliseconds):

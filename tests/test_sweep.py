@@ -102,9 +102,11 @@ def test_device_transfer_equals_host_transfer():
     transfer(sw.transfers, host.x, host.y, host.c, host.u)
     with BatchSolver(0) as s:
         transfer_device(s, sw.transfers, dev)
-        bad = np.array([[0, 0, 0]], np.int32)  # a window paired with itself
-        with pytest.raises(Exception):
-            transfer_device(s, sw.transfers, dev, bad)
+        for bad in ([[0, 0, 0]],                 # a window paired with itself
+                    [[5, 1, 0], [1, 2, 0]],      # a partner that is itself a listed window
+                    [[5, 1, 0], [5, 2, 0]]):     # a window listed twice
+            with pytest.raises(Exception):
+                transfer_device(s, sw.transfers, dev, np.array(bad, np.int32))
     assert torch.equal(dev.x.cpu(), host.x)
     np.testing.assert_allclose(dev.y.cpu().numpy(), host.y.numpy(), rtol=1e-14, atol=0)
 
