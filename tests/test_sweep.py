@@ -169,3 +169,29 @@ def test_seed_split_feature_partners_are_nearest_in_standardised_features():
     for r, p in zip(rest, pick):
         d = ((f[seeds] - f[r]) ** 2).sum(1)
         assert d[p] == d.min()
+
+
+@pytest.mark.gpu
+def test_config5_multi_year_seeded_sweep_on_gpu_matches_highs():
+    """BASELINE config 5 as bench_configs.py runs it: the GPU min-SOE requirement (dvh_outage_min_soe, capped at E),
+    several opt years in one seeded sweep batch (window ids 12 y + month), warm starts by dvh_warm_transfer, the
+    LP-relaxed ICE band kernel; every window optimal and within 1e-5 of HiGHS with primal residual <= 1e-6."""
+    from dervet_hip import BatchSolver
+    from oracle import cpu_baseline, window_lp
+    ids = np.arange(16)
+    with BatchSolver(0) as s:
+        ms = scenarios.config5_min_soe(ids, s)
+        P = scenarios.sweep_parameters(ids)
+        sw = SeededSweep(lambda v: scenarios.config5(v, years=2, min_soe=ms[np.asarray(list(v))], cap_min_soe=True),
+                         ids, P["E"], stride=8, features=scenarios.sweep_features(P))
+        dev = sw.packed.to_torch("cuda:0").alloc_outputs()
+        _, paths = sw.solve(s, dev)
+        st, ist = dev.stats.cpu().numpy(), dev.istats.cpu().numpy()
+    assert sw.packed.count == 16 * 24 and paths.get("band_windows", 0) == sw.packed.count, paths
+    assert (ist[:, 0] == 0).all()
+    lps = [window_lp.from_packed_window(sw.packed.window(k)) for k in range(sw.packed.count)]
+    hobj, hst, _, _ = cpu_baseline.highs_batch(lps, 8)
+    assert (hst == 0).all()
+    err = np.abs(st[:, 0] - hobj) / np.maximum(np.abs(hobj), 1.0)
+    assert err.max() <= 1e-5, (int(err.argmax()), float(err.max()))
+    assert st[:, 1].max() <= 1e-6
