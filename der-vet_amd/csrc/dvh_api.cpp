@@ -69,8 +69,9 @@ struct dvh_handle {
   double timing[3] = {0, 0, 0};
   int last_variant = -1;
   int n_ell = 0, n_generic = 0, n_large = 0, n_band = 0, n_chain = 0;
-  int kernel_path = 0;  // 0 band -> ELL -> generic, 1 generic only, 2 ELL -> generic (no band kernel), 3 as 0 with
-                        // the one-step-per-lane battery band kernel
+  int kernel_path = 0;  // 0 band -> ELL -> generic, 1 generic only, 2 ELL -> generic (no band kernel), 3 / 4 as 0
+                        // with the battery band kernel's one-step / three-step form forced (0 picks by batch size)
+  int cus = 0;          // compute units of the device (band kernel form choice)
   dvh::LargeSolver* large = nullptr;  // grid-wide path for windows above dvh::kSmallMax (created on first use)
   float large_ms[2] = {0, 0};         // setup, PDHG time of the large windows of the last solve
   // Further devices of this handle (device_mask bits after the first, or dvh_create_devices): same options; a
@@ -305,7 +306,7 @@ int dvh_last_path_counts4(const dvh_handle* h, int32_t* out4) {
 }
 
 int dvh_set_kernel_path(dvh_handle* h, int mode) {
-  if (!h || mode < 0 || mode > 3) return DVH_ERR_ARG;
+  if (!h || mode < 0 || mode > 4) return DVH_ERR_ARG;
   h->kernel_path = mode;
   for (dvh_handle* p : h->peers) p->kernel_path = mode;
   return DVH_OK;
@@ -620,7 +621,7 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
   };
   // medium tier candidates: battery-shaped sizes (n = 3T + J, m <= 2T + 1) up to kPMax segments of kChainB steps;
   // the plan kernel verifies the pattern, anything else goes to the grid-wide path
-  const bool chain_on = (h->kernel_path == 0 || h->kernel_path == 3) && o.rho == 1.0 && o.max_iters + o.power_iters < (1 << 17);
+  const bool chain_on = (h->kernel_path == 0 || h->kernel_path >= 3) && o.rho == 1.0 && o.max_iters + o.power_iters < (1 << 17);
   auto is_medium = [&](int k) {
     const int64_t* d = &desc[8 * (size_t)k];
     const int64_t T = d[2] - 1;
@@ -736,12 +737,19 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
     const bool fast = h->kernel_path != 1 && o.rho == 1.0;
     std::vector<int32_t> ell_list;  // empty + ell_all: the whole chunk
     bool ell_all = true;
-    if (fast && (h->kernel_path == 0 || h->kernel_path == 3)) {
-      const int band_form = h->kernel_path == 3 ? 1 : 3;
+    if (fast && (h->kernel_path == 0 || h->kernel_path >= 3)) {
+      // battery band kernel form: three steps per lane (two windows per CU) once the windows outnumber the CUs;
+      // a window alone on its CU is faster in the one-step form (0.75 vs 0.97 us per iteration,
+      // profiles/r02x_band_forms.log), e.g. one scenario's 12-36 monthly windows
+      if (h->cus <= 0 && hipDeviceGetAttribute(&h->cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess)
+        h->cus = 256;
+      const int forced_form = h->kernel_path == 3 ? 1 : h->kernel_path == 4 ? 3 : 0;
       // pass 1: battery (+ DCM) windows over the whole chunk; pass 2: the ICE variant over what pass 1 returned
       auto band_pass = [&](bool ice, const std::vector<int32_t>* in, std::vector<int32_t>& out) -> hipError_t {
         hipError_t r;
         int bvar = -1;
+        const int nl = in ? (int)in->size() : c.ch.count;
+        const int band_form = forced_form ? forced_form : (nl <= h->cus ? 1 : 3);
         if (in) {
           r = hipMemcpyAsync(h->d_list.p, in->data(), I * in->size(), hipMemcpyHostToDevice, s);
           if (r != hipSuccess) return r;

@@ -148,12 +148,13 @@ class BatchSolver:
         return {"band_windows": c[3], "ell_windows": v[0], "generic_windows": v[1], "variant": v[2],
                 "generic_only": bool(v[3]), "large_windows": c[2], "chain_windows": c[4]}
 
-    _PATHS = {"default": 0, "generic": 1, "ell": 2, "band1": 3}
+    _PATHS = {"default": 0, "generic": 1, "ell": 2, "band1": 3, "band3": 4}
 
     def set_kernel_path(self, path):
         """Kernel cascade: "default" (battery-banded -> ELL -> generic CSR), "ell" (ELL -> generic), "generic", or
-        "band1" (the default cascade with the one-step-per-lane, 768-thread battery band kernel instead of the
-        three-step, two-windows-per-CU form).  A bool selects "generic" (True) / "default" (False)."""
+        "band1" / "band3" (the default cascade with the battery band kernel's form forced: one step per lane, 768
+        threads / three steps per lane, 256 threads, two windows per CU; the default picks one-step for batches of
+        at most one battery window per CU).  A bool selects "generic" (True) / "default" (False)."""
         mode = (1 if path else 0) if isinstance(path, bool) else self._PATHS[path]
         self._check(self._lib.dvh_set_kernel_path(self._h, mode), "dvh_set_kernel_path")
 

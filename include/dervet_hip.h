@@ -255,9 +255,10 @@ int dvh_outage_min_soe(dvh_handle* h, const dvh_outage_case* cases, int32_t coun
 int dvh_last_outage_ms(const dvh_handle* h, double* ms);
 
 /* Kernel cascade (testing / A-B timing): 0 = default (battery-banded -> ELL -> generic CSR), 1 = generic
- * CSR kernel for every window, 2 = ELL -> generic (no battery-banded kernel), 3 = as 0 with the battery-banded
- * kernel in its one-step-per-lane form (768 threads per window; the default form runs 3 steps per lane, two
- * windows per CU). */
+ * CSR kernel for every window, 2 = ELL -> generic (no battery-banded kernel), 3 / 4 = as 0 with the battery-banded
+ * kernel's form forced: one step per lane (768 threads per window, one window per CU) / three steps per lane (256
+ * threads, two windows per CU).  The default picks the one-step form when the batch has at most one battery window
+ * per compute unit, else the three-step form. */
 int dvh_set_kernel_path(dvh_handle* h, int mode);
 
 #ifdef __cplusplus

@@ -138,16 +138,32 @@ def test_band_kernel_forms_agree(T):
     lps = _lps(groups)
     out = {}
     with BatchSolver(0) as s:
-        for path, variant in (("default", 9002004), ("band1", 9000012)):
+        for path, variant in (("band3", 9002004), ("band1", 9000012)):
             s.set_kernel_path(path)
             out[path] = s.solve(lps)
             st = s.kernel_stats()
             assert st["band_windows"] == len(lps) and st["variant"] == variant, (path, st)
-    for ra, rb in zip(out["default"], out["band1"]):
+    for ra, rb in zip(out["band3"], out["band1"]):
         assert ra.status == rb.status == 0
         assert abs(ra.obj - rb.obj) <= (1e-9 if T >= 100 else 1e-7) * max(1.0, abs(rb.obj))
         assert T < 100 or abs(ra.iters - rb.iters) <= 64
-    _check(lps, out["default"], f"band form 3, T={T}")
+    _check(lps, out["band3"], f"band form 3, T={T}")
+
+
+def test_band_kernel_form_follows_batch_size():
+    """The default cascade runs a batch of at most one battery window per CU in the one-step form (a lone window
+    is faster there) and larger batches in the three-step, two-windows-per-CU form."""
+    import torch
+    small = _lps(scenarios.config1())
+    big = pack(_lps(scenarios.config4(range(30)))).to_torch("cuda:0").alloc_outputs()  # 360 windows > 256 CUs
+    with BatchSolver(0) as s:
+        _check(small, s.solve(small), "config1 one-step")
+        assert s.kernel_stats()["variant"] == 9000012, s.kernel_stats()
+        s.solve_packed(big)
+        torch.cuda.synchronize()
+        st = s.kernel_stats()
+        assert st["variant"] == 9002004 and st["band_windows"] == 360, st
+        assert (big.istats.cpu().numpy()[:, 0] == 0).all()
 
 
 def test_band_kernel_config1_no_dcm(gpu_solver):
