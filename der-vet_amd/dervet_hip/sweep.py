@@ -154,7 +154,9 @@ def transfer_device(solver, tr_list, pb, pairs=None):
     """``transfer`` for a device-resident batch through the library (``dvh_warm_transfer``): one launch on the
     solver's stream, ordered after the seed solve and before the warm one; no host-side tensor work."""
     import ctypes
-    pairs = transfer_pairs(tr_list) if pairs is None else pairs
+    pairs = transfer_pairs(tr_list) if pairs is None else np.ascontiguousarray(pairs, np.int32)
+    if pairs.ndim != 2 or pairs.shape[1] != 3:
+        raise ValueError(f"pairs must be [count, 3] {{window, partner, T}}, got shape {pairs.shape}")
     p = pb.as_ctypes()
     solver._check(solver._lib.dvh_warm_transfer(solver._h, ctypes.byref(p), pairs.ctypes.data_as(ctypes.c_void_p),
                                                 len(pairs)), "dvh_warm_transfer")
