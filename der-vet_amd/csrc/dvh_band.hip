@@ -54,7 +54,7 @@ __host__ __device__ inline size_t band_lds_doubles(int B, int S, bool ice, int L
 }
 __host__ __device__ inline size_t band_ints_bytes(int B, int S) { return sizeof(int32_t) * (4 * (size_t)S * B + 4); }
 // The ints share the anchors' (kLfAnchors) or, in the other relieved forms, the check images' space
-__host__ __device__ inline bool band_ints_shared(int LF) { return (LF & kLfAnchors) || (LF && !(LF & kLfImages)); }
+__host__ __device__ constexpr bool band_ints_shared(int LF) { return (LF & kLfAnchors) || (LF && !(LF & kLfImages)); }
 __host__ __device__ inline size_t band_lds_bytes(int B, int S, bool ice, int LF) {
   const size_t d = align16(sizeof(double) * band_lds_doubles(B, S, ice, LF));
   return band_ints_shared(LF) ? d : d + align16(band_ints_bytes(B, S));
@@ -128,7 +128,7 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
   double* RO = YA + (LA ? NR * SB : 0);
   double* CQ = RO + (ICE ? 6 * SB : 0);  // [5 S][B] (kLfCosts)
   static_assert(!LA || sizeof(double) * (NC + NR) * SB >= sizeof(int32_t) * (4 * SB + 4), "ints fit the anchors");
-  constexpr bool IS = (LF & kLfAnchors) || (LF && !(LF & kLfImages));  // band_ints_shared(LF)
+  constexpr bool IS = band_ints_shared(LF);  // the ints share the anchors' / images' LDS
   int32_t* dcm = LA   ? reinterpret_cast<int32_t*>(XA)
                  : IS ? reinterpret_cast<int32_t*>(XP)
                       : reinterpret_cast<int32_t*>(smem + align16(sizeof(double) * band_lds_doubles(B, S, ICE, LF)));
@@ -574,6 +574,7 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
     for (int u = 0; u < 4; ++u) fin[u] = NAN;
   const int chk = o.check_every > 0 ? o.check_every : 64;
   double tau = uniform(eta / pw), sigma = uniform(eta * pw);
+  double sigma2n = uniform(-2.0 * sigma);  // the equality rows' fused dual step (non-check iterations)
   const int kkt_every = o.kkt_every > 0 ? o.kkt_every : 1;
   int ck = chk, kk_ = kkt_every;
   int kbase = 0;
@@ -699,6 +700,10 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
         kx[s][1] = fma(kd[s][2], xtv[s], kx[s][1]);  // kfin_tau
 #pragma unroll
         for (int r = 0; r < NR; ++r) {  // row 0 (SOE) is an equality; DCM / ICE rows are >=: duals stay >= 0
+          if (!CHECK && r == 0) {  // equality row, no image needed: 2 (y - sigma Kx) - y = y - 2 sigma Kx
+            y[s][0] = fma(ca, fma(sigma2n, kx[s][0], y[s][0]), cb * ayv(s, 0));
+            continue;
+          }
           double p1 = fma(-sigma, kx[s][r], y[s][r]);
           if (r > 0) p1 = vmax(p1, 0.0);
           if (CHECK) {
@@ -870,6 +875,7 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
       if (ddx > 1e-10 && ddy > 1e-10) pw = uniform(pw_update(ddy / ddx, pw, o.theta));
       tau = uniform(eta / pw);
       sigma = uniform(eta * pw);
+      sigma2n = uniform(-2.0 * sigma);
       double xp[S][NC], yp[S][NR];
       load_images(xp, yp);
 #pragma unroll
