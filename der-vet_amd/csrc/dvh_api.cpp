@@ -124,6 +124,7 @@ static std::string check_options(const dvh_options* o) {
   if (o->max_iters <= 0) return "max_iters must be > 0";
   if (o->check_every <= 0) return "check_every must be > 0";
   if (o->kkt_every <= 0) return "kkt_every must be > 0";
+  if (o->kkt_predict < 0) return "kkt_predict must be >= 0";
   if (o->ruiz_iters < 0 || o->power_iters <= 0) return "ruiz_iters must be >= 0 and power_iters > 0";
   if (!(o->step_safety > 0.0 && o->step_safety < 1.0)) return "step_safety must be in (0, 1)";
   if (!(o->reflection >= 0.0 && o->reflection <= 1.0)) return "reflection must be in [0, 1]";
@@ -602,6 +603,7 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
   o.ruiz_iters = h->opts.ruiz_iters;
   o.power_iters = h->opts.power_iters;
   o.warm = h->opts.warm_start != 0;
+  o.kkt_predict = h->opts.kkt_predict;
   o.small_max = dvh::kSmallMax;
   dvh::Batch b{bt->desc, bt->indptr, bt->indices, bt->data, bt->c, bt->c0, bt->q, bt->l, bt->u,
                bt->x, bt->y, bt->stats, bt->istats};

@@ -34,6 +34,7 @@ namespace {
 constexpr int kBandSteps = 768;  // steps per window (T <= kBandSteps)
 constexpr int kJMax = 4;         // tau (demand-period) columns per window
 constexpr int kNeedsEll = -2;
+constexpr int kKktMaxSkip = 4;  // kkt_predict: due KKT checks skipped in a row at most
 
 // LDS layout (B lanes, S steps per lane, SB = S B steps), doubles then ints:
 //   XE[B+1] YS[B+1] XT[kJMax] red[kNRed(NW+1)+4] TP[kJMax][B] XP[NC S][B] YP[NR S][B] (ICE: RO[6 S][B])
@@ -577,6 +578,8 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
   double sigma2n = uniform(-2.0 * sigma);  // the equality rows' fused dual step (non-check iterations)
   const int kkt_every = o.kkt_every > 0 ? o.kkt_every : 1;
   int ck = chk, kk_ = kkt_every;
+  double kq_last = -1.0, kr_last = 0.0;  // the last KKT check's worst ratio to eps and fixed-point residual
+  int kskip = 0;                         // due KKT checks skipped since (kkt_predict)
   int kbase = 0;
   auto hload = [&](int k0_) {
     const int kq = k0_ + lane;
@@ -760,7 +763,8 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
       iterate(Tt(), F());
     // ---------------- check: fixed-point residual of z_k, restart test; every kkt_every-th check the relative
     // KKT error of T(z_k) in the unscaled space (as pdhg_ell_kernel)
-    const bool kkt = (--kk_ == 0) || (it + chk > o.max_iters);
+    const bool last = it + chk > o.max_iters;
+    bool kkt = (--kk_ == 0) || last;
     if (kkt) kk_ = kkt_every;
     double acc[kNRed];
     acc[0] = mv0;
@@ -769,6 +773,21 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
     acc[3] = mv3;
 #pragma unroll
     for (int u = 4; u < kNRed; ++u) acc[u] = 0.0;
+    double r = 0.0;
+    if (o.kkt_predict > 0) {
+      // predicted KKT gate: the restart sums first; a due check runs only if the last check's worst ratio to eps,
+      // scaled by the fixed-point residual's decrease since then, is within kkt_predict (or 4 were skipped)
+      double acc4[4] = {acc[0], acc[1], acc[2], acc[3]};
+      block_sum1<B, 4, true>(acc4, red);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] = acc4[u];
+      r = sqrt(pw * acc[0] + acc[2] / pw);
+      if (kkt && !last && kq_last >= 0.0 && kskip < kKktMaxSkip &&
+          kq_last * r > (double)o.kkt_predict * kr_last) {
+        kkt = false;
+        ++kskip;
+      }
+    }
     if (kkt) {
       // images of T(z_k) in XE / XT / YS / TP (rewritten from z after the check)
       double xp[S][NC], yp[S][NR];
@@ -839,7 +858,16 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
       }
       if (ilane) row_kkt(0, sp[4] * XE[0], sp[3], sp[2], false);
     }
-    if (kkt) {
+    if (o.kkt_predict > 0) {
+      if (kkt) {  // the KKT sums in the slots after the restart sums' (red is not reused before a barrier)
+        double acc6[kNRed - 4];
+#pragma unroll
+        for (int u = 4; u < kNRed; ++u) acc6[u - 4] = acc[u];
+        block_sum1<B, kNRed - 4, true>(acc6, red + 4 * NW);
+#pragma unroll
+        for (int u = 4; u < kNRed; ++u) acc[u] = acc6[u - 4];
+      }
+    } else if (kkt) {
       block_sum1<B, kNRed, true>(acc, red);
     } else {
       double acc4[4] = {acc[0], acc[1], acc[2], acc[3]};
@@ -847,6 +875,7 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc[u] = acc4[u];
     }
+    if (!(o.kkt_predict > 0)) r = sqrt(pw * acc[0] + acc[2] / pw);
     if (kkt) {
       const double pobj = acc[6] + c0, dobj = acc[7] + acc[8] + c0;
       const double pres = sqrt(acc[4]) / (1.0 + qnorm), dres = sqrt(acc[5]) / (1.0 + cnorm);
@@ -861,12 +890,14 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
         status = kOptimal;
         break;
       }
+      kq_last = fmax(fmax(pres, dres), gap) / o.eps;
+      kr_last = r;
+      kskip = 0;
       if (!(isfinite(pobj) && isfinite(dobj))) {
         status = kNumerical;
         break;
       }
     }
-    const double r = sqrt(pw * acc[0] + acc[2] / pw);
     if (r0 < 0.0) r0 = r;
     const bool restart = (r <= o.b_suff * r0) || (r <= o.b_nec * r0 && rprev >= 0.0 && r > rprev) ||
                          ((double)kin >= o.b_art * (double)it);

@@ -27,6 +27,7 @@ struct Opts {
   int setup_segments;  // set by launch_setup
   int small_max;       // setup skips (scal[6] = 2) windows with n or m above this
   int warm;            // start from the (unscaled) x / y in the output buffers (band kernel; others cold)
+  int kkt_predict;     // dvh_options.kkt_predict (band kernel; 0 = off)
 };
 
 // Inputs of one chunk of the packed batch (device pointers, global offsets from desc).

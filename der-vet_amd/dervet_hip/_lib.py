@@ -27,7 +27,8 @@ class Options(ctypes.Structure):
                 ("restart_necessary", ctypes.c_double), ("restart_artificial", ctypes.c_double),
                 ("primal_weight_theta", ctypes.c_double), ("verbose", ctypes.c_int32),
                 ("kkt_every", ctypes.c_int32), ("warm_start", ctypes.c_int32), ("pad0", ctypes.c_int32),
-                ("eps_obj", ctypes.c_double), ("reserved", ctypes.c_int32 * 2)]
+                ("eps_obj", ctypes.c_double), ("kkt_predict", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
 
 
 class LP(ctypes.Structure):

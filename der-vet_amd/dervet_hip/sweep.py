@@ -73,7 +73,10 @@ def seed_split(keys, stride, features=None, cover=False):
 # dvh_options for the warm phase: restart checks every 64 iterations, KKT every 2nd check (the cold default is
 # 32 / 4).  GPU sweep on 48,000 config-4 windows (profiles/r01h_warm_params*.log): warm phase 2,203 -> 2,152
 # iterations, PDHG time of the schedule 376.6 -> 357.2 ms; every other restart / weight setting tried was slower.
-WARM_OPTIONS = {"check_every": 64, "kkt_every": 2}
+# Round 2: KKT at every restart check, but a due check is skipped while its predicted outcome is > 4x eps
+# (dvh_options.kkt_predict; a KKT check costs ~6 iterations): PDHG 550 -> 527 ms on the bench batch, 2,073 -> 2,038
+# warm iterations (profiles/r02zy_kkt_predict.log).
+WARM_OPTIONS = {"check_every": 64, "kkt_every": 1, "kkt_predict": 4}
 
 
 @dataclass

@@ -13,7 +13,8 @@ dev = pb.to_torch("cuda:0").alloc_outputs()
 s = BatchSolver(0)
 nwin = pb.count
 for label, kw in [("nochecks", dict(check_every=100000, kkt_every=1)), ("chk16", dict(check_every=16, kkt_every=1000000)),
-                  ("chk16kkt4", dict(check_every=16, kkt_every=4)), ("chk64kkt1", dict(check_every=64, kkt_every=1))]:
+                  ("chk16kkt4", dict(check_every=16, kkt_every=4)), ("chk64kkt1", dict(check_every=64, kkt_every=1)),
+                  ("chk64", dict(check_every=64, kkt_every=1000000)), ("chk64kkt2", dict(check_every=64, kkt_every=2))]:
     if ONLY and label not in ONLY:
         continue
     for iters in (1024, 4096):

@@ -34,7 +34,7 @@ def test_version_and_defaults():
     lib = _lib.load()
     assert lib.dvh_version().decode().startswith("dervet_hip")
     o = _lib.default_options()
-    assert o.eps == 1e-6 and o.check_every == 32 and o.kkt_every == 4 and o.max_iters == 100000
+    assert o.eps == 1e-6 and o.check_every == 32 and o.kkt_every == 4 and o.max_iters == 100000 and o.kkt_predict == 0
     assert o.restart_artificial == 0.1 and o.primal_weight_theta == 1.0 and o.step_safety == 0.998
 
 

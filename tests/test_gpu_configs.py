@@ -166,6 +166,42 @@ def test_band_kernel_form_follows_batch_size():
         assert (big.istats.cpu().numpy()[:, 0] == 0).all()
 
 
+@pytest.mark.parametrize("path", ["band1", "band3"])
+def test_kkt_predict_only_delays_termination(path):
+    """dvh_options.kkt_predict skips due KKT checks without touching the iterates (restarts depend on the
+    fixed-point residual only): every window ends at the same or a later check (later by more than the 4 skipped
+    checks where a check the plain run passed is skipped and the next ones fail: the KKT error is not monotone),
+    bit-identical where the iteration counts agree, and still passes the same termination test."""
+    lps = _lps(scenarios.config4(range(24)))
+    s = BatchSolver(0)
+    try:
+        s.set_kernel_path(path)
+        s.set_options(check_every=64, kkt_every=1)
+        plain = s.solve(lps)
+        s.set_options(kkt_predict=4)
+        pred = s.solve(lps)
+        assert s.kernel_stats()["band_windows"] == len(lps)
+    finally:
+        s.close()
+    delay = []
+    for a, b in zip(plain, pred):
+        assert a.status == 0 and b.status == 0
+        assert a.iters <= b.iters and (b.iters - a.iters) % 64 == 0, (a.iters, b.iters)
+        delay.append(b.iters - a.iters)
+        if a.iters == b.iters:
+            assert a.obj == b.obj and np.array_equal(a.x, b.x) and np.array_equal(a.y, b.y)
+        else:  # both passed the same termination test, at different checks
+            assert abs(a.obj - b.obj) <= 2e-6 * max(1.0, abs(a.obj))
+    assert np.mean(delay) <= 64, np.mean(delay)
+    _check(lps[::23], pred[::23], f"kkt_predict {path}")
+    bad = BatchSolver(0)
+    try:
+        with pytest.raises(SolverError, match="kkt_predict"):
+            bad.set_options(kkt_predict=-1)
+    finally:
+        bad.close()
+
+
 def test_band_kernel_config1_no_dcm(gpu_solver):
     """Config 1 (DA arbitrage, no demand charge: J = 0, no >= rows) takes the battery-banded kernel."""
     lps = _lps(scenarios.config1())
