@@ -152,6 +152,9 @@ def main():
                          "from their nearest seed (dervet_hip/sweep.py); cold: every window from zero")
     ap.add_argument("--seed-stride", type=int, default=32)
     ap.add_argument("--no-cold-ref", action="store_true", help="skip the untimed all-cold reference solve")
+    ap.add_argument("--kkt-predict", type=int, default=4,
+                    help="dvh_options.kkt_predict for cold solves (--schedule cold and the cold reference; the seeded "
+                         "schedule's phases use sweep.SEED_OPTIONS / WARM_OPTIONS); 0 = every due KKT check runs")
     ap.add_argument("--build", choices=("device", "host"), default="device",
                     help="window expansion: on the GPU from compact inputs (lp/gpu_builder.py) or by the host "
                          "builder + upload (bit-identical batches; untimed by the contract, reported as build)")
@@ -209,6 +212,7 @@ def main():
     pb = dev  # windows are read back from the device for the CPU legs
     count = len(desc)
     opts = {k: v for k, v in (("check_every", args.check_every), ("kkt_every", args.kkt_every)) if v > 0}
+    opts["kkt_predict"] = args.kkt_predict
     if opts:
         solver.set_options(**opts)
 
@@ -347,7 +351,7 @@ def main():
                   "frac_obj_rel_err_le_1e-5": float(np.mean(rel <= 1e-5)) if ok.any() else None,
                   "max_benefit_rel_err": float(ben_rel.max()) if ok.any() else None,
                   "median_benefit_usd": float(np.median(ben_h)) if ok.any() else None,
-                  "full_population": "profiles/r02zz_certify.json (all 120,000 windows vs HiGHS, seeded and cold)"}
+                  "full_population": "profiles/r02zzc_certify.json (all 120,000 windows vs HiGHS, seeded and cold)"}
 
     line = {
         "metric": METRIC,

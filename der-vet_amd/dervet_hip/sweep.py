@@ -77,6 +77,9 @@ def seed_split(keys, stride, features=None, cover=False):
 # (dvh_options.kkt_predict; a KKT check costs ~6 iterations): PDHG 550 -> 527 ms on the bench batch, 2,073 -> 2,038
 # warm iterations (profiles/r02zy_kkt_predict.log).
 WARM_OPTIONS = {"check_every": 64, "kkt_every": 1, "kkt_predict": 4}
+# dvh_options for the cold seed phase: the defaults (checks every 32, KKT every 4th) with the same KKT gate: on the
+# bench's 120,000 windows all cold, PDHG 864.6 -> 824.6 ms at unchanged iterations (profiles/r02zzb_cold_kkt_predict.log)
+SEED_OPTIONS = {"kkt_predict": 4}
 
 
 @dataclass
@@ -231,15 +234,17 @@ class SeededSweep:
             return gpu_builder.pack_specs_device(self.specs, solver, device)
         return self.packed.to_torch(device).alloc_outputs()
 
-    def solve(self, solver, dev, warm_options=None):
+    def solve(self, solver, dev, warm_options=None, seed_options=None):
         """dev: this sweep's packed batch on the device (``self.packed.to_torch(..).alloc_outputs()``).
-        warm_options: dvh_options fields for the warm phase only (restored afterwards; None: WARM_OPTIONS).
+        warm_options: dvh_options fields for the warm phase only (restored afterwards; None: WARM_OPTIONS);
+        seed_options: the same for the cold seed phase (None: SEED_OPTIONS).
         Returns the kernel timings {setup_ms, pdhg_ms, total_ms} and the windows per kernel path, summed over
         the two phases."""
         cnt = dev.count
         o0 = solver.options()
         warm_options = dict(WARM_OPTIONS if warm_options is None else warm_options)
-        restore = {k: getattr(o0, k) for k in warm_options}
+        seed_options = dict(SEED_OPTIONS if seed_options is None else seed_options)
+        restore = {k: getattr(o0, k) for k in list(warm_options) + list(seed_options)}
         restore["warm_start"] = o0.warm_start
         tm = {"total_ms": 0.0, "setup_ms": 0.0, "pdhg_ms": 0.0}
         paths = {}
@@ -251,11 +256,11 @@ class SeededSweep:
                 if k.endswith("_windows"):
                     paths[k] = paths.get(k, 0) + v
 
-        solver.set_options(warm_start=0)
+        solver.set_options(warm_start=0, **seed_options)
         try:
             solver.solve_packed(sub_batch(dev, 0, self.n_seed))
         finally:
-            solver.set_options(warm_start=o0.warm_start)
+            solver.set_options(**restore)
         account()
         if cnt > self.n_seed:
             if dev.x.is_cuda and not os.environ.get("DVH_SWEEP_TORCH_TRANSFER"):
