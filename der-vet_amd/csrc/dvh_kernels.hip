@@ -77,8 +77,8 @@ __global__ __launch_bounds__(kSetupB) void setup_kernel(const Batch b, const Wor
                                                         const int32_t* list) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ double red[(kSetupB / kWave + 1) * 4];
-  __shared__ int sh_part[kSetupB];
   __shared__ int sh_cnt[2];
+  __shared__ int sh_wt[kSetupB / kWave];
   const int k = MED ? list[blockIdx.x] : ch.first + (int)blockIdx.x;
   const int kl = k - ch.first;
   const WinOff W = win_offsets(b, ch, k);
@@ -147,18 +147,17 @@ __global__ __launch_bounds__(kSetupB) void setup_kernel(const Batch b, const Wor
     int acc = 0;
     for (int j = s0; j < e0; ++j)
       for (int sg = 0; sg < nseg; ++sg) acc += cursor[sg * (n + 1) + j];
-    sh_part[tid] = acc;
-    __syncthreads();
-    if (tid == 0) {
-      int run = 0;
-      for (int t = 0; t < kSetupB; ++t) {
-        const int v = sh_part[t];
-        sh_part[t] = run;
-        run += v;
-      }
+    // exclusive scan of the per-thread totals (integer: exact in any order): wave scans, then the wave totals
+    int inc = acc;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const int t = __shfl_up(inc, o, kWave);
+      if (lane >= o) inc += t;
     }
+    if (lane == kWave - 1) sh_wt[wid] = inc;
     __syncthreads();
-    int run = sh_part[tid];
+    int run = inc - acc;
+    for (int u = 0; u < wid; ++u) run += sh_wt[u];
     for (int j = s0; j < e0; ++j) {
       Tp[j] = run;
       for (int sg = 0; sg < nseg; ++sg) {
@@ -173,20 +172,27 @@ __global__ __launch_bounds__(kSetupB) void setup_kernel(const Batch b, const Wor
   // 3. stable fill of K^T, wave sg walks segment sg in row-major order; ties inside a 64-entry chunk are
   //    ranked by lane
   if (wid < nseg) {
+    const int nb = 32 - __builtin_clz((unsigned)(n > kWave ? n : kWave));
     int32_t* cur = cursor + wid * (n + 1);
     const int a = seg_lo(wid), e = seg_lo(wid + 1);
     for (int base = a; base < e; base += kWave) {
       const int p = base + lane;
       const bool v = p < e;
       const int j = v ? Kc[p] : -1 - lane;
-      int rank = 0, cnt = 0;
-      for (int l = 0; l < kWave; ++l) {
-        const int jj = __shfl(j, l, kWave);
-        if (jj == j) {
-          ++cnt;
-          rank += (l < lane);
-        }
+      // lanes holding the same column: AND of one ballot per bit of j (bits 0 .. nb-1 cover the columns and the
+      // padding lanes' -1 - lane among themselves; the sign bit tells the two apart)
+      unsigned long long eq = ~0ull;
+      for (int bt = 0; bt < nb; ++bt) {
+        const bool on = (j >> bt) & 1;
+        const unsigned long long bal = __ballot(on);
+        eq &= on ? bal : ~bal;
       }
+      {
+        const bool on = j < 0;
+        const unsigned long long bal = __ballot(on);
+        eq &= on ? bal : ~bal;
+      }
+      const int rank = __popcll(eq & ((1ull << lane) - 1ull)), cnt = __popcll(eq);
       int pos = 0;
       if (v) pos = cur[j] + rank;
       __builtin_amdgcn_wave_barrier();
@@ -200,12 +206,23 @@ __global__ __launch_bounds__(kSetupB) void setup_kernel(const Batch b, const Wor
     }
   }
   __syncthreads();
+  // 4. long-row lists (deterministic ballot compaction): every thread flags rows / columns (bytes over the dead
+  //    transpose cursors), wave 0 compacts the flags from LDS
+  unsigned char* lfl = reinterpret_cast<unsigned char*>(cursor);
+  // (the cursors hold nseg (n + 1) ints; a window with more rows than that reads the lengths from global memory)
+  const bool fl_lds = (int64_t)m + n <= 4 * (int64_t)nseg * (n + 1);
+  auto row_long = [&](int i) { return fl_lds ? lfl[i] != 0 : (Kp[i + 1] - Kp[i]) > kLongRow; };
+  auto col_long = [&](int j) { return fl_lds ? lfl[m + j] != 0 : (Tp[j + 1] - Tp[j]) > kLongRow; };
+  if (fl_lds) {
+    for (int i = tid; i < m; i += kSetupB) lfl[i] = (Kp[i + 1] - Kp[i]) > kLongRow;
+    for (int j = tid; j < n; j += kSetupB) lfl[m + j] = (Tp[j + 1] - Tp[j]) > kLongRow;
+  }
+  __syncthreads();
   if (wid == 0) {
-    // 4. long-row lists (deterministic ballot compaction)
     int nk = 0, nt = 0;
     for (int base = 0; base < m; base += kWave) {
       const int i = base + lane;
-      const bool isl = i < m && (Kp[i + 1] - Kp[i]) > kLongRow;
+      const bool isl = i < m && row_long(i);
       const unsigned long long bal = __ballot(isl);
       const int pre = __popcll(bal & ((1ull << lane) - 1ull));
       if (isl && nk + pre < kLMax) longk[nk + pre] = i;
@@ -213,7 +230,7 @@ __global__ __launch_bounds__(kSetupB) void setup_kernel(const Batch b, const Wor
     }
     for (int base = 0; base < n; base += kWave) {
       const int j = base + lane;
-      const bool isl = j < n && (Tp[j + 1] - Tp[j]) > kLongRow;
+      const bool isl = j < n && col_long(j);
       const unsigned long long bal = __ballot(isl);
       const int pre = __popcll(bal & ((1ull << lane) - 1ull));
       if (isl && nt + pre < kLMax) longt[nt + pre] = j;
