@@ -351,7 +351,7 @@ def main():
                   "frac_obj_rel_err_le_1e-5": float(np.mean(rel <= 1e-5)) if ok.any() else None,
                   "max_benefit_rel_err": float(ben_rel.max()) if ok.any() else None,
                   "median_benefit_usd": float(np.median(ben_h)) if ok.any() else None,
-                  "full_population": "profiles/r02zzg_certify.json (all 120,000 windows vs HiGHS, seeded and cold)"}
+                  "full_population": "profiles/r02zzi_certify.json (all 120,000 windows vs HiGHS, seeded and cold)"}
 
     line = {
         "metric": METRIC,

@@ -34,7 +34,6 @@ namespace {
 constexpr int kBandSteps = 768;  // steps per window (T <= kBandSteps)
 constexpr int kJMax = 4;         // tau (demand-period) columns per window
 constexpr int kNeedsEll = -2;
-constexpr int kKktMaxSkip = 4;  // kkt_predict: due KKT checks skipped in a row at most
 
 // LDS layout (B lanes, S steps per lane, SB = S B steps), doubles then ints:
 //   XE[B+1] YS[B+1] XT[kJMax] red[kNRed(NW+1)+4] TP[kJMax][B] XP[NC S][B] YP[NR S][B] (ICE: RO[6 S][B])
@@ -578,8 +577,7 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
   double sigma2n = uniform(-2.0 * sigma);  // the equality rows' fused dual step (non-check iterations)
   const int kkt_every = o.kkt_every > 0 ? o.kkt_every : 1;
   int ck = chk, kk_ = kkt_every;
-  double kq_last = -1.0, kr_last = 0.0;  // the last KKT check's worst ratio to eps and fixed-point residual
-  int kskip = 0;                         // due KKT checks skipped since (kkt_predict)
+  KktGate gate;  // dvh_options.kkt_predict (dvh_device.h)
   int kbase = 0;
   auto hload = [&](int k0_) {
     const int kq = k0_ + lane;
@@ -782,10 +780,9 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc[u] = acc4[u];
       r = sqrt(pw * acc[0] + acc[2] / pw);
-      if (kkt && !last && kq_last >= 0.0 && kskip < kKktMaxSkip &&
-          kq_last * r > (double)o.kkt_predict * kr_last) {
+      if (kkt && !last && kkt_gate_skip(o, gate, r)) {
         kkt = false;
-        ++kskip;
+        ++gate.skip;
       }
     }
     if (kkt) {
@@ -890,9 +887,7 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
         status = kOptimal;
         break;
       }
-      kq_last = fmax(fmax(pres, dres), gap) / o.eps;
-      kr_last = r;
-      kskip = 0;
+      gate.note(pres, dres, gap, o.eps, r);
       if (!(isfinite(pobj) && isfinite(dobj))) {
         status = kNumerical;
         break;

@@ -156,6 +156,23 @@ __device__ __forceinline__ bool kkt_done(const Opts& o, double pres, double dres
   return !(o.eps_obj > 0.0) || fabs(pobj - dobj) + sqrt(rp2 * y2) <= o.eps_obj * (1.0 + fabs(pobj));
 }
 
+// Predicted KKT gate (dvh_options.kkt_predict = P > 0): a due KKT check is skipped while the last check's worst
+// ratio max(pres, dres, gap) / eps, scaled by the fixed-point residual's decrease since then (r / r_then), exceeds P,
+// at most kKktMaxSkip due checks in a row.  Only the timing of the termination test changes, not the iterates.
+constexpr int kKktMaxSkip = 4;
+struct KktGate {
+  double q = -1.0, r = 0.0;  // the last KKT check's worst ratio to eps and fixed-point residual (q < 0: none yet)
+  int skip = 0;              // due checks skipped since
+  __device__ void note(double pres, double dres, double gap, double eps, double rr) {
+    q = fmax(fmax(pres, dres), gap) / eps;
+    r = rr;
+    skip = 0;
+  }
+};
+__device__ __forceinline__ bool kkt_gate_skip(const Opts& o, const KktGate& g, double r) {
+  return g.q >= 0.0 && g.skip < kKktMaxSkip && g.q * r > (double)o.kkt_predict * g.r;
+}
+
 struct WinOff {
   int n, m, meq, nnz;
   int64_t row, nz, on, om;     // global offsets (inputs / outputs)

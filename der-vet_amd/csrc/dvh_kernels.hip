@@ -1271,6 +1271,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(WPE))) void p
   double tau = uniform(eta / pw), sigma = uniform(eta * pw);
   const int kkt_every = o.kkt_every > 0 ? o.kkt_every : 1;
   int ck = chk, kk_ = kkt_every;
+  KktGate gate;  // dvh_options.kkt_predict (as pdhg_band_kernel)
   // Halpern weights 1/(k+2): lane l holds the weight of k = kbase + l; an iteration reads its weight with
   // v_readlane (uniform lane index -> SGPRs), the slice is reloaded every 64 iterations.
   int kbase = 0;
@@ -1435,7 +1436,8 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(WPE))) void p
 
     // ---------------- check (every check_every iterations): fixed-point residual of z_k, restart test;
     // every kkt_every-th check also the relative KKT error of T(z_k) = (x+, y+) in the unscaled space.
-    const bool kkt = (--kk_ == 0) || (it + chk > o.max_iters);  // the last check before the limit is a KKT one
+    const bool last = it + chk > o.max_iters;  // the last check before the limit is a KKT one
+    bool kkt = (--kk_ == 0) || last;
     if (kkt) kk_ = kkt_every;
     double acc[kNRed];  // 0..3 movement norms, 4 ||r_p||^2, 5 ||r_d||^2, 6 c'x, 7 q'y, 8 bound term
     acc[0] = mv0;
@@ -1444,6 +1446,18 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(WPE))) void p
     acc[3] = mv3;
 #pragma unroll
     for (int t = 4; t < kNRed; ++t) acc[t] = 0.0;
+    double r = 0.0;
+    if (o.kkt_predict > 0) {  // predicted KKT gate: the restart sums first (kkt_gate_skip, dvh_device.h)
+      double acc4[4] = {acc[0], acc[1], acc[2], acc[3]};
+      block_sum1<B, 4, true>(acc4, red);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = acc4[t];
+      r = sqrt(pw * acc[0] + acc[2] / pw);
+      if (kkt && !last && kkt_gate_skip(o, gate, r)) {
+        kkt = false;
+        ++gate.skip;
+      }
+    }
     // The KKT products gather from images of T(z_k): XP / YP (PL; the long slots are copied in here), or
     // X / Y refilled from the HBM copies (restored after the check unless a restart rewrites them).
     double* const XK = PL ? XP : X;
@@ -1511,7 +1525,16 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(WPE))) void p
     }
     // readlane broadcast: the sums (and all decisions below) are uniform.  A restart-only check needs the
     // four movement norms alone (each wave-wide sum is ~25 VALU ops).
-    if (kkt) {
+    if (o.kkt_predict > 0) {
+      if (kkt) {  // the KKT sums in the slots after the restart sums'
+        double acc6[kNRed - 4];
+#pragma unroll
+        for (int t = 4; t < kNRed; ++t) acc6[t - 4] = acc[t];
+        block_sum1<B, kNRed - 4, true>(acc6, red + 4 * NW);
+#pragma unroll
+        for (int t = 4; t < kNRed; ++t) acc[t] = acc6[t - 4];
+      }
+    } else if (kkt) {
       block_sum1<B, kNRed, true>(acc, red);
     } else {
       double acc4[4] = {acc[0], acc[1], acc[2], acc[3]};
@@ -1519,6 +1542,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(WPE))) void p
 #pragma unroll
       for (int t = 0; t < 4; ++t) acc[t] = acc4[t];
     }
+    if (!(o.kkt_predict > 0)) r = sqrt(pw * acc[0] + acc[2] / pw);
     if (kkt) {
       const double pobj = acc[6] + c0, dobj = acc[7] + acc[8] + c0;
       const double pres = sqrt(acc[4]) / (1.0 + qnorm), dres = sqrt(acc[5]) / (1.0 + cnorm);
@@ -1533,12 +1557,12 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(WPE))) void p
         status = kOptimal;
         break;
       }
+      gate.note(pres, dres, gap, o.eps, r);
       if (!(isfinite(pobj) && isfinite(dobj))) {
         status = kNumerical;
         break;
       }
     }
-    const double r = sqrt(pw * acc[0] + acc[2] / pw);
     if (r0 < 0.0) r0 = r;
     const bool restart = (r <= o.b_suff * r0) || (r <= o.b_nec * r0 && rprev >= 0.0 && r > rprev) ||
                          ((double)kin >= o.b_art * (double)it);

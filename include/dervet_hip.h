@@ -75,7 +75,7 @@ typedef struct dvh_options {
   double eps_obj;             /* objective-error termination (0 = off), default 1e-6: besides the KKT test, */
                               /* |pobj - dobj| + ||y||_2 ||r_p||_2 <= eps_obj (1 + |pobj|) (unscaled), an    */
                               /* estimate of |pobj - opt| (gap + the dual-weighted primal residual)          */
-  int32_t kkt_predict;        /* 0 = off (default).  P > 0 (battery band kernels; the other tiers ignore it): a */
+  int32_t kkt_predict;        /* 0 = off (default).  P > 0 (band and ELL kernels; the other tiers ignore it): a  */
                               /* due KKT check is skipped while its predicted outcome, the last check's worst   */
                               /* ratio max(pres, dres, gap) / eps scaled by the fixed-point residual's decrease  */
                               /* since then, exceeds P; at most 4 due checks in a row are skipped.  Termination  */

@@ -43,8 +43,8 @@ def main():
     s = BatchSolver(0)
     for name, groups in workloads():
         dev = builder.pack_groups(groups).to_torch("cuda:0").alloc_outputs()
-        for eps_obj in (1e-6, 0.0):
-            s.set_options(eps_obj=eps_obj)
+        for opts in ({"eps_obj": 1e-6}, {"eps_obj": 0.0}, {"kkt_predict": 4}):
+            s.set_options(**opts)
             best = None
             for _ in range(3):
                 torch.cuda.synchronize()
@@ -55,11 +55,11 @@ def main():
                 best = dt if best is None else min(best, dt)
             ist = dev.istats.cpu().numpy()
             it = ist[:, 1]
-            print(json.dumps({"workload": name, "eps_obj": eps_obj, "wall_ms": round(best * 1e3, 2),
+            print(json.dumps({"workload": name, "options": opts, "wall_ms": round(best * 1e3, 2),
                               "iters_mean": float(it.mean()), "iters_p99": float(np.percentile(it, 99)),
                               "iters_max": int(it.max()), "optimal": int((ist[:, 0] == 0).sum()),
                               "windows": int(len(ist)), "paths": s.kernel_stats()}), flush=True)
-        s.set_options()
+            s.set_options(eps_obj=1e-6, kkt_predict=0)
 
 
 if __name__ == "__main__":

@@ -166,7 +166,7 @@ def test_band_kernel_form_follows_batch_size():
         assert (big.istats.cpu().numpy()[:, 0] == 0).all()
 
 
-@pytest.mark.parametrize("path", ["band1", "band3"])
+@pytest.mark.parametrize("path", ["band1", "band3", "ell"])
 def test_kkt_predict_only_delays_termination(path):
     """dvh_options.kkt_predict skips due KKT checks without touching the iterates (restarts depend on the
     fixed-point residual only): every window ends at the same or a later check (later by more than the 4 skipped
@@ -180,7 +180,7 @@ def test_kkt_predict_only_delays_termination(path):
         plain = s.solve(lps)
         s.set_options(kkt_predict=4)
         pred = s.solve(lps)
-        assert s.kernel_stats()["band_windows"] == len(lps)
+        assert s.kernel_stats()["ell_windows" if path == "ell" else "band_windows"] == len(lps)
     finally:
         s.close()
     delay = []
