@@ -83,7 +83,10 @@ __device__ __noinline__ RowKkt row_kkt_fn(double kv, double qi, double yi, doubl
   return {r * r, (yi * dr) * (yi * dr)};
 }
 
-template <int B, int S, bool ICE, int LF, int WPS>
+// GATE: the predicted KKT gate (dvh_options.kkt_predict > 0) is compiled in only where the host asks for it -- its
+// state and extra reduction raised the register allocation of the check path by 30-40 spilled VGPRs in every form
+// (profiles/r02zzk_ab_configs12_spills.log), which runs with the default options paid for nothing.
+template <int B, int S, bool ICE, int LF, int WPS, bool GATE>
 __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const Work w, const Chunk ch, const Opts o,
                                                         const int32_t* list) {
   constexpr int NW = B / kWave;
@@ -772,7 +775,7 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
 #pragma unroll
     for (int u = 4; u < kNRed; ++u) acc[u] = 0.0;
     double r = 0.0;
-    if (o.kkt_predict > 0) {
+    if constexpr (GATE) {
       // predicted KKT gate: the restart sums first; a due check runs only if the last check's worst ratio to eps,
       // scaled by the fixed-point residual's decrease since then, is within kkt_predict (or 4 were skipped)
       double acc4[4] = {acc[0], acc[1], acc[2], acc[3]};
@@ -855,7 +858,7 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
       }
       if (ilane) row_kkt(0, sp[4] * XE[0], sp[3], sp[2], false);
     }
-    if (o.kkt_predict > 0) {
+    if constexpr (GATE) {
       if (kkt) {  // the KKT sums in the slots after the restart sums' (red is not reused before a barrier)
         double acc6[kNRed - 4];
 #pragma unroll
@@ -872,7 +875,7 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc[u] = acc4[u];
     }
-    if (!(o.kkt_predict > 0)) r = sqrt(pw * acc[0] + acc[2] / pw);
+    if constexpr (!GATE) r = sqrt(pw * acc[0] + acc[2] / pw);
     if (kkt) {
       const double pobj = acc[6] + c0, dobj = acc[7] + acc[8] + c0;
       const double pres = sqrt(acc[4]) / (1.0 + qnorm), dres = sqrt(acc[5]) / (1.0 + cnorm);
@@ -887,7 +890,7 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
         status = kOptimal;
         break;
       }
-      gate.note(pres, dres, gap, o.eps, r);
+      if constexpr (GATE) gate.note(pres, dres, gap, o.eps, r);
       if (!(isfinite(pobj) && isfinite(dobj))) {
         status = kNumerical;
         break;
@@ -963,12 +966,12 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
   }
 }
 
-template <int B, int S, bool ICE, int LF, int WPS>
-hipError_t launch_band_one(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, hipStream_t s,
+template <int B, int S, bool ICE, int LF, int WPS, bool GATE>
+hipError_t launch_band_one_g(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, hipStream_t s,
                            const int32_t* list, int nlist, int* variant_out) {
   static_assert(B * S == kBandSteps, "every form covers T <= kBandSteps");
   const size_t lds = band_lds_bytes(B, S, ICE, LF);
-  auto kern = pdhg_band_kernel<B, S, ICE, LF, WPS>;
+  auto kern = pdhg_band_kernel<B, S, ICE, LF, WPS, GATE>;
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   if (getenv("DVH_BAND_OCC")) {  // residency diagnostics (A/B helper)
@@ -979,12 +982,18 @@ hipError_t launch_band_one(const Batch& b, const Work& w, const Chunk& ch, const
     hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kern, B, lds);
     hipFuncAttributes fa;
     hipFuncGetAttributes(&fa, (const void*)kern);
-    fprintf(stderr, "band<%d,%d,%d,%d>: lds %zu B, blocks/CU %d, lds/CU %zu, regs %d, local %zu\n", B, S, (int)ICE, LF,
-            lds, nb, (size_t)pr.maxSharedMemoryPerMultiProcessor, fa.numRegs, (size_t)fa.localSizeBytes);
+    fprintf(stderr, "band<%d,%d,%d,%d,gate %d>: lds %zu B, blocks/CU %d, lds/CU %zu, regs %d, local %zu\n", B, S, (int)ICE, LF,
+            (int)GATE, lds, nb, (size_t)pr.maxSharedMemoryPerMultiProcessor, fa.numRegs, (size_t)fa.localSizeBytes);
   }
   hipLaunchKernelGGL(kern, dim3(list ? nlist : ch.count), dim3(B), lds, s, b, w, ch, o, list);
   if (variant_out) *variant_out = 9000000 + 1000 * (S - 1) + (ICE ? 100 : 0) + B / kWave;
   return hipGetLastError();
+}
+template <int B, int S, bool ICE, int LF, int WPS>
+hipError_t launch_band_one(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, hipStream_t s,
+                           const int32_t* list, int nlist, int* variant_out) {
+  if (o.kkt_predict > 0) return launch_band_one_g<B, S, ICE, LF, WPS, true>(b, w, ch, o, s, list, nlist, variant_out);
+  return launch_band_one_g<B, S, ICE, LF, WPS, false>(b, w, ch, o, s, list, nlist, variant_out);
 }
 
 }  // namespace

@@ -867,7 +867,9 @@ __host__ __device__ inline size_t ell_lds_bytes(int n, int m, int B, int XS, int
 
 // WPE: minimum waves per SIMD the register allocation must allow (the small-window variants run several
 // single- or two-wave workgroups per CU and need the occupancy; the large ones are sized by B alone).
-template <int B, int XS, int YS, int WX, int WY, int KR, int WPE = 1>
+// GATE: the predicted KKT gate compiled in only when dvh_options.kkt_predict > 0 (as pdhg_band_kernel: a runtime
+// branch kept both check paths' state live and spilled)
+template <int B, int XS, int YS, int WX, int WY, int KR, int WPE = 1, bool GATE = false>
 __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(WPE))) void pdhg_ell_kernel(
     const Batch b, const Work w, const Chunk ch, const Opts o, const int32_t* list) {
   constexpr int NW = B / kWave;
@@ -1447,7 +1449,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(WPE))) void p
 #pragma unroll
     for (int t = 4; t < kNRed; ++t) acc[t] = 0.0;
     double r = 0.0;
-    if (o.kkt_predict > 0) {  // predicted KKT gate: the restart sums first (kkt_gate_skip, dvh_device.h)
+    if constexpr (GATE) {  // predicted KKT gate: the restart sums first (kkt_gate_skip, dvh_device.h)
       double acc4[4] = {acc[0], acc[1], acc[2], acc[3]};
       block_sum1<B, 4, true>(acc4, red);
 #pragma unroll
@@ -1525,7 +1527,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(WPE))) void p
     }
     // readlane broadcast: the sums (and all decisions below) are uniform.  A restart-only check needs the
     // four movement norms alone (each wave-wide sum is ~25 VALU ops).
-    if (o.kkt_predict > 0) {
+    if constexpr (GATE) {
       if (kkt) {  // the KKT sums in the slots after the restart sums'
         double acc6[kNRed - 4];
 #pragma unroll
@@ -1542,7 +1544,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(WPE))) void p
 #pragma unroll
       for (int t = 0; t < 4; ++t) acc[t] = acc4[t];
     }
-    if (!(o.kkt_predict > 0)) r = sqrt(pw * acc[0] + acc[2] / pw);
+    if constexpr (!GATE) r = sqrt(pw * acc[0] + acc[2] / pw);
     if (kkt) {
       const double pobj = acc[6] + c0, dobj = acc[7] + acc[8] + c0;
       const double pres = sqrt(acc[4]) / (1.0 + qnorm), dres = sqrt(acc[5]) / (1.0 + cnorm);
@@ -1557,7 +1559,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(WPE))) void p
         status = kOptimal;
         break;
       }
-      gate.note(pres, dres, gap, o.eps, r);
+      if constexpr (GATE) gate.note(pres, dres, gap, o.eps, r);
       if (!(isfinite(pobj) && isfinite(dobj))) {
         status = kNumerical;
         break;
@@ -1655,7 +1657,8 @@ hipError_t launch_ell_one(const Batch& b, const Work& w, const Chunk& ch, const 
                           hipStream_t s, const int32_t* list, int nlist) {
   const size_t lds = ell_lds_bytes(max_n, max_m, B, XS, YS, WX, WY, KR);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  auto kern = pdhg_ell_kernel<B, XS, YS, WX, WY, KR, WPE>;
+  auto kern = o.kkt_predict > 0 ? pdhg_ell_kernel<B, XS, YS, WX, WY, KR, WPE, true>
+                                : pdhg_ell_kernel<B, XS, YS, WX, WY, KR, WPE, false>;
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3(list ? nlist : ch.count), dim3(B), lds, s, b, w, ch, o, list);
