@@ -17,6 +17,7 @@
 
 #include "../../include/dervet_hip.h"
 #include "dvh_internal.h"
+#include "dvh_validate.h"
 
 #define DVH_VERSION_STRING "dervet_hip 0.1.0 (gfx950, restarted reflected-Halpern PDHG)"
 
@@ -65,7 +66,10 @@ struct dvh_handle {
   DevBuf s_pairs, s_bad;                          // seeded-sweep warm transfer (dvh_sweep.hip)
   double outage_ms = 0.0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  // per-chunk timing events: a pool created on first use and reused by every solve (destroyed with the handle), so
+  // no exit path of a solve can leak them; chunk_used = the events of the last solve
   std::vector<std::array<hipEvent_t, 3>> chunk_events;
+  size_t chunk_used = 0;
   double timing[3] = {0, 0, 0};
   int last_variant = -1;
   int n_ell = 0, n_generic = 0, n_large = 0, n_band = 0, n_chain = 0;
@@ -223,6 +227,10 @@ int dvh_destroy(dvh_handle* h) {
   for (DevBuf* b : bufs) b->release();
   for (auto& e : h->ev)
     if (e) hipEventDestroy(e);
+  for (auto& ce : h->chunk_events)
+    for (hipEvent_t e : ce)
+      if (e) hipEventDestroy(e);
+  h->chunk_events.clear();
   if (h->large) dvh::large_destroy(h->large);
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;
@@ -504,7 +512,20 @@ extern "C" int dvh_build_battery_group(dvh_handle* h, const dvh_battery_group* g
   std::vector<int64_t> desc(8 * (size_t)g->G);
   DVH_HIP(h, hipMemcpyAsync(desc.data(), b->desc + 8 * (int64_t)first, desc.size() * sizeof(int64_t),
                             hipMemcpyDeviceToHost, s));
+  // the demand-charge rows' steps and tau columns index the window's base series and columns: range-checked here
+  // (an entry >= T or >= J made the kernel read base[] out of bounds and write column indices outside the
+  // window), in the same sync as the descriptors
+  std::vector<int32_t> dt_((size_t)g->mI), dj_((size_t)g->mI);
+  if (g->mI > 0) {
+    DVH_HIP(h, hipMemcpyAsync(dt_.data(), g->dcm_t, sizeof(int32_t) * dt_.size(), hipMemcpyDefault, s));
+    DVH_HIP(h, hipMemcpyAsync(dj_.data(), g->dcm_j, sizeof(int32_t) * dj_.size(), hipMemcpyDefault, s));
+  }
   DVH_HIP(h, hipStreamSynchronize(s));
+  for (int32_t i = 0; i < g->mI; ++i)
+    if (dt_[i] < 0 || dt_[i] >= g->T || dj_[i] < 0 || dj_[i] >= g->J)
+      return fail(h, DVH_ERR_ARG, "battery group: demand-charge row " + std::to_string(i) + " (step " +
+                                      std::to_string(dt_[i]) + ", column " + std::to_string(dj_[i]) +
+                                      ") outside T = " + std::to_string(g->T) + ", J = " + std::to_string(g->J));
   const int64_t T = g->T, n = 3 * T + g->J, m = T + 1 + g->mI, nnz = 4 * T + 3 * (int64_t)g->mI;
   for (int w = 0; w < g->G; ++w) {
     const int64_t* d = &desc[8 * (size_t)w];
@@ -696,17 +717,27 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
   DVH_HIP(h, h->d_list.ensure(I * (size_t)wc));
   h->n_ell = h->n_generic = h->n_large = h->n_band = h->n_chain = 0;
   h->large_ms[0] = h->large_ms[1] = 0.0f;
-  h->chunk_events.clear();
+  h->chunk_used = 0;
   DVH_HIP(h, hipEventRecord(h->ev[0], s));
   std::vector<double> scal;
   std::vector<int32_t> ist;
   for (const C& c : chunks) {
     if (c.nsmall == 0 && c.med.empty()) continue;
-    hipEvent_t e0, e1, e2;
-    DVH_HIP(h, hipEventCreate(&e0));
-    DVH_HIP(h, hipEventCreate(&e1));
-    DVH_HIP(h, hipEventCreate(&e2));
-    h->chunk_events.push_back({e0, e1, e2});
+    if (h->chunk_used == h->chunk_events.size()) {
+      std::array<hipEvent_t, 3> ce{nullptr, nullptr, nullptr};
+      for (hipEvent_t& e : ce) {
+        const hipError_t r = hipEventCreate(&e);
+        if (r != hipSuccess) {
+          for (hipEvent_t x : ce)
+            if (x) hipEventDestroy(x);
+          return hip_fail(h, r, "hipEventCreate");
+        }
+      }
+      h->chunk_events.push_back(ce);
+    }
+    const hipEvent_t e0 = h->chunk_events[h->chunk_used][0], e1 = h->chunk_events[h->chunk_used][1],
+                     e2 = h->chunk_events[h->chunk_used][2];
+    ++h->chunk_used;
     DVH_HIP(h, hipEventRecord(e0, s));
     if (c.nsmall > 0) DVH_HIP(h, dvh::launch_setup(b, w, c.ch, o, c.mn, c.mm, s));
     if (!c.med.empty()) {
@@ -868,74 +899,14 @@ static int finish_timing(dvh_handle* h, hipStream_t s) {
   float t = 0;
   h->timing[0] = h->timing[1] = h->timing[2] = 0;
   if (hipEventElapsedTime(&t, h->ev[0], h->ev[3]) == hipSuccess) h->timing[0] = t;
-  for (auto& ce : h->chunk_events) {
+  for (size_t i = 0; i < h->chunk_used; ++i) {
+    const auto& ce = h->chunk_events[i];
     if (hipEventElapsedTime(&t, ce[0], ce[1]) == hipSuccess) h->timing[1] += t;
     if (hipEventElapsedTime(&t, ce[1], ce[2]) == hipSuccess) h->timing[2] += t;
-    for (hipEvent_t e : ce) hipEventDestroy(e);
   }
-  h->chunk_events.clear();
   h->timing[1] += h->large_ms[0];
   h->timing[2] += h->large_ms[1];
   return DVH_OK;
-}
-
-static std::string validate(const dvh_lp& lp, int k) {
-  char buf[256];
-  const int m = lp.m_eq + lp.m_ineq;
-  if (lp.n <= 0 || lp.m_eq < 0 || lp.m_ineq < 0 || lp.nnz < 0) {
-    snprintf(buf, sizeof buf, "window %d: invalid sizes n=%d m_eq=%d m_ineq=%d nnz=%d", k, lp.n, lp.m_eq, lp.m_ineq,
-             lp.nnz);
-    return buf;
-  }
-  if (!lp.indptr || (lp.nnz > 0 && (!lp.indices || !lp.data)) || !lp.c || (m > 0 && !lp.q) || !lp.l || !lp.u) {
-    snprintf(buf, sizeof buf, "window %d: null array", k);
-    return buf;
-  }
-  if (lp.indptr[0] != 0 || lp.indptr[m] != lp.nnz) {
-    snprintf(buf, sizeof buf, "window %d: indptr[0] must be 0 and indptr[m] == nnz", k);
-    return buf;
-  }
-  for (int i = 0; i < m; ++i)
-    if (lp.indptr[i + 1] < lp.indptr[i]) {
-      snprintf(buf, sizeof buf, "window %d: indptr not monotone at row %d", k, i);
-      return buf;
-    }
-  for (int p = 0; p < lp.nnz; ++p) {
-    if (lp.indices[p] < 0 || lp.indices[p] >= lp.n) {
-      snprintf(buf, sizeof buf, "window %d: column index %d out of range at nnz %d", k, lp.indices[p], p);
-      return buf;
-    }
-    if (!std::isfinite(lp.data[p])) {
-      snprintf(buf, sizeof buf, "window %d: non-finite matrix value at nnz %d", k, p);
-      return buf;
-    }
-  }
-  for (int i = 0; i < m; ++i) {
-    // duplicate column within a row makes the transpose ambiguous for nothing; reject
-    for (int p = lp.indptr[i] + 1; p < lp.indptr[i + 1]; ++p)
-      for (int r = lp.indptr[i]; r < p; ++r)
-        if (lp.indices[r] == lp.indices[p]) {
-          snprintf(buf, sizeof buf, "window %d: duplicate column %d in row %d", k, lp.indices[p], i);
-          return buf;
-        }
-    if (!std::isfinite(lp.q[i])) {
-      snprintf(buf, sizeof buf, "window %d: non-finite rhs at row %d", k, i);
-      return buf;
-    }
-  }
-  for (int j = 0; j < lp.n; ++j) {
-    // crossed finite bounds (l > u) are a valid, infeasible window: status PRIMAL_INFEASIBLE (setup kernel)
-    if (!std::isfinite(lp.c[j]) || std::isnan(lp.l[j]) || std::isnan(lp.u[j]) || lp.l[j] == INFINITY ||
-        lp.u[j] == -INFINITY) {
-      snprintf(buf, sizeof buf, "window %d: invalid objective or bounds at variable %d", k, j);
-      return buf;
-    }
-  }
-  if (!std::isfinite(lp.c0)) {
-    snprintf(buf, sizeof buf, "window %d: non-finite c0", k);
-    return buf;
-  }
-  return "";
 }
 
 static int solve_batch_one(dvh_handle* h, const dvh_lp* lps, int32_t count, dvh_result* out);
@@ -1009,7 +980,7 @@ static int solve_batch_one(dvh_handle* h, const dvh_lp* lps, int32_t count, dvh_
   std::vector<int64_t> desc(8 * (size_t)count);
   int64_t tn = 0, tm = 0, tz = 0, tr = 0;
   for (int k = 0; k < count; ++k) {
-    std::string msg = validate(lps[k], k);
+    std::string msg = dvh::validate_lp(lps[k], k);
     if (!msg.empty()) return fail(h, DVH_ERR_ARG, msg);
     const dvh_lp& lp = lps[k];
     const int m = lp.m_eq + lp.m_ineq;

@@ -119,7 +119,12 @@ def cycle_damage(ene, e_rated, upper, life):
 
 
 class Degradation:
-    """Degradation state of S batteries (vectorised)."""
+    """Degradation state of S batteries (vectorised).
+
+    incl_cycle_degrade = False turns the whole module off, calendar loss included: dervet gates the degradation
+    calls on it (Battery.py:82, :101), and the reference's own test pins it -- 041-no_Degradation_Test_MP.csv has
+    yearly_degrade = 10 with incl_cycle_degrade = 0 and test_2finances.py:102-104 asserts the 2017 and 2022
+    avoided energy charges are equal (tests/test_degradation_ref.py)."""
 
     def __init__(self, e_rated, yearly_degrade=0.0, incl_cycle_degrade=True, table=None, eol_condition=80.0,
                  state_of_health=73.0, replaceable=True):
@@ -133,18 +138,39 @@ class Degradation:
         self.replaceable = np.broadcast_to(np.asarray(replaceable, bool), (S,)).copy()
         self.degrade_perc = np.zeros(S)
         self.replacements = np.zeros(S, np.int64)
+        self.skipped = np.zeros(S, np.int64)  # windows whose dispatch was not used (status not OPTIMAL / ITER_LIMIT)
+        self.years_degraded = [set() for _ in range(S)]  # Battery.py:104 years_system_degraded
 
     def capacity(self):
         """Effective energy capacity (kWh) the next window is built with."""
         return np.maximum(self.e_rated * (1.0 - self.degrade_perc), 0.0)
 
-    def update(self, ene, days):
-        """After a window of `days` days with SOE profiles ene [S, T]: returns this window's degradation [S]."""
+    def age(self, days):
+        """Calendar loss only, e.g. from the operation year's start to the first window (Battery.py:84-85)."""
+        if self.cycle and days > 0:
+            self.degrade_perc += self.yearly / 100.0 * (days / 365.0)
+
+    def update(self, ene, days, valid=None, year=None):
+        """After a window of `days` days with SOE profiles ene [S, T]: returns this window's degradation [S].
+        valid [S] (default all): rows whose dispatch is usable; the others take the calendar loss only (a window
+        that is infeasible or failed numerically has no SOE profile to count) and are counted in ``skipped``.
+        year: the window's first year, recorded when a battery reaches its state of health (Battery.py:102-104)."""
+        S = len(self.e_rated)
+        if not self.cycle:
+            return np.zeros(S)
         d = self.yearly / 100.0 * (days / 365.0)
-        if self.cycle:
-            d = d + cycle_damage(ene, self.e_rated, self.upper, self.life) * (1.0 - self.eol / 100.0)
+        ok = np.ones(S, bool) if valid is None else np.asarray(valid, bool)
+        if ok.any():
+            cyc = np.zeros(S)
+            cyc[ok] = cycle_damage(np.asarray(ene)[ok], self.e_rated[ok], self.upper, self.life)
+            d = d + cyc * (1.0 - self.eol / 100.0)
+        self.skipped += ~ok
         self.degrade_perc += d
-        worn = (self.capacity() <= self.e_rated * self.soh) & self.replaceable
+        reached = self.capacity() <= self.e_rated * self.soh
+        if year is not None:
+            for i in np.nonzero(reached)[0]:
+                self.years_degraded[i].add(int(year))
+        worn = reached & self.replaceable
         self.degrade_perc[worn] = 0.0
         self.replacements += worn
         return d
@@ -157,12 +183,14 @@ class DegradationSweep:
     e.g. ``lambda k, E: scenarios.config4(ids, E=E, only=[k])``); positions: the window ids in time order; dt: hours
     per step."""
 
-    def __init__(self, build, positions, degradation, dt=1.0, builder=None):
+    def __init__(self, build, positions, degradation, dt=1.0, builder=None, years=None):
         self.build, self.positions, self.deg, self.dt = build, list(positions), degradation, float(dt)
         self.builder = builder
+        self.years = years  # position -> the window's first year (replacement years, Battery.py:104), optional
 
     def run(self, solver, device="cuda:0"):
-        """Returns per position {k, iters [S], status [S], obj [S], degradation [S], capacity_before [S], ene [S, T]}.
+        """Returns per position {k, iters [S], status [S], obj [S], degradation [S], capacity_before [S], ene [S, T],
+        x (each window's primal solution)}.
         A solver with ``solve_packed`` (BatchSolver) gets the position's batch resident in HBM; any other solver
         with ``solve(lps)`` (e.g. the CPU restatement) gets WindowLPs.  When build returns device-builder specs
         (``scenarios.config4(..., spec=True)``) the windows are expanded on the GPU (lp/gpu_builder.py; ``builder``
@@ -189,6 +217,7 @@ class DegradationSweep:
                 del dev
                 T = int(d[0, 2]) - 1
                 ene = np.stack([x[int(r[6]) + 2 * T:int(r[6]) + 3 * T] for r in d])
+                xs = [x[int(r[6]):int(r[6]) + int(r[0])] for r in d]
             else:
                 lps = [lp for g in groups for lp in builder.group_window_lps(g)]
                 res = solver.solve(lps)
@@ -196,7 +225,11 @@ class DegradationSweep:
                 obj = np.array([r.obj for r in res])
                 T = lps[0].m_eq - 1
                 ene = np.stack([r.x[2 * T:3 * T] for r in res])
-            deg = self.deg.update(ene, T * self.dt / 24.0)
+                xs = [np.asarray(r.x) for r in res]
+            # only OPTIMAL / ITER_LIMIT dispatch is counted (an infeasible window's x is no SOE profile)
+            valid = np.isin(ist[:, 0], (0, 3))
+            deg = self.deg.update(ene, T * self.dt / 24.0, valid=valid,
+                                  year=None if self.years is None else self.years[k])
             out.append(dict(k=k, iters=ist[:, 1], status=ist[:, 0], obj=obj, degradation=deg, capacity_before=cap,
-                            ene=ene))
+                            ene=ene, x=xs))
         return out

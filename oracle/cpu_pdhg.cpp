@@ -17,6 +17,8 @@
 #include <vector>
 
 #include "../include/dervet_hip.h"
+// the product's host-side input validation (plain C++, der-vet_amd/csrc/dvh_validate.cpp), compiled in by build()
+#include "../der-vet_amd/csrc/dvh_validate.h"
 
 struct dvh_handle {
   dvh_options opts;
@@ -333,6 +335,13 @@ int dvh_set_options(dvh_handle* h, const dvh_options* opts) {
 int dvh_solve_batch(dvh_handle* h, const dvh_lp* lps, int32_t count, dvh_result* out) {
   if (!h) return DVH_ERR_ARG;
   if (count < 0 || (count > 0 && (!lps || !out))) return DVH_ERR_ARG;
+  for (int k = 0; k < count; ++k) {  // the same checks and messages as libdervet_hip's dvh_solve_batch
+    std::string msg = dvh::validate_lp(lps[k], k);
+    if (!msg.empty()) {
+      h->err = msg;
+      return DVH_ERR_ARG;
+    }
+  }
   const auto t0 = std::chrono::steady_clock::now();
   const dvh_options o = h->opts;
   if (h->threads > 0) omp_set_num_threads(h->threads);

@@ -17,10 +17,16 @@ LIB = os.path.join(HERE, "libdvh_cpu.so")
 SRC = os.path.join(HERE, "cpu_pdhg.cpp")
 
 
+VALIDATE = os.path.join(HERE, "..", "der-vet_amd", "csrc", "dvh_validate.cpp")
+DEPS = [SRC, VALIDATE, os.path.join(HERE, "..", "der-vet_amd", "csrc", "dvh_validate.h"),
+        os.path.join(HERE, "..", "include", "dervet_hip.h")]
+
+
 def build(force=False, verbose=False):
-    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= os.path.getmtime(SRC):
+    if not force and os.path.exists(LIB) and all(os.path.getmtime(LIB) >= os.path.getmtime(d) for d in DEPS):
         return LIB
-    cmd = ["g++", "-O3", "-march=x86-64-v2", "-std=c++17", "-fopenmp", "-fPIC", "-shared", "-o", LIB + ".tmp", SRC]
+    cmd = ["g++", "-O3", "-march=x86-64-v2", "-std=c++17", "-fopenmp", "-fPIC", "-shared", "-o", LIB + ".tmp", SRC,
+           VALIDATE]
     if verbose:
         print(" ".join(cmd))
     r = subprocess.run(cmd, capture_output=True, text=True)

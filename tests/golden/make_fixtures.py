@@ -16,6 +16,10 @@ Sources (all paths relative to /root/reference):
     objective_values}uc3.csv + Model_params/Usecase3/planned/*_Step2.csv        (DA + FR market windows)
   * test/test_validation_report_sept1/Results/Usecase2/<case>/step2/{simple_monthly_bill, pro_forma, npv}*.csv
     (per-window bills with / without the DERs, the pro forma and its NPV row: battery-benefit and CBA parity)
+  * test/test_storagevet_features/model_params/{040-Degradation_Test_MP, 041-no_Degradation_Test_MP,
+    010-degradation_test}.csv + test/datasets/000-040-degradation_test_{timeseries,tariff}.csv,
+    test/datasets/000-001-cycle.csv, data/battery_cycle_life.csv, data/hourly_timeseries.csv
+    (the reference's degradation cases, test_2finances.py:44-104 and test_3battery.py:74-75)
 
 Usage:  python tests/golden/make_fixtures.py [/root/reference]
 """
@@ -274,8 +278,61 @@ def make_bills():
     print("wrote bills", sorted(out))
 
 
+DEG_CASES = {
+    # name: (model params csv under test/test_storagevet_features/model_params, the reference test asserting on it)
+    "040": ("040-Degradation_Test_MP.csv", "test/test_storagevet_features/test_2finances.py:44-75"),
+    "041": ("041-no_Degradation_Test_MP.csv", "test/test_storagevet_features/test_2finances.py:78-104"),
+    "010": ("010-degradation_test.csv", "test/test_storagevet_features/test_3battery.py:74-75"),
+}
+
+
+def _ref_path(p):
+    """A model-parameter file path (Windows separators, relative to the reference root) under REF."""
+    return os.path.join(REF, *[c for c in p.replace("\\", "/").split("/") if c not in (".", "")])
+
+
+def make_degradation_cases():
+    """Inputs of the reference's degradation test cases: the battery / scenario / finance parameters, the active
+    value streams with their growth, the tariff and the cycle-life table.  The 040 / 041 time series has zero site
+    load (checked here), so their windows need only the tariff; 010's DA prices are data/hourly_timeseries.csv's
+    (checked equal to the bench fixture's column)."""
+    out = {}
+    mpdir = os.path.join(REF, "test", "test_storagevet_features", "model_params")
+    for name, (mp, asserted_by) in DEG_CASES.items():
+        params = read_params(os.path.join(mpdir, mp))
+        sc, bt, fi = params["Scenario"], params["Battery"], params.get("Finance", {})
+        _, ts = read_csv_cols(_ref_path(sc["time_series_filename"]))
+        streams = {t: {k: v for k, v in params[t].items() if k == "growth"} for t in params
+                   if t not in ("Scenario", "Battery", "Finance")}
+        cyc = np.loadtxt(_ref_path(bt["cycle_life_filename"]), delimiter=",", skiprows=1)
+        case = {
+            "source": "test/test_storagevet_features/model_params/" + mp,
+            "asserted_by": asserted_by,
+            "scenario": {k: sc[k] for k in ("opt_years", "start_year", "end_year", "n", "dt", "binary")},
+            "battery": {k: bt[k] for k in ("ch_max_rated", "dis_max_rated", "ene_max_rated", "ulsoc", "llsoc", "rte",
+                                           "sdr", "soc_target", "yearly_degrade", "incl_cycle_degrade",
+                                           "cycle_life_table_eol_condition", "state_of_health", "replaceable",
+                                           "operation_year", "hp", "fixedOM", "OMexpenses", "cycle_life_filename")},
+            "finance": {k: fi[k] for k in ("inflation_rate", "npv_discount_rate") if k in fi},
+            "value_streams": streams,
+            "cycle_life": {"upper": cyc[:, 0].tolist(), "life": cyc[:, 1].tolist()},
+            "time_series": sc["time_series_filename"],
+            "site_load_zero": bool(np.all(fcol(ts, "Site Load (kW)") == 0.0)),
+        }
+        if "retailTimeShift" in streams:
+            case["tariff"] = read_tariff(_ref_path(fi["customer_tariff_filename"]))
+        if "DA" in streams:
+            _, hd = read_csv_cols(os.path.join(REF, "data", "hourly_timeseries.csv"))
+            da = fcol(ts, "DA Price ($/kWh)")
+            case["da_price_is_bench_hourly_da_price"] = bool(np.array_equal(da, fcol(hd, "DA Price ($/kWh)")))
+        out[name] = case
+    with open(os.path.join(HERE, "degradation_cases.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+    print("wrote degradation cases", sorted(out))
+
+
 if __name__ == "__main__":
-    what = sys.argv[2:] or ["golden", "bench", "reliability", "market", "bills"]
+    what = sys.argv[2:] or ["golden", "bench", "reliability", "market", "bills", "degradation"]
     if "golden" in what:
         make_golden_cases()
     if "bench" in what:
@@ -286,3 +343,5 @@ if __name__ == "__main__":
         make_market_cases()
     if "bills" in what:
         make_bills()
+    if "degradation" in what:
+        make_degradation_cases()

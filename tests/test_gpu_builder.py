@@ -85,3 +85,15 @@ def test_seeded_sweep_on_device_built_windows_equals_host_built(gpu_solver):
         assert torch.equal(getattr(dh, f), getattr(dd, f)), f
     w = dd.window(5)
     assert np.array_equal(w["c"], sh.packed.window(5)["c"])
+
+
+@pytest.mark.parametrize("field,value", [("dcm_t", "T"), ("dcm_t", -1), ("dcm_j", "J")])
+def test_device_builder_rejects_demand_rows_outside_the_window(gpu_solver, field, value):
+    """dvh_build_battery_group range-checks the demand-charge rows' steps (< T) and tau columns (< J)
+    before the launch, instead of reading base[] and writing column indices outside the window."""
+    spec = scenarios.config4(range(1), spec=True)[0]
+    bad = np.array(getattr(spec, field), copy=True)
+    bad[len(bad) // 2] = getattr(spec, value) if isinstance(value, str) else value
+    setattr(spec, field, bad)
+    with pytest.raises(RuntimeError, match="demand-charge row"):
+        gpu_builder.pack_specs_device([spec], gpu_solver)

@@ -1,0 +1,35 @@
+"""GPU: the reference's degradation cases (tests/test_degradation_ref.py restates what they assert) through the
+product path -- every window position solved on cuda:0 by the band kernel, capacities updated from the GPU's SOE
+profiles -- and against the same sweep solved by HiGHS: per-year avoided charges within 1e-5 relative, capacities
+within 1e-6 relative, and the reference's assertions (040: 2017 saves more than 2022; 041: equal, exactly)."""
+import numpy as np
+import pytest
+
+import degradation_ref as dr
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name", ["040", "041", "010"])
+def test_reference_degradation_case_on_the_gpu(gpu_solver, name):
+    case = dr.cases()[name]
+    sw, _ = dr.sweep(case, spec=True)              # windows expanded on the GPU (device builder)
+    res = sw.run(gpu_solver)
+    assert all((p["status"] == 0).all() for p in res)
+    assert gpu_solver.kernel_stats()["band_windows"] == 1
+    hs, hb = dr.sweep(case)
+    av = dr.avoided_charges(case, sw, hb, res)     # terms evaluated on the host-built (bit-identical) windows
+    href = hs.run(dr.HighsSolver(), device=None)
+    hav = dr.avoided_charges(case, hs, hb, href)
+    for y in av:
+        assert av[y] == pytest.approx(hav[y], rel=1e-5), (y, av[y], hav[y])
+    caps = np.array([p["capacity_before"][0] for p in res])
+    hcaps = np.array([p["capacity_before"][0] for p in href])
+    assert np.allclose(caps, hcaps, rtol=1e-6, atol=0.0)
+    if name == "040":
+        assert av[2017] > av[2022]                   # test_2finances.py:67-69
+    if name == "041":
+        assert av[2017] == av[2022]                  # test_2finances.py:102-104: identical LPs, bitwise results
+    if name == "010":
+        assert sw.deg.replacements[0] == 0 and (np.diff(caps) <= 0).all()
+    print(f"{name}: avoided {av}, final capacity {sw.deg.capacity()[0]:.3f} kWh (HiGHS {hs.deg.capacity()[0]:.3f})")
