@@ -198,9 +198,13 @@ def main():
         t1 = time.time()
         dev = gpu_builder.pack_specs_device(specs, solver, f"cuda:{local}")
         desc = gpu_builder.desc_of(specs)[0]
+        specs_tags = [s_.tags for s_ in specs]
         del specs
     else:
-        hb = builder.pack_groups(make(scen))
+        groups = make(scen)
+        specs_tags = [g.tags for g in groups]
+        hb = builder.pack_groups(groups)
+        del groups
         t1 = time.time()
         dev = hb.to_torch(f"cuda:{local}").alloc_outputs()
         desc = np.asarray(hb.desc)
@@ -226,6 +230,10 @@ def main():
     runs = parallel.dispatch_runs(desc) if dist is not None else None
     tmax = max(r[4] for r in runs) if runs else 0
     gather = {}
+    tags_dev = None
+    if dist is not None:  # every gathered row carries its (scenario, window): no packing-order rebuild downstream
+        tg = sweep.tags if sweep is not None else [t for s_ in specs_tags for t in s_]
+        tags_dev = torch.as_tensor(parallel.tag_array(tg), device=f"cuda:{local}")
 
     def step():
         nonlocal gathered
@@ -238,7 +246,7 @@ def main():
             # the ch / dis / ene dispatch (fixed stride 3 * tmax); equal window counts per rank (weak scaling)
             torch.cuda.synchronize()
             tg = time.perf_counter()
-            rows = parallel.result_rows(dev.stats, dev.istats, dev.x, desc, tmax, runs)
+            rows = parallel.result_rows(dev.stats, dev.istats, dev.x, desc, tmax, runs, tags=tags_dev)
             gathered = parallel.gather_rows(rows, counts=[count] * world)
             torch.cuda.synchronize()
             gather.update(ms=round(1e3 * (time.perf_counter() - tg), 2), bytes_per_rank=int(rows.numel() * 8),
@@ -257,6 +265,8 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
     ms_per_step = 1e3 * el / args.steps
+    if gather:  # the all-gather's share of a step (this rank's last step)
+        gather["frac"] = round(gather["ms"] / ms_per_step, 4)
     windows_total = count * world
     value = windows_total / (el / args.steps)
 

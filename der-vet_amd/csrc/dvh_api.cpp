@@ -62,6 +62,8 @@ struct dvh_handle {
   DevBuf d_list, d_hinv;
   DevBuf m_list, m_plan, m_pos, m_xbuf, m_abort;  // medium tier (dvh_chain.hip)
   int chain_cap = -1;                             // resident 768-thread workgroups (cooperative limit)
+  long long spin_ticks = 0;                       // chain kernel: longest exchange wait (wall-clock ticks)
+  int n_chain_aborts = 0;                         // team launches that aborted (their unfinished windows ran grid-wide)
   DevBuf o_data, o_cases, o_len, o_hist, o_soe;  // reliability sweep
   DevBuf s_pairs, s_bad;                          // seeded-sweep warm transfer (dvh_sweep.hip)
   double outage_ms = 0.0;
@@ -539,70 +541,135 @@ extern "C" int dvh_build_battery_group(dvh_handle* h, const dvh_battery_group* g
   return DVH_OK;
 }
 
-// Medium tier over the candidates of one chunk (setup already run): plan, then the team kernel over the windows the
-// plan accepts; med_done[k] = 1 for the windows it solved or that the setup reported infeasible.  The others stay
-// with the grid-wide path.
+// Medium tier over the candidates of one chunk: plan (structure, segmentation, crossed bounds) -> setup of the
+// planned windows (the one-workgroup setup kernel, or grid-wide for n >= kMedSetupNMax) -> team launches: windows of
+// up to kChainMedMax segments together, longer ones (the 5-minute annual window) in launches of their own.
+// med_done[k] = 1 for the windows solved or reported infeasible; the others stay with the grid-wide path, and so do
+// the windows a launch had not finished when it aborted (a segment exchange outlasted the spin limit).
 static int chain_pass(dvh_handle* h, const dvh::Batch& b, const dvh::Work& w, const dvh::Chunk& ch,
-                      const dvh::Opts& o, const std::vector<int32_t>& med, int max_T, std::vector<char>& med_done,
-                      hipStream_t s) {
+                      const dvh::Opts& o, const std::vector<int32_t>& med, int max_T,
+                      const std::vector<int64_t>& desc, std::vector<char>& med_done, hipStream_t s) {
   const int nm = (int)med.size();
   if (nm == 0) return DVH_OK;
   const size_t I = sizeof(int32_t);
+  DVH_HIP(h, h->m_list.ensure(I * (size_t)nm));
+  DVH_HIP(h, hipMemcpyAsync(h->m_list.p, med.data(), I * nm, hipMemcpyHostToDevice, s));
   DVH_HIP(h, h->m_plan.ensure(I * (size_t)nm * dvh::kPlanInts));
   hipError_t e = dvh::launch_chain_plan(b, w, ch, h->m_list.as<int32_t>(), nm, max_T, h->m_plan.as<int32_t>(), s);
   if (e != hipSuccess) return hip_fail(h, e, "launch_chain_plan");
-  std::vector<int32_t> plan((size_t)nm * dvh::kPlanInts);
-  DVH_HIP(h, hipMemcpyAsync(plan.data(), h->m_plan.p, I * plan.size(), hipMemcpyDeviceToHost, s));
+  std::vector<int32_t> head((size_t)nm * 4);  // {P, T, J, k} of every plan record
+  DVH_HIP(h, hipMemcpy2DAsync(head.data(), 4 * I, h->m_plan.p, I * dvh::kPlanInts, 4 * I, nm, hipMemcpyDeviceToHost, s));
   DVH_HIP(h, hipStreamSynchronize(s));
-  std::vector<int32_t> pos;
-  int PT = 0;
+  std::vector<int32_t> small_setup, accepted;
   for (int i = 0; i < nm; ++i) {
-    const int P = plan[(size_t)i * dvh::kPlanInts];
-    if (P < 0) med_done[med[i]] = 1;  // crossed bounds: PRIMAL_INFEASIBLE from the setup kernel
-    if (P > 0) {
-      pos.push_back(i);
-      PT = std::max(PT, P);
-    }
+    const int P = head[4 * (size_t)i];
+    if (P < 0) med_done[med[i]] = 1;  // crossed bounds: PRIMAL_INFEASIBLE from the plan kernel
+    if (P <= 0) continue;
+    accepted.push_back(i);
+    if (desc[8 * (size_t)med[i]] < dvh::kMedSetupNMax) small_setup.push_back(med[i]);
   }
-  if (pos.empty()) return DVH_OK;
+  if (accepted.empty()) return DVH_OK;
+  // setup of the planned windows
+  if (!small_setup.empty()) {
+    int mn = 0;
+    for (int k : small_setup) mn = std::max<int>(mn, (int)desc[8 * (size_t)k]);
+    DVH_HIP(h, h->m_pos.ensure(I * small_setup.size()));
+    DVH_HIP(h, hipMemcpyAsync(h->m_pos.p, small_setup.data(), I * small_setup.size(), hipMemcpyHostToDevice, s));
+    e = dvh::launch_setup_medium(b, w, ch, o, mn, h->m_pos.as<int32_t>(), (int)small_setup.size(), s);
+    if (e != hipSuccess) return hip_fail(h, e, "launch_setup_medium");
+  }
+  for (int i : accepted) {
+    const int k = med[i];
+    if (desc[8 * (size_t)k] < dvh::kMedSetupNMax) continue;
+    e = dvh::launch_setup_long(b, w, ch, o, k, &desc[8 * (size_t)k], s);
+    if (e != hipSuccess) return hip_fail(h, e, "launch_setup_long");
+  }
+  // the one-workgroup setup flags windows it cannot scale (more long rows than its lists): those go grid-wide
+  std::vector<double> flag6(accepted.size(), 0.0);
+  for (size_t a = 0; a < accepted.size(); ++a)
+    DVH_HIP(h, hipMemcpyAsync(&flag6[a], w.scal + (int64_t)(med[accepted[a]] - ch.first) * dvh::kScal + 6,
+                              sizeof(double), hipMemcpyDeviceToHost, s));
+  DVH_HIP(h, hipStreamSynchronize(s));
+  std::vector<int32_t> groups[2];  // plan positions: [0] up to kChainMedMax segments, [1] longer
+  int PTg[2] = {0, 0};
+  for (size_t a = 0; a < accepted.size(); ++a) {
+    if (flag6[a] != 0.0) continue;
+    const int i = accepted[a], P = head[4 * (size_t)i];
+    const int g = P > dvh::kChainMedMax ? 1 : 0;
+    groups[g].push_back(i);
+    PTg[g] = std::max(PTg[g], P);
+  }
   if (h->chain_cap < 0) {
     int cap = 0;
     if (dvh::chain_capacity(h->device, &cap) != hipSuccess) cap = 0;
     (void)hipGetLastError();
     h->chain_cap = cap;
   }
+  if (h->spin_ticks <= 0) {
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device) != hipSuccess || khz <= 0) khz = 100000;
+    h->spin_ticks = (long long)khz * 1000 * 2;  // 2 s: a partner's hand-off normally takes microseconds
+  }
   const int S = h->chain_cap / 8;  // resident slots per XCD
-  const int NT = S >= PT ? dvh::chain_team_count(S, PT) : 0;
-  if (NT < 1) return DVH_OK;  // cannot keep a team resident: the grid-wide path takes them
-  DVH_HIP(h, h->m_pos.ensure(I * pos.size()));
-  DVH_HIP(h, hipMemcpyAsync(h->m_pos.p, pos.data(), I * pos.size(), hipMemcpyHostToDevice, s));
-  DVH_HIP(h, h->m_xbuf.ensure(dvh::chain_xbuf_bytes(NT, PT)));
-  DVH_HIP(h, h->m_abort.ensure(dvh::chain_abort_bytes(S)));
-  e = dvh::launch_chain(b, w, ch, o, h->m_pos.as<int32_t>(), (int)pos.size(), h->m_plan.as<int32_t>(), PT, S,
-                        h->m_xbuf.p, h->m_abort.as<int32_t>(), s);
-  if (e == hipErrorCooperativeLaunchTooLarge) {  // not resident after all: leave them to the grid-wide path
-    (void)hipGetLastError();
-    h->chain_cap = 0;
-    return DVH_OK;
-  }
-  if (e != hipSuccess) return hip_fail(h, e, "launch_chain");
-  std::vector<int32_t> ab(dvh::chain_abort_bytes(S) / I);
-  DVH_HIP(h, hipMemcpyAsync(ab.data(), h->m_abort.p, I * ab.size(), hipMemcpyDeviceToHost, s));
-  DVH_HIP(h, hipStreamSynchronize(s));
-  if (ab[0] != 0) {
-    std::string msg = "medium tier: a segment exchange timed out (PT " + std::to_string(PT) + ", NT " +
-                      std::to_string(NT) + "); workgroups {block: state list round entry tag seen}:";
-    for (int g = 0; g < 8 * S; ++g) {
-      const int32_t* d = &ab[16 + 8 * (size_t)g];
-      if (d[0] == 0) continue;
-      char buf[128];
-      snprintf(buf, sizeof buf, " %d: %d %d %d 0x%x 0x%x 0x%x;", g, d[0], d[1], d[2], d[3], d[4], d[5]);
-      msg += buf;
+  for (int g = 0; g < 2; ++g) {
+    const int PT = PTg[g];
+    if (groups[g].empty()) continue;
+    const int NT = S >= 1 && PT <= 8 * S ? dvh::chain_team_count(S, PT) : 0;
+    if (NT < 1) continue;  // cannot keep a team resident: the grid-wide path takes them
+    constexpr int kMaxPerLaunch = 0x3FFF - 2;  // window tags keep 14 bits of a team's window count
+    for (size_t a0 = 0; a0 < groups[g].size(); a0 += kMaxPerLaunch) {
+      const int np = (int)std::min<size_t>(kMaxPerLaunch, groups[g].size() - a0);
+      const int32_t* pos = groups[g].data() + a0;
+      std::vector<int32_t> ks(np);
+      for (int q = 0; q < np; ++q) ks[q] = med[pos[q]];
+      DVH_HIP(h, h->m_pos.ensure(I * 2 * (size_t)np));
+      int32_t* dpos = h->m_pos.as<int32_t>();
+      DVH_HIP(h, hipMemcpyAsync(dpos, pos, I * np, hipMemcpyHostToDevice, s));
+      DVH_HIP(h, hipMemcpyAsync(dpos + np, ks.data(), I * np, hipMemcpyHostToDevice, s));
+      e = dvh::launch_chain_mark(b, dpos + np, np, s);
+      if (e != hipSuccess) return hip_fail(h, e, "launch_chain_mark");
+      DVH_HIP(h, h->m_xbuf.ensure(dvh::chain_xbuf_bytes(NT, PT)));
+      DVH_HIP(h, h->m_abort.ensure(dvh::chain_abort_bytes(S)));
+      e = dvh::launch_chain(b, w, ch, o, dpos, np, h->m_plan.as<int32_t>(), PT, S, h->m_xbuf.p,
+                            h->m_abort.as<int32_t>(), h->spin_ticks, s);
+      if (e == hipErrorCooperativeLaunchTooLarge) {  // not resident after all: leave them to the grid-wide path
+        (void)hipGetLastError();
+        h->chain_cap = 0;
+        return DVH_OK;
+      }
+      if (e != hipSuccess) return hip_fail(h, e, "launch_chain");
+      std::vector<int32_t> ab(dvh::chain_abort_bytes(S) / I);
+      DVH_HIP(h, hipMemcpyAsync(ab.data(), h->m_abort.p, I * ab.size(), hipMemcpyDeviceToHost, s));
+      DVH_HIP(h, hipStreamSynchronize(s));
+      if (ab[0] != 0) {
+        // a segment exchange outlasted the spin limit: the windows the launch finished keep their results, the
+        // others (still marked pending) go to the grid-wide path; the diagnostics stay readable in dvh_last_error
+        std::string msg = "medium tier: a segment exchange timed out (PT " + std::to_string(PT) + ", NT " +
+                          std::to_string(NT) + "); unfinished windows moved to the grid-wide path; workgroups "
+                          "{block: state list round entry tag seen}:";
+        for (int gb = 0; gb < 8 * S; ++gb) {
+          const int32_t* d = &ab[16 + 8 * (size_t)gb];
+          if (d[0] == 0) continue;
+          char buf[128];
+          snprintf(buf, sizeof buf, " %d: %d %d %d 0x%x 0x%x 0x%x;", gb, d[0], d[1], d[2], d[3], d[4], d[5]);
+          msg += buf;
+        }
+        h->err = msg;
+        ++h->n_chain_aborts;
+        std::vector<int32_t> st(2);
+        for (int q = 0; q < np; ++q) {
+          DVH_HIP(h, hipMemcpy(st.data(), b.istats + 2 * (int64_t)ks[q], 2 * I, hipMemcpyDeviceToHost));
+          if (st[0] != dvh::kChainPending) {
+            med_done[ks[q]] = 1;
+            ++h->n_chain;
+          }
+        }
+        continue;
+      }
+      for (int q = 0; q < np; ++q) med_done[ks[q]] = 1;
+      h->n_chain += np;
     }
-    return fail(h, DVH_ERR_HIP, msg);
   }
-  for (int i : pos) med_done[med[i]] = 1;
-  h->n_chain += (int)pos.size();
   return DVH_OK;
 }
 
@@ -649,7 +716,7 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
     const int64_t* d = &desc[8 * (size_t)k];
     const int64_t T = d[2] - 1;
     return chain_on && is_large(k) && T > dvh::kChainB && T <= (int64_t)dvh::kPMax * dvh::kChainB &&
-           d[0] >= 3 * T && d[0] <= 3 * T + dvh::kChainJMax && d[1] <= 2 * T + 1 && d[0] < 40000;
+           d[0] >= 3 * T && d[0] <= 3 * T + dvh::kChainJMax && d[1] <= 2 * T + 1;
   };
   std::vector<int> large;
   std::vector<char> med_done(count, 0);  // solved (or reported infeasible) by the medium tier
@@ -740,15 +807,9 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
     ++h->chunk_used;
     DVH_HIP(h, hipEventRecord(e0, s));
     if (c.nsmall > 0) DVH_HIP(h, dvh::launch_setup(b, w, c.ch, o, c.mn, c.mm, s));
-    if (!c.med.empty()) {
-      DVH_HIP(h, h->m_list.ensure(I * c.med.size()));
-      DVH_HIP(h, hipMemcpyAsync(h->m_list.p, c.med.data(), I * c.med.size(), hipMemcpyHostToDevice, s));
-      hipError_t e = dvh::launch_setup_medium(b, w, c.ch, o, c.med_n, h->m_list.as<int32_t>(), (int)c.med.size(), s);
-      if (e != hipSuccess) return hip_fail(h, e, "launch_setup_medium");
-    }
     DVH_HIP(h, hipEventRecord(e1, s));
     if (c.nsmall == 0) {
-      if (int rc = chain_pass(h, b, w, c.ch, o, c.med, c.med_T, med_done, s)) return rc;
+      if (int rc = chain_pass(h, b, w, c.ch, o, c.med, c.med_T, desc, med_done, s)) return rc;
       DVH_HIP(h, hipEventRecord(e2, s));
       continue;
     }
@@ -876,7 +937,7 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
       if (variant < 0) variant = gv;
       DVH_HIP(h, hipStreamSynchronize(s));  // d_list is reused by the next chunk
     }
-    if (int rc = chain_pass(h, b, w, c.ch, o, c.med, c.med_T, med_done, s)) return rc;
+    if (int rc = chain_pass(h, b, w, c.ch, o, c.med, c.med_T, desc, med_done, s)) return rc;
     DVH_HIP(h, hipEventRecord(e2, s));
     h->last_variant = variant;
   }

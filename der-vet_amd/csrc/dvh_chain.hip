@@ -32,6 +32,7 @@
 //
 // Same algorithm, scaling, steps and checks as the band kernel (restated in oracle/pdlp_ref.py); a segment's
 // arithmetic is the band kernel's for its steps, so results agree with the on-chip kernels to rounding.
+#include <algorithm>
 #include <type_traits>
 
 #include "dvh_device.h"
@@ -40,8 +41,8 @@ namespace dvh {
 namespace {
 
 constexpr int kCB = kChainB;  // threads (and maximum steps) per segment
-constexpr int kJSeg = 4;      // tau columns per segment
-constexpr int kXSeg = 100;    // granules per segment in the exchange buffer
+constexpr int kJSeg = kChainJSeg;  // tau columns per segment
+constexpr int kXSeg = 140;    // granules per segment in the exchange buffer
 // granule offsets inside a segment's area (p = round parity)
 constexpr int kOffD = 0;      // + 2p: reflected first ene (down, to s-1)
 constexpr int kOffU = 4;      // + 6p: reflected ch, dis, ene of the last step (up, to s+1)
@@ -50,10 +51,11 @@ constexpr int kOffK = 32;     // + 12p: KKT images {first ene, 4 tau partials}
 constexpr int kOffC = 56;     // + 20p + 2v: check partial sums
 constexpr int kOffW = 96;     // + p: the team's next window (segment 0's area)
 constexpr int kOffAck = 98;   // + p: this segment has read it
+constexpr int kOffT = 100;    // + 20p + 2v: check sums over all segments (segment 0's area: the leader's)
 // poll-list entries per segment: A [0, 256), K [256, 512), C [512, 1016), up [1016, 1022), down [1022, 1024)
 constexpr int kPollMax = 1024;
 constexpr int kPollK = 256, kPollC = 512, kPollU = 1016, kPollD = 1022;
-constexpr unsigned kSpinMax = 1u << 22;
+static_assert(kPMax - 1 <= kPollU - kPollC, "the window hand-out's acknowledgements fit the C list");
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) int gi32;
@@ -92,44 +94,57 @@ __device__ __forceinline__ void put_f64(gu64* g, unsigned tag, double v) {
 // LDS layout (doubles): XE[B+1] YS[B+1] XT[4] XK[4] GK[4] red[kNRed(NW+1)+4] TP[4][B] XP[3][B] YP[2][B]
 //   CR[kPMax][kNRed]
 //   RO[6][B] (objective and upper bound of the lane's ch, dis, ene: read-only, kept out of VGPRs)
-//   | ints: poll offsets [kPollMax], poll values [kPollMax], misc[16]
+//   | ints: poll offsets [kPollMax], poll values [kPollMax], misc[32]
 __host__ __device__ inline size_t chain_lds_doubles() {
   const int NW = kCB / kWave;
   return 2 * (size_t)(kCB + 1) + 12 + (size_t)kNRed * (NW + 1) + 4 + (size_t)kJSeg * kCB + 5 * (size_t)kCB +
          (size_t)kPMax * kNRed + 6 * (size_t)kCB;
 }
 __host__ __device__ inline size_t chain_lds_bytes() {
-  return align16(sizeof(double) * chain_lds_doubles()) + sizeof(int32_t) * (2 * (size_t)kPollMax + 16);
+  return align16(sizeof(double) * chain_lds_doubles()) + sizeof(int32_t) * (2 * (size_t)kPollMax + 32);
 }
 
 // ---------------------------------------------------------------------------------------------------------------
-// Plan: one workgroup per listed window.  Verifies the battery + DCM pattern (as the band kernel), writes the
-// step -> DCM row / tau maps into the window's vbuf workspace, and cuts the steps into segments greedily: a new
-// segment starts when the current one holds kCB steps, when a step brings a tau column the segment has no slot
-// left for, or where a run of steps of one tau column begins that would not end inside the current segment but
-// fits in a segment of its own (so demand periods that fit are not split).  plan[0] = P (0: not this tier;
-// -1: already reported by the setup kernel).
+// Plan: one workgroup per listed window, before the setup (it reads only the window's unscaled data).  Reports crossed
+// bounds (plan[0] = -1, status PRIMAL_INFEASIBLE as the setup kernel would), verifies the battery + DCM pattern (as
+// the band kernel), writes the step -> DCM row / tau maps into the window's vbuf workspace, and cuts the steps into
+// segments greedily: a new segment starts when the current one holds kCB steps, when a step brings a tau column the
+// segment has no slot left for, or where a run of steps of one tau column begins that would not end inside the
+// current segment but fits in a segment of its own (so demand periods that fit are not split).  The greedy walks the
+// RUNS of equal tau ids (compacted in parallel), not the steps: a 5-minute annual window (105,120 steps) with monthly
+// demand columns has 12 runs.  A column's sharers must be a contiguous range of segments; a segment inside the range
+// that has none of the column's rows holds it in a free slot (its partials are zero), or the window is not planned.
+// plan[0] = P (0: not this tier, -1: crossed bounds, reported).
 // ---------------------------------------------------------------------------------------------------------------
 constexpr int kPlanB = 1024;
+constexpr int kRunsLds = 16384;  // run starts staged in LDS; more runs are read from the window's wbuf workspace
 
 __global__ __launch_bounds__(kPlanB) void chain_plan_kernel(const Batch b, const Work w, const Chunk ch,
                                                             const int32_t* list, int32_t* plan) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  int32_t* jl = reinterpret_cast<int32_t*>(smem);  // [T] tau id per step (-1: no DCM row)
-  int32_t* re = jl + kPMax * kCB;                   // [T] end of the run of equal tau ids through step t
-  __shared__ int32_t jmask[kChainJMax];
+  int32_t* rs_lds = reinterpret_cast<int32_t*>(smem);  // [kRunsLds + 1] run starts
+  __shared__ int32_t colLo[kChainJMax], colHi[kChainJMax];
   __shared__ int32_t set[kJSeg];
-  __shared__ int flag;
+  __shared__ int32_t wtot[kPlanB / kWave];
   const int k = list[blockIdx.x];
-  const int kl = k - ch.first;
   const WinOff W = win_offsets(b, ch, k);
   const int n = W.n, m = W.m, meq = W.meq;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   int32_t* pl = plan + (int64_t)blockIdx.x * kPlanInts;
-  const double* scal = w.scal + (int64_t)kl * kScal;
-  if (scal[6] != 0.0) {  // crossed bounds (reported) or unsupported structure
-    if (tid == 0) pl[0] = scal[6] == 3.0 ? -1 : 0;
-    return;
+  // 0. crossed bounds: infeasible as given (as setup_kernel step 0)
+  {
+    int crossed = 0;
+    for (int j = tid; j < n; j += kPlanB) crossed |= b.l[W.on + j] > b.u[W.on + j];
+    if (__syncthreads_or(crossed)) {
+      if (tid == 0) {
+        pl[0] = -1;
+        w.scal[(int64_t)(k - ch.first) * kScal + 6] = 3.0;
+        b.istats[2 * k] = 1;  // DVH_PRIMAL_INFEASIBLE
+        b.istats[2 * k + 1] = 0;
+        for (int u = 0; u < 4; ++u) b.stats[4 * k + u] = u == 0 ? NAN : 0.0;
+      }
+      return;
+    }
   }
   const int T = meq - 1, J = n - 3 * T, MI = m - meq;
   if (T < 1 || T > kPMax * kCB || J < 0 || J > kChainJMax || MI < 0 || MI > T || (J == 0 && MI > 0)) {
@@ -138,14 +153,16 @@ __global__ __launch_bounds__(kPlanB) void chain_plan_kernel(const Batch b, const
   }
   const int32_t* gkp = b.indptr + W.row;
   const int32_t* gkc = b.indices + W.nz;
-  const double* ls = w.ls + W.wn;
+  const double* lo = b.l + W.on;
   int32_t* dm = reinterpret_cast<int32_t*>(w.vbuf + W.wn);  // [T] DCM row, [T..2T) tau id
   for (int t = tid; t < T; t += kPlanB) {
     dm[t] = -1;
     dm[T + t] = -1;
   }
-  for (int j = tid; j < kChainJMax; j += kPlanB) jmask[j] = 0;
-  if (tid == 0) flag = 0;
+  for (int j = tid; j < kChainJMax; j += kPlanB) {
+    colLo[j] = 0x7fffffff;
+    colHi[j] = -1;
+  }
   __syncthreads();
   int bad = 0;
   for (int r = tid; r <= T; r += kPlanB) {
@@ -166,7 +183,7 @@ __global__ __launch_bounds__(kPlanB) void chain_plan_kernel(const Batch b, const
       if (kind == 4 || ((seen >> kind) & 1u)) bad = 1;
       seen |= 1u << kind;
     }
-    bad |= ls[t] != 0.0 || ls[T + t] != 0.0;  // no lower bound kept for ch / dis
+    bad |= lo[t] != 0.0 || lo[T + t] != 0.0;  // no lower bound kept for ch / dis (l / Dc == 0 iff l == 0)
   }
   for (int i = meq + tid; i < m; i += kPlanB) {
     const int p0 = gkp[i], len = gkp[i + 1] - p0;
@@ -204,42 +221,252 @@ __global__ __launch_bounds__(kPlanB) void chain_plan_kernel(const Batch b, const
     if (tid == 0) pl[0] = 0;
     return;
   }
-  for (int t = tid; t < T; t += kPlanB) jl[t] = dm[T + t];
+  // 1. runs of equal tau ids: starts compacted in step order (ballot per wave, wave totals scanned per chunk)
+  int32_t* rs_g = reinterpret_cast<int32_t*>(w.wbuf + W.wm);  // [T + 1] when they do not fit LDS (m >= T + 1)
+  int R = 0;
+  for (int base = 0; base < T; base += kPlanB) {
+    const int t = base + tid;
+    const bool st = t < T && (t == 0 || dm[T + t] != dm[T + t - 1]);
+    const unsigned long long bal = __ballot(st);
+    if (lane == 0) wtot[wid] = __popcll(bal);
+    __syncthreads();
+    int off = R;
+    for (int u = 0; u < wid; ++u) off += wtot[u];
+    int tot = 0;
+    for (int u = 0; u < kPlanB / kWave; ++u) tot += wtot[u];
+    if (st) {
+      const int pos = off + __popcll(bal & ((1ull << lane) - 1ull));
+      rs_g[pos] = t;
+      if (pos < kRunsLds) rs_lds[pos] = t;
+    }
+    R += tot;
+    __syncthreads();
+  }
   __syncthreads();
+  // 2. the greedy over the runs (thread 0)
   if (tid == 0) {
-    for (int t = T - 1; t >= 0; --t) re[t] = (t + 1 < T && jl[t + 1] == jl[t]) ? re[t + 1] : t + 1;
+    const int32_t* rs = R < kRunsLds ? rs_lds : rs_g;
+    const int32_t* jl = dm + T;
     int P = 0, s0 = 0, ns = 0, ok = 1;
-    pl[4] = 0;
-    for (int t = 0; t <= T && ok; ++t) {
-      const int j = t < T ? jl[t] : -1;
+    pl[kPlanStart] = 0;
+    auto close = [&](int t) {  // segment P = [s0, t)
+      if (P >= kPMax) {
+        ok = 0;
+        return;
+      }
+      for (int u = 0; u < kJSeg; ++u) {
+        const int id = u < ns ? set[u] : -1;
+        pl[kPlanSlot + 4 * P + u] = id;
+        if (id >= 0) {
+          colLo[id] = min(colLo[id], P);
+          colHi[id] = max(colHi[id], P);
+        }
+      }
+      ++P;
+      pl[kPlanStart + P] = t;
+      s0 = t;
+      ns = 0;
+    };
+    for (int r = 0; r < R && ok; ++r) {
+      const int a = rs[r], e = r + 1 < R ? rs[r + 1] : T;
+      const int j = jl[a];
       bool newj = j >= 0;
       for (int u = 0; u < ns && newj; ++u) newj = set[u] != j;
-      const bool run_cut = t < T && t > s0 && jl[t] != jl[t - 1] && re[t] - s0 > kCB && re[t] - t <= kCB;
-      if (t == T || t - s0 == kCB || (newj && ns == kJSeg) || run_cut) {  // close segment P = [s0, t)
-        for (int u = 0; u < kJSeg; ++u) {
-          pl[24 + 4 * P + u] = u < ns ? set[u] : -1;
-          if (u < ns) jmask[set[u]] |= 1 << P;
-        }
-        ++P;
-        pl[4 + P] = t;
-        s0 = t;
-        ns = 0;
-        if (t == T) break;
-        if (P >= kPMax) ok = 0;
+      const bool run_cut = a > s0 && e - s0 > kCB && e - a <= kCB;
+      if (a - s0 == kCB || (newj && ns == kJSeg) || run_cut) {
+        close(a);
         newj = j >= 0;
       }
-      if (newj) set[ns++] = j;
+      if (newj && ok) set[ns++] = j;
+      while (ok && e - s0 > kCB) {  // full segments inside the run
+        close(s0 + kCB);
+        if (j >= 0) set[ns++] = j;
+      }
     }
-    for (int j = 0; j < J; ++j) ok &= jmask[j] != 0;  // every tau column has rows (its update has an owner)
-    for (int s = 0; s < P && ok; ++s)
+    if (ok) close(T);
+    // sharers: a contiguous range of segments, each holding the column in a slot (a free slot if it has no rows)
+    for (int jj = 0; jj < J && ok; ++jj) {
+      if (colHi[jj] < 0) {
+        ok = 0;  // a tau column without rows: its update has no owner
+        break;
+      }
+      for (int sg = colLo[jj] + 1; sg < colHi[jj] && ok; ++sg) {
+        int u = 0, fr = -1;
+        for (; u < kJSeg; ++u) {
+          const int id = pl[kPlanSlot + 4 * sg + u];
+          if (id == jj) break;
+          if (id < 0 && fr < 0) fr = u;
+        }
+        if (u == kJSeg) {
+          if (fr < 0) ok = 0;
+          else pl[kPlanSlot + 4 * sg + fr] = jj;
+        }
+      }
+    }
+    for (int sg = 0; sg < P && ok; ++sg)
       for (int u = 0; u < kJSeg; ++u) {
-        const int id = pl[24 + 4 * s + u];
-        pl[88 + 4 * s + u] = id >= 0 ? jmask[id] : 0;
+        const int id = pl[kPlanSlot + 4 * sg + u];
+        pl[kPlanLo + 4 * sg + u] = id >= 0 ? colLo[id] : 0;
+        pl[kPlanHi + 4 * sg + u] = id >= 0 ? colHi[id] : -1;
       }
     pl[1] = T;
     pl[2] = J;
     pl[3] = k;
     pl[0] = ok ? P : 0;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Grid-wide setup of one planned window too large for the one-workgroup setup kernel (n >= kMedSetupNMax: the
+// 5-minute annual window).  The same scaling as setup_kernel (Ruiz inf-norm passes, one Pock-Chambolle pass,
+// oracle/pdlp_ref.py), with the columns' entries located through the plan's step maps instead of a transpose: ch_t
+// and dis_t sit in row t + 1 (their SOE row) and their DCM row, ene_t in rows t and t + 1, tau_j in the DCM rows of
+// its steps (a workgroup per tau column, fixed summation order).  Writes what the chain kernel reads: scaled K in CSR
+// order (kval), Dr / Dc, scaled c / l / u / q, and scal[0..3, 6, 7].
+// ---------------------------------------------------------------------------------------------------------------
+constexpr int kLB = 256;
+
+struct LongArgs {
+  Batch b;
+  Work w;
+  WinOff W;
+  int k, kl, T, J, n, m;
+};
+
+__device__ __forceinline__ double long_entry(const LongArgs& a, int r, int col) {  // K(r, col), 0 if absent
+  const int32_t* kp = a.b.indptr + a.W.row;
+  const int32_t* kc = a.b.indices + a.W.nz;
+  const double* kv = a.b.data + a.W.nz;
+  for (int p = kp[r]; p < kp[r + 1]; ++p)
+    if (kc[p] == col) return kv[p];
+  return 0.0;
+}
+
+__global__ __launch_bounds__(kLB) void long_init(LongArgs a) {
+  const int t = blockIdx.x * kLB + threadIdx.x;
+  if (t < a.n) a.w.dc[a.W.wn + t] = 1.0;
+  if (t < a.m) a.w.dr[a.W.wm + t] = 1.0;
+}
+
+template <bool MAXR>
+__global__ __launch_bounds__(kLB) void long_pass(LongArgs a) {
+  const int t = blockIdx.x * kLB + threadIdx.x;
+  const double* Dr = a.w.dr + a.W.wm;
+  const double* Dc = a.w.dc + a.W.wn;
+  auto acc_of = [](double acc, double v) { return MAXR ? fmax(acc, v) : acc + v; };
+  if (t < a.m) {
+    const int32_t* kp = a.b.indptr + a.W.row;
+    const int32_t* kc = a.b.indices + a.W.nz;
+    const double* kv = a.b.data + a.W.nz;
+    double acc = 0.0;
+    for (int p = kp[t]; p < kp[t + 1]; ++p) acc = acc_of(acc, fabs(kv[p]) * Dr[t] * Dc[kc[p]]);
+    a.w.tmpr[a.W.wm + t] = acc > 0.0 ? 1.0 / sqrt(acc) : 1.0;
+  }
+  if (t < 3 * a.T) {
+    const int T = a.T, v = t / T, st = t - v * T;
+    const int32_t* dm = reinterpret_cast<const int32_t*>(a.w.vbuf + a.W.wn);
+    const int r1 = v < 2 ? st + 1 : st, r2 = v < 2 ? dm[st] : st + 1;  // ascending rows
+    double acc = fabs(long_entry(a, r1, t)) * Dc[t] * Dr[r1];
+    if (r2 >= 0) acc = acc_of(acc, fabs(long_entry(a, r2, t)) * Dc[t] * Dr[r2]);
+    a.w.tmpc[a.W.wn + t] = acc > 0.0 ? 1.0 / sqrt(acc) : 1.0;
+  }
+}
+
+// one workgroup per tau column: its DCM rows in step order, partials per thread (strided), then in thread order
+template <bool MAXR>
+__global__ __launch_bounds__(kLB) void long_tau_pass(LongArgs a) {
+  __shared__ double red[kLB];
+  const int j = blockIdx.x, col = 3 * a.T + j, T = a.T;
+  const double* Dr = a.w.dr + a.W.wm;
+  const double* Dc = a.w.dc + a.W.wn;
+  const int32_t* dm = reinterpret_cast<const int32_t*>(a.w.vbuf + a.W.wn);
+  double acc = 0.0;
+  for (int t = threadIdx.x; t < T; t += kLB) {
+    if (dm[T + t] != j) continue;
+    const int r = dm[t];
+    const double v = fabs(long_entry(a, r, col)) * Dc[col] * Dr[r];
+    acc = MAXR ? fmax(acc, v) : acc + v;
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    for (int u = 0; u < kLB; ++u) s = MAXR ? fmax(s, red[u]) : s + red[u];
+    a.w.tmpc[a.W.wn + col] = s > 0.0 ? 1.0 / sqrt(s) : 1.0;
+  }
+}
+
+__global__ __launch_bounds__(kLB) void long_apply(LongArgs a) {
+  const int t = blockIdx.x * kLB + threadIdx.x;
+  if (t < a.n) a.w.dc[a.W.wn + t] *= a.w.tmpc[a.W.wn + t];
+  if (t < a.m) a.w.dr[a.W.wm + t] *= a.w.tmpr[a.W.wm + t];
+}
+
+// scaled data, reciprocal scalings, per-workgroup norm partials (wbuf scratch: [block][4])
+__global__ __launch_bounds__(kLB) void long_fill(LongArgs a) {
+  __shared__ double red[4 * (kLB / kWave)];
+  const int t = blockIdx.x * kLB + threadIdx.x;
+  const double* Dr = a.w.dr + a.W.wm;
+  const double* Dc = a.w.dc + a.W.wn;
+  double nrm[4] = {0.0, 0.0, 0.0, 0.0};  // ||cs||^2, ||qs||^2, ||c||^2, ||q||^2
+  if (t < a.m) {
+    const int32_t* kp = a.b.indptr + a.W.row;
+    const int32_t* kc = a.b.indices + a.W.nz;
+    const double* kv = a.b.data + a.W.nz;
+    const double d = Dr[t];
+    for (int p = kp[t]; p < kp[t + 1]; ++p) a.w.kval[a.W.wz + p] = kv[p] * d * Dc[kc[p]];
+    const double qi = a.b.q[a.W.om + t];
+    a.w.qs[a.W.wm + t] = qi * d;
+    a.w.tmpr[a.W.wm + t] = 1.0 / d;
+    nrm[1] = qi * d * qi * d;
+    nrm[3] = qi * qi;
+  }
+  if (t < a.n) {
+    const double cj = a.b.c[a.W.on + t], d = Dc[t];
+    a.w.cs[a.W.wn + t] = cj * d;
+    a.w.ls[a.W.wn + t] = a.b.l[a.W.on + t] / d;
+    a.w.us[a.W.wn + t] = a.b.u[a.W.on + t] / d;
+    a.w.tmpc[a.W.wn + t] = 1.0 / d;
+    nrm[0] = cj * d * cj * d;
+    nrm[2] = cj * cj;
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) nrm[u] = wave_sum(nrm[u]);
+  if (lane == 0)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) red[4 * wid + u] = nrm[u];
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    double s = 0.0;
+    for (int q = 0; q < kLB / kWave; ++q) s += red[4 * q + threadIdx.x];
+    a.w.wbuf[a.W.wm + 4 * (int64_t)blockIdx.x + threadIdx.x] = s;
+  }
+}
+
+__global__ __launch_bounds__(kLB) void long_norms(LongArgs a, int nblk, double step_safety) {
+  __shared__ double red[4 * kLB];
+  double v[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int q = threadIdx.x; q < nblk; q += kLB)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] += a.w.wbuf[a.W.wm + 4 * (int64_t)q + u];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) red[4 * threadIdx.x + u] = v[u];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int q = 0; q < kLB; ++q)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s[u] += red[4 * q + u];
+    double* scal = a.w.scal + (int64_t)a.kl * kScal;
+    const double ncs = sqrt(s[0]), nqs = sqrt(s[1]);
+    scal[0] = step_safety;  // refined by the chain kernel's power iteration
+    scal[1] = (ncs > 1e-10 && nqs > 1e-10) ? ncs / nqs : 1.0;
+    scal[2] = sqrt(s[2]);
+    scal[3] = sqrt(s[3]);
+    scal[4] = scal[5] = 0.0;
+    scal[6] = 0.0;
+    scal[7] = 1.0;
   }
 }
 
@@ -254,14 +481,21 @@ struct ChainArgs {
   int* abort_word;           // zeroed before the launch (with the diagnostics); [0] abort, [8] next window
   int PT, NT;
   int S;                     // workgroup slots per XCD (grid = 8 S)
+  long long spin_ticks;      // longest wait for a partner's exchange (wall-clock ticks) before the launch aborts
 };
 
 // Team and segment of workgroup b: blocks b and b + 8 share an XCD (round-robin dispatch, MI355X_MICROARCH.md --
 // a speed assumption only, never a correctness one), so each XCD's first floor(S / PT) * PT slots form local
-// teams and the remaining slots of all XCDs are pooled into further teams.  team >= NT: idle.
+// teams and the remaining slots of all XCDs are pooled into further teams.  A team larger than an XCD (PT > S: the
+// long windows) takes consecutive segments from one XCD's slots before the next XCD's, so only the few boundaries
+// between XCDs hand off across L2s.  team >= NT: idle.
 __host__ __device__ inline void chain_team_of(int b, int S, int PT, int* team, int* seg) {
   const int xcd = b % 8, slot = b / 8, LT = S / PT, used = LT * PT;
-  if (slot < used) {
+  if (PT > S) {
+    const int li = xcd * S + slot;
+    *team = li / PT;
+    *seg = li % PT;
+  } else if (slot < used) {
     *team = xcd * LT + slot / PT;
     *seg = slot % PT;
   } else {
@@ -271,6 +505,7 @@ __host__ __device__ inline void chain_team_of(int b, int S, int PT, int* team, i
   }
 }
 __host__ __device__ inline int chain_teams(int S, int PT) {
+  if (PT > S) return (8 * S) / PT;
   const int LT = S / PT;
   return 8 * LT + (8 * (S - LT * PT)) / PT;
 }
@@ -299,7 +534,8 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
   int32_t* poff = reinterpret_cast<int32_t*>(smem + align16(sizeof(double) * chain_lds_doubles()));
   unsigned* pval = reinterpret_cast<unsigned*>(poff + kPollMax);
   // misc: [0] dead flag, [1] A entries, [2] K entries, [4] tau-image start in K,
-  //       [8 + u] offset of slot u's partials relative to the tau start, [12 + u] share mask of slot u
+  //       [8 + u] offset of slot u's partials relative to the tau start, [12 + u] / [16 + u] first / last segment
+  //       sharing slot u's column
   int32_t* misc = poff + 2 * kPollMax;
   gu64* tb = (gu64*)a.xbuf + (int64_t)team * a.PT * kXSeg;  // the team's exchange area
   gi32* abort_word = (gi32*)a.abort_word;
@@ -311,27 +547,35 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
     // ---- the team's next window: segment 0 takes it from the launch-wide counter (after every segment has read
     //      the previous hand-out) and hands it to the others; every segment acknowledges
     if (wid == 0) {
-      auto poll1 = [&](int e0, int cnt, unsigned tag) -> bool {  // cnt <= 64 one-granule entries (C list area)
-        const bool act = lane < cnt;
-        gu64* p = tb + (act ? poff[e0 + lane] : 0);
-        bool ok = !act;
-        unsigned spins = 0;
-        while (!__all(ok)) {
-          if (!ok) {
-            const unsigned long long xv = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((unsigned)(xv >> 32) == tag) {
-              ok = true;
-              pval[e0 + lane] = (unsigned)xv;
+      // one-granule entries of the C list area; bounded: the wait is limited in time (an acknowledgement); unbounded:
+      // the next window's hand-out, which comes when segment 0 has finished its window (however long that takes --
+      // segment 0 itself only waits in bounded polls, so it either hands out or aborts, and the abort word ends this)
+      auto poll1 = [&](int e0, int cnt, unsigned tag, bool bounded) -> bool {
+        const long long t0 = wall_clock64();
+        for (int base = 0; base < cnt; base += kWave) {
+          const bool act = base + lane < cnt;
+          gu64* p = tb + (act ? poff[e0 + base + lane] : 0);
+          bool ok = !act;
+          unsigned spins = 0;
+          while (!__all(ok)) {
+            if (!ok) {
+              const unsigned long long xv = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              if ((unsigned)(xv >> 32) == tag) {
+                ok = true;
+                pval[e0 + base + lane] = (unsigned)xv;
+              }
             }
-          }
-          if ((++spins & 1023u) == 0 &&
-              (spins > kSpinMax || __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-            if (lane == 0) {
-              __hip_atomic_store(abort_word + 16 + 8 * (int)blockIdx.x, spins > kSpinMax ? 3 : 2, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-              __hip_atomic_store(abort_word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((++spins & 1023u) == 0) {
+              const bool late = bounded && wall_clock64() - t0 > a.spin_ticks;
+              if (late || __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                if (lane == 0) {
+                  __hip_atomic_store(abort_word + 16 + 8 * (int)blockIdx.x, late ? 3 : 2, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+                  __hip_atomic_store(abort_word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                return false;
+              }
             }
-            return false;
           }
         }
         return true;
@@ -342,9 +586,9 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
       int wi = 0;
       if (seg == 0) {
         if (wseq > 1 && a.PT > 1) {  // acknowledgements of the previous hand-out
-          if (lane < a.PT - 1) poff[kPollC + lane] = (lane + 1) * kXSeg + kOffAck + (par ^ 1);
+          for (int e = lane; e < a.PT - 1; e += kWave) poff[kPollC + e] = (e + 1) * kXSeg + kOffAck + (par ^ 1);
           __builtin_amdgcn_wave_barrier();
-          ok = poll1(kPollC, a.PT - 1, chain_tag(wseq - 1, 0x3FFFF));
+          ok = poll1(kPollC, a.PT - 1, chain_tag(wseq - 1, 0x3FFFF), true);
         }
         if (lane == 0) wi = __hip_atomic_fetch_add(abort_word + 8, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         wi = __builtin_amdgcn_readfirstlane(wi);
@@ -354,7 +598,7 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
       } else {
         if (lane == 0) poff[kPollC] = kOffW + par;
         __builtin_amdgcn_wave_barrier();
-        ok = poll1(kPollC, 1, wtag);
+        ok = poll1(kPollC, 1, wtag, false);
         wi = (int)pval[kPollC];
         if (ok && lane == 0)
           __hip_atomic_store(mine + kOffAck + par, ((unsigned long long)wtag << 32), __ATOMIC_RELAXED,
@@ -372,7 +616,7 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
     const int P = pl[0];
     if (seg >= P) continue;
     const int T = pl[1], k = pl[3];
-    const int t0 = pl[4 + seg], L = pl[5 + seg] - t0;
+    const int t0 = pl[kPlanStart + seg], L = pl[kPlanStart + seg + 1] - t0;
     const bool first = seg == 0, last = seg == P - 1;
     const int kl = k - ch.first;
     const WinOff W = win_offsets(b, ch, k);
@@ -380,7 +624,7 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
     const double* scal = w.scal + (int64_t)kl * kScal;
     int nsl = 0;
 #pragma unroll
-    for (int u = 0; u < kJSeg; ++u) nsl += pl[24 + 4 * seg + u] >= 0;
+    for (int u = 0; u < kJSeg; ++u) nsl += pl[kPlanSlot + 4 * seg + u] >= 0;
     const int wl = (L - 1) >> 6;  // wave holding the segment's last step
     const int32_t* gkp = b.indptr + W.row;
     const int32_t* gkc = b.indices + W.nz;
@@ -412,13 +656,14 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
       misc[4] = ek - kPollK;
       int rel = 0;
       for (int u = 0; u < nsl; ++u) {
-        const int id = pl[24 + 4 * seg + u], msk = pl[88 + 4 * seg + u];
+        const int id = pl[kPlanSlot + 4 * seg + u], rlo = pl[kPlanLo + 4 * seg + u], rhi = pl[kPlanHi + 4 * seg + u];
         misc[8 + u] = rel;
-        misc[12 + u] = msk;
-        for (int r = 0; r < P; ++r) {
-          if (!((msk >> r) & 1) || r == seg) continue;
+        misc[12 + u] = rlo;
+        misc[16 + u] = rhi;
+        for (int r = rlo; r <= rhi; ++r) {
+          if (r == seg) continue;
           int ur = 0;
-          while (ur < kJSeg - 1 && pl[24 + 4 * r + ur] != id) ++ur;
+          while (ur < kJSeg - 1 && pl[kPlanSlot + 4 * r + ur] != id) ++ur;
           poff[e++] = (r * kXSeg + kOffA2 + 2 * ur) | (8 << 16);
           poff[e++] = (r * kXSeg + kOffA2 + 2 * ur + 1) | (8 << 16);
           poff[ek++] = (r * kXSeg + kOffK + 2 + 2 * ur) | (12 << 16);
@@ -433,10 +678,11 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
     const int nA = misc[1], nK = misc[2], kTau = misc[4];
 
     // polls entries [e0, e0 + cnt) for round c (tag, parity); the 32-bit halves land in pval[e0 ..]; false: the
-    // spin expired or another workgroup aborted (the abort word is then set)
+    // wait outlasted spin_ticks or another workgroup aborted (the abort word is then set)
     auto poll = [&](int e0, int cnt, int c) -> bool {
       const unsigned tag = chain_tag(wseq, c);
       const int par = c & 1;
+      const long long tw = wall_clock64();
       for (int base = 0; base < cnt; base += kWave) {
         const int e = base + lane;
         const bool act = e < cnt;
@@ -456,14 +702,15 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
           }
           if (__all(ok)) break;
           ++spins;
-          if ((spins & 1023u) == 0 &&
-              (spins > kSpinMax || __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+          bool late = false;
+          if ((spins & 1023u) == 0 && ((late = wall_clock64() - tw > a.spin_ticks) ||
+                                       __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
             // diagnostics per workgroup (abort_word[16 + 8 blockIdx]): {1 = timed out / 2 = saw the abort, list
             // start, round, entry, expected tag, tag seen}
             const unsigned long long bad = __ballot(!ok);
             const int fl = bad ? __ffsll((long long)bad) - 1 : 0;
             if (lane == fl) {
-              const int d[6] = {spins > kSpinMax ? 1 : 2, e0, c, ent, (int)tag, (int)seen};
+              const int d[6] = {late ? 1 : 2, e0, c, ent, (int)tag, (int)seen};
               for (int u = 0; u < 6; ++u)
                 __hip_atomic_store(abort_word + 16 + 8 * (int)blockIdx.x + u, d[u], __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
@@ -480,11 +727,10 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
     // tau total of slot u from this segment's partial and the polled ones (entries at e0 + rel[u] ..), summed in
     // segment order -- the same additions in every segment holding the slot's rows
     auto tau_total = [&](int u, double own, int e0) -> double {
-      const int msk = misc[12 + u];
+      const int rlo = misc[12 + u], rhi = misc[16 + u];
       int e = e0 + misc[8 + u];
       double s = 0.0;
-      for (int r = 0; r < P; ++r) {
-        if (!((msk >> r) & 1)) continue;
+      for (int r = rlo; r <= rhi; ++r) {
         if (r == seg) {
           s += own;
         } else {
@@ -541,7 +787,7 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
         const int jg = dm[T + t];
 #pragma unroll
         for (int u = 0; u < kJSeg; ++u)
-          if (pl[24 + 4 * seg + u] == jg) jt = u;
+          if (pl[kPlanSlot + 4 * seg + u] == jg) jt = u;
         for (int p = gkp[drow]; p < gkp[drow + 1]; ++p) {
           const int c = gkc[p];
           const double av = gkv[p];
@@ -571,8 +817,8 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
     int jg0 = 0;
     bool town = false;  // this segment owns the slot (the lowest segment holding its rows): KKT / norm terms
     if (tlane) {
-      jg0 = pl[24 + 4 * seg + lane];
-      town = (__ffs(pl[88 + 4 * seg + lane]) - 1) == seg;
+      jg0 = pl[kPlanSlot + 4 * seg + lane];
+      town = pl[kPlanLo + 4 * seg + lane] == seg;
     }
     double sp[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     if (tlane) {
@@ -692,42 +938,78 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
       if (!first && wid == 0 && !poll(kPollU, 6, cB) && lane == 0) misc[0] = 1;
     };
     // check reduction: this segment's NV partials (identical in every lane on entry) -> the sums over all segments
-    // in segment order, in every lane; false: abort
+    // in segment order, in every lane; false: abort.  A leader reduction: every other segment publishes its partials,
+    // segment 0 collects them with all its waves (P - 1 segments x NV values: one or two polls per thread even for
+    // the 137 segments of a 5-minute annual window), sums them in segment order and publishes the totals, which the
+    // others poll -- two hops, but O(P) loads in total instead of O(P^2), and every segment gets the same bits.
     auto round_c = [&](auto& acc) -> bool {
       constexpr int nv = sizeof(acc) / sizeof(double);
       ++cC;
-      if (wid == 0) {
-        const unsigned tag = chain_tag(wseq, cC);
-        double mv = 0.0;
+      const int par = cC & 1;
+      const unsigned tag = chain_tag(wseq, cC);
+      double mv = 0.0;
 #pragma unroll
-        for (int v = 0; v < nv; ++v)
-          if (lane == v) mv = acc[v];
-        if (lane < nv) put_f64(mine + kOffC + 20 * (cC & 1) + 2 * lane, tag, mv);
-        int e = 0;
-        for (int r = 0; r < P; ++r) {
-          if (r == seg) continue;
-          if (lane < 2 * nv) poff[kPollC + e + lane] = (r * kXSeg + kOffC + lane) | (20 << 16);
-          e += 2 * nv;
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (!poll(kPollC, e, cC)) {
-          if (lane == 0) misc[0] = 1;
-        } else {
-          e = 0;
-          for (int r = 0; r < P; ++r) {
-            if (lane < nv) CR[r * kNRed + lane] = r == seg ? mv : pv64(kPollC + e + 2 * lane);
-            if (r != seg) e += 2 * nv;
+      for (int v = 0; v < nv; ++v)
+        if (lane == v) mv = acc[v];
+      if (first) {
+        if (wid == 0 && lane < nv) CR[lane] = mv;
+        const int cnt = (P - 1) * nv;
+        const long long tw = wall_clock64();
+        for (int base = 0; base < cnt; base += B) {
+          const int i = base + tid;
+          const bool act = i < cnt;
+          const int r = act ? 1 + i / nv : 0, v = act ? i % nv : 0;
+          gu64* g = tb + (int64_t)r * kXSeg + kOffC + 20 * par + 2 * v;
+          bool ok = !act;
+          unsigned hi = 0, lo = 0, spins = 0;
+          while (!__all(ok)) {
+            if (!ok) {
+              const unsigned long long a0 = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              const unsigned long long a1 = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              if ((unsigned)(a0 >> 32) == tag && (unsigned)(a1 >> 32) == tag) {
+                ok = true;
+                hi = (unsigned)a0;
+                lo = (unsigned)a1;
+              }
+            }
+            bool late = false;
+            if ((++spins & 1023u) == 0 && ((late = wall_clock64() - tw > a.spin_ticks) ||
+                                           __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+              if (lane == 0) {
+                const int d[6] = {late ? 1 : 2, -1, cC, r, (int)tag, 0};
+                for (int u = 0; u < 6; ++u)
+                  __hip_atomic_store(abort_word + 16 + 8 * (int)blockIdx.x + u, d[u], __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(abort_word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                misc[0] = 1;
+              }
+              break;
+            }
           }
+          if (act && ok) CR[r * kNRed + v] = __hiloint2double((int)hi, (int)lo);
+          if (misc[0]) break;
+        }
+        lds_barrier();
+        if (wid == 0 && lane < nv && !misc[0]) {
+          double s = 0.0;
+          for (int r = 0; r < P; ++r) s += CR[r * kNRed + lane];
+          put_f64(tb + kOffT + 20 * par + 2 * lane, tag, s);
+          CR[lane] = s;
+        }
+      } else if (wid == 0) {
+        if (lane < nv) put_f64(mine + kOffC + 20 * par + 2 * lane, tag, mv);
+        if (lane < 2 * nv) poff[kPollC + lane] = (kOffT + lane) | (20 << 16);
+        __builtin_amdgcn_wave_barrier();
+        if (!poll(kPollC, 2 * nv, cC)) {
+          if (lane == 0) misc[0] = 1;
+        } else if (lane < nv) {
+          CR[lane] = pv64(kPollC + 2 * lane);
         }
       }
       lds_barrier();
       if (misc[0]) return false;
 #pragma unroll
-      for (int v = 0; v < nv; ++v) {
-        double s = 0.0;
-        for (int r = 0; r < P; ++r) s += CR[r * kNRed + v];
-        acc[v] = s;
-      }
+      for (int v = 0; v < nv; ++v) acc[v] = CR[v];
       lds_barrier();  // CR is rewritten by the next reduction
       return true;
     };
@@ -1085,8 +1367,7 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
 hipError_t launch_chain_plan(const Batch& b, const Work& w, const Chunk& ch, const int32_t* list, int nlist,
                              int max_T, int32_t* plan, hipStream_t s) {
   (void)max_T;
-  const size_t lds = 2 * sizeof(int32_t) * (size_t)kPMax * kCB;  // tau ids and run ends
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  const size_t lds = sizeof(int32_t) * ((size_t)kRunsLds + 1);  // run starts
   hipError_t e = hipFuncSetAttribute((const void*)chain_plan_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds);
   if (e != hipSuccess) return e;
@@ -1114,7 +1395,9 @@ size_t chain_xbuf_bytes(int NT, int PT) { return sizeof(unsigned long long) * (s
 int chain_team_count(int S, int PT) { return chain_teams(S, PT); }
 
 hipError_t launch_chain(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, const int32_t* pos, int npos,
-                        const int32_t* plan, int PT, int S, void* xbuf, int32_t* abort_word, hipStream_t s) {
+                        const int32_t* plan, int PT, int S, void* xbuf, int32_t* abort_word, long long spin_ticks,
+                        hipStream_t s) {
+  if (npos > 0x3FFF - 1) return hipErrorInvalidValue;  // window tags keep 14 bits of a team's window count
   const int NT = chain_teams(S, PT);
   const size_t lds = chain_lds_bytes();
   hipError_t e = hipFuncSetAttribute((const void*)pdhg_chain_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1124,13 +1407,69 @@ hipError_t launch_chain(const Batch& b, const Work& w, const Chunk& ch, const Op
   if (e != hipSuccess) return e;
   e = hipMemsetAsync(abort_word, 0, chain_abort_bytes(S), s);
   if (e != hipSuccess) return e;
-  ChainArgs a{pos, npos, plan, static_cast<unsigned long long*>(xbuf), abort_word, PT, NT, S};
+  ChainArgs a{pos, npos, plan, static_cast<unsigned long long*>(xbuf), abort_word, PT, NT, S, spin_ticks};
   Batch bb = b;
   Work ww = w;
   Chunk cc = ch;
   Opts oo = o;
   void* args[] = {&bb, &ww, &cc, &oo, &a};
   return hipLaunchCooperativeKernel((const void*)pdhg_chain_kernel, dim3(8 * S), dim3(kCB), args, (unsigned)lds, s);
+}
+
+namespace {
+__global__ void chain_mark_kernel(int32_t* istats, const int32_t* list, int nlist) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nlist) istats[2 * (int64_t)list[i]] = kChainPending;
+}
+}  // namespace
+
+hipError_t launch_chain_mark(const Batch& b, const int32_t* list, int nlist, hipStream_t s) {
+  if (nlist <= 0) return hipSuccess;
+  hipLaunchKernelGGL(chain_mark_kernel, dim3((nlist + 255) / 256), dim3(256), 0, s, b.istats, list, nlist);
+  return hipGetLastError();
+}
+
+hipError_t launch_setup_long(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int k, const int64_t* d,
+                             hipStream_t s) {
+  LongArgs a;
+  a.b = b;
+  a.w = w;
+  a.k = k;
+  a.kl = k - ch.first;
+  a.n = (int)d[0];
+  a.m = (int)d[1];
+  a.T = (int)d[2] - 1;
+  a.J = a.n - 3 * a.T;
+  a.W.n = a.n;
+  a.W.m = a.m;
+  a.W.meq = (int)d[2];
+  a.W.nnz = (int)d[3];
+  a.W.row = d[4];
+  a.W.nz = d[5];
+  a.W.on = d[6];
+  a.W.om = d[7];
+  a.W.wn = a.W.on - ch.base_n;
+  a.W.wm = a.W.om - ch.base_m;
+  a.W.wz = a.W.nz - ch.base_nz;
+  a.W.wtr = a.W.wn + a.kl;
+  if (a.T < 1 || a.J < 0) return hipErrorInvalidValue;
+  const int nb = (std::max(a.n, a.m) + kLB - 1) / kLB;
+  if (4 * (int64_t)nb > a.m) return hipErrorInvalidValue;  // norm partials in the window's wbuf
+  hipLaunchKernelGGL(long_init, dim3(nb), dim3(kLB), 0, s, a);
+  for (int pass = 0; pass <= o.ruiz_iters; ++pass) {
+    const bool pc = pass == o.ruiz_iters;
+    if (pc) {
+      hipLaunchKernelGGL(long_pass<false>, dim3(nb), dim3(kLB), 0, s, a);
+      if (a.J) hipLaunchKernelGGL(long_tau_pass<false>, dim3(a.J), dim3(kLB), 0, s, a);
+    } else {
+      hipLaunchKernelGGL(long_pass<true>, dim3(nb), dim3(kLB), 0, s, a);
+      if (a.J) hipLaunchKernelGGL(long_tau_pass<true>, dim3(a.J), dim3(kLB), 0, s, a);
+    }
+    hipLaunchKernelGGL(long_apply, dim3(nb), dim3(kLB), 0, s, a);
+  }
+  hipLaunchKernelGGL(long_fill, dim3(nb), dim3(kLB), 0, s, a);
+  hipLaunchKernelGGL(long_norms, dim3(1), dim3(kLB), 0, s, a, nb, o.step_safety);
+  return hipGetLastError();
 }
 
 }  // namespace dvh

@@ -13,11 +13,26 @@ constexpr int kLMax = 64;      // long rows per matrix per window handled on chi
 constexpr int kScal = 16;      // per-window scalars written by the setup kernel
 constexpr int kHalpernTab = 65536;  // table of Halpern weights 1/(k+2)
 constexpr int kSmallMax = 4096;     // windows with n or m above this go to the medium tier or the large-LP path
-// Medium tier (dvh_chain.hip): battery windows of up to kPMax segments of kChainB steps, one workgroup per segment
+// Medium tier (dvh_chain.hip): battery windows of up to kPMax segments of kChainB steps, one workgroup per segment.
+// Windows of up to kChainMedMax segments run as a batch (teams inside one XCD where they fit); longer ones (the
+// 5-minute annual window of BASELINE config 3: T = 105,120, 137 segments) run in a launch of their own, one team
+// spanning the chip.
 constexpr int kChainB = 768;
-constexpr int kPMax = 16;
+constexpr int kPMax = 192;
+constexpr int kChainMedMax = 16;
 constexpr int kChainJMax = 256;     // tau (demand) columns per medium window
-constexpr int kPlanInts = 160;      // plan words per window: P, T, J, k, starts[17], slot ids[16][4], masks[16][4]
+constexpr int kChainJSeg = 4;       // tau columns per segment
+// plan words per window: [0] P, [1] T, [2] J, [3] k, [kPlanStart + s] first step of segment s (P + 1 entries),
+// per (segment s, slot u): the tau column [kPlanSlot + 4 s + u] (-1: none) and the contiguous range of segments that
+// share it [kPlanLo / kPlanHi + 4 s + u] (every segment of the range holds the column in a slot)
+constexpr int kPlanStart = 4;
+constexpr int kPlanSlot = kPlanStart + kPMax + 4;
+constexpr int kPlanLo = kPlanSlot + kChainJSeg * kPMax;
+constexpr int kPlanHi = kPlanLo + kChainJSeg * kPMax;
+constexpr int kPlanInts = kPlanHi + kChainJSeg * kPMax;
+// windows whose n reaches this are set up grid-wide (setup_long, dvh_chain.hip): the one-workgroup setup kernel keeps
+// n + 1 transpose cursors in LDS
+constexpr int kMedSetupNMax = 40000;
 
 // Kernel-side copy of dvh_options (POD, passed by value).
 struct Opts {
@@ -105,15 +120,27 @@ hipError_t launch_setup_medium(const Batch& b, const Work& w, const Chunk& ch, c
 // Medium tier (dvh_chain.hip): plan (structure check + segmentation, plan[kPlanInts] per listed window, plan[0] =
 // P, 0 = not this tier, -1 = reported infeasible by the setup) and the team kernel over the windows at positions
 // pos[] of the plan (PT workgroups per team, NT teams, cooperative launch; xbuf >= chain_xbuf_bytes(NT, PT)).
+// The plan reads only the window's own (unscaled) data: it runs before the setup, reports crossed bounds itself
+// (PRIMAL_INFEASIBLE, plan[0] = -1) and leaves the step -> DCM row / tau maps in the window's vbuf workspace.
 hipError_t launch_chain_plan(const Batch& b, const Work& w, const Chunk& ch, const int32_t* list, int nlist,
                              int max_T, int32_t* plan, hipStream_t s);
+// Grid-wide setup (scaling, scaled data, norms: what setup_kernel writes for the chain kernel) of one planned window
+// whose n is too large for the one-workgroup setup; uses the plan's maps.
+hipError_t launch_setup_long(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int k, const int64_t* d,
+                             hipStream_t s);
+// istats status of the listed windows set to kChainPending before a team launch: after an aborted launch the windows
+// still pending go to the grid-wide path
+constexpr int kChainPending = -7;
+hipError_t launch_chain_mark(const Batch& b, const int32_t* list, int nlist, hipStream_t s);
 hipError_t chain_capacity(int device, int* blocks);
 size_t chain_xbuf_bytes(int NT, int PT);
 size_t chain_abort_bytes(int S);  // abort word, window counter, per-workgroup diagnostics (grid 8 S)
 // S: resident workgroup slots per XCD (grid = 8 S); teams of PT workgroups, chain_team_count(S, PT) of them
 int chain_team_count(int S, int PT);
+// spin_ticks: the longest a segment waits for a partner's exchange (wall-clock ticks) before the launch aborts
 hipError_t launch_chain(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, const int32_t* pos, int npos,
-                        const int32_t* plan, int PT, int S, void* xbuf, int32_t* abort_word, hipStream_t s);
+                        const int32_t* plan, int PT, int S, void* xbuf, int32_t* abort_word, long long spin_ticks,
+                        hipStream_t s);
 // Seeded-sweep warm starts (dvh_sweep.hip): pairs[count][3] = {window, partner window, T (> 0: battery + DCM dual
 // scaling) }; bad counts pairs whose windows differ in shape (skipped).
 hipError_t launch_warm_transfer(const int64_t* desc, const double* c, const double* u, double* x, double* y,

@@ -111,6 +111,26 @@ def config1(with_retail=False):
                              da_price=ri["hourly_da_price"][None, :])
 
 
+def config3(variant="da", n="year"):
+    """BASELINE config 3: the 5-minute (dt = 1/12 h, Model_Parameters_Template_DER.csv:4) year of
+    test/datasets/000-004-timeseries_5min_negprices.csv (2019, 105,120 steps, 2,375 negative DA prices) with the
+    template battery.  variant "da": DA time shift alone, no site load (n = 315,360); "dcm": DA + retailETS + the 12
+    monthly demand charges of data/tariff.csv on the file's site load, less the template's fixed PV (100 kW,
+    curtail 0, grid_charge 0: Model_Parameters_Template_DER.csv PV rows) with data/multi_der_hourly_timeseries.csv's
+    2017 "PV Gen (kW/rated kW)/1" profile held over each hour (n = 315,372, m = 210,241).  n: the window ("year": one
+    annual window; an int: sub-windows of that many steps, e.g. 288 = daily, for the stitched start)."""
+    ri = reference_inputs()
+    T = len(ri["fivemin_da_price"])
+    da = ri["fivemin_da_price"][None, :]
+    if variant == "da":
+        return windows_by_period(2019, 1.0 / 12, np.zeros((1, T)), None, template_battery(), da_price=da, n=n)
+    if variant != "dcm":
+        raise ValueError(f"config3 variant {variant!r}")
+    pv = 100.0 * np.repeat(np.nan_to_num(ri["multi_der_pv_profile"]), 12)[:T]
+    return windows_by_period(2019, 1.0 / 12, ri["fivemin_site_load"][None, :], pv[None, :], template_battery(),
+                             da_price=da, tariff_def=tariff(), n=n, grid_charge=False)
+
+
 def config2_battery():
     return dict(E=4000.0, Pch=1000.0, Pdis=1000.0, rte=0.91, sdr=0.0, soc_target=1.0, ulsoc=1.0, llsoc=0.0,
                 fixedOM=10.0, OMexpenses=0.0, hp=0.0)

@@ -16,7 +16,10 @@ Partitions:
 """
 import numpy as np
 
-RESULT_COLS = 6  # obj, primal_res_rel, dual_res_rel, gap_rel, status, iters
+# obj, primal_res_rel, dual_res_rel, gap_rel, status, iters, scenario, window: every gathered row names its own
+# (scenario, window), so a consumer maps rows without rebuilding the packing order (a seeded sweep packs seed
+# scenarios first)
+RESULT_COLS = 8
 
 
 def shard(total, world, rank):
@@ -69,12 +72,32 @@ def dispatch_runs(desc):
     return runs
 
 
-def result_rows(stats, istats, x=None, desc=None, tmax=None, runs=None):
-    """Per-window result rows (float64): {obj, primal_res_rel, dual_res_rel, gap_rel, status, iters} and, with x /
-    desc, the window's dispatch ch, dis, ene in a fixed stride of 3 * tmax (zero padded).  Works on device or host
-    tensors (strided copies per run of equal windows; no index tensors)."""
+def tag_array(tags):
+    """[count, 2] float64 (scenario, window) of packed windows' tags ((scenario, window) tuples; any other tag:
+    (-1, its position))."""
+    out = np.empty((len(tags), 2), np.float64)
+    for i, t in enumerate(tags):
+        if isinstance(t, tuple) and len(t) == 2 and all(isinstance(v, (int, np.integer)) for v in t):
+            out[i] = t
+        else:
+            out[i] = (-1, i)
+    return out
+
+
+def result_rows(stats, istats, x=None, desc=None, tmax=None, runs=None, tags=None):
+    """Per-window result rows (float64): {obj, primal_res_rel, dual_res_rel, gap_rel, status, iters, scenario,
+    window} and, with x / desc, the window's dispatch ch, dis, ene in a fixed stride of 3 * tmax (zero padded).
+    tags: [count, 2] (scenario, window) per window (``tag_array``; a tensor on the rows' device, or numpy); None:
+    (-1, local position).  Works on device or host tensors (strided copies per run of equal windows; no index
+    tensors)."""
     import torch
-    base = torch.cat([stats.to(torch.float64), istats.to(torch.float64)], dim=1)
+    k = stats.shape[0]
+    if tags is None:
+        tg = torch.stack([torch.full((k,), -1.0, dtype=torch.float64, device=stats.device),
+                          torch.arange(k, dtype=torch.float64, device=stats.device)], dim=1)
+    else:
+        tg = torch.as_tensor(tags, dtype=torch.float64).to(stats.device)
+    base = torch.cat([stats.to(torch.float64), istats.to(torch.float64), tg], dim=1)
     if x is None:
         return base.contiguous()
     runs = runs if runs is not None else dispatch_runs(desc)
@@ -119,9 +142,16 @@ def gather_rows(rows, group=None, counts=None):
 def rows_to_numpy(rows, tmax=None):
     r = rows.detach().cpu().numpy()
     out = dict(obj=r[:, 0], primal_res_rel=r[:, 1], dual_res_rel=r[:, 2], gap_rel=r[:, 3],
-               status=r[:, 4].astype(np.int32), iters=r[:, 5].astype(np.int64))
+               status=r[:, 4].astype(np.int32), iters=r[:, 5].astype(np.int64), scenario=r[:, 6].astype(np.int64),
+               window=r[:, 7].astype(np.int64))
     if r.shape[1] > RESULT_COLS:
         tm = tmax or (r.shape[1] - RESULT_COLS) // 3
         out.update(ch=r[:, RESULT_COLS:RESULT_COLS + tm], dis=r[:, RESULT_COLS + tm:RESULT_COLS + 2 * tm],
                    ene=r[:, RESULT_COLS + 2 * tm:RESULT_COLS + 3 * tm])
     return out
+
+
+def by_tag(rows_np):
+    """rows_to_numpy output re-ordered by (scenario, window) -- the consumer's order, whatever the packing."""
+    order = np.lexsort((rows_np["window"], rows_np["scenario"]))
+    return {k: v[order] for k, v in rows_np.items()}

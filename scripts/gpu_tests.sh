@@ -1,0 +1,9 @@
+#!/bin/bash
+# Full -m gpu suite + smoke on the GPU box (one process, per-test timeout); log under gpurun_out/<tag>/
+set -o pipefail
+TAG=${1:-r03}
+O=gpurun_out/$TAG; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -40 $O/gpu_tests.log; exit 1; }
+tail -3 $O/gpu_tests.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $O/smoke.log; exit 1; }
+tail -2 $O/smoke.log

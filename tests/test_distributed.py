@@ -24,13 +24,20 @@ def _free_port():
     return p
 
 
-def _rows_for(scenario_ids, tmax=744):
-    """Result rows (obj, 0, 0, 0, status, 0, ch, dis, ene padded to tmax) for the windows of the given scenarios,
-    via HiGHS."""
+def _rows_for(scenario_ids, tmax=744, seeded=False):
+    """Result rows (obj, 0, 0, 0, status, 0, scenario, window, ch, dis, ene padded to tmax) for the windows of the
+    given scenarios, via HiGHS.  seeded: packed as bench.py's seeded sweep packs them (seed scenarios first)."""
     from dervet_hip.lp import builder, scenarios
+    from dervet_hip.sweep import SeededSweep
     from oracle import window_lp
-    groups = scenarios.config4(scenario_ids)
-    pb = builder.pack_groups(groups)
+    if seeded:
+        ids = list(scenario_ids)
+        P = scenarios.sweep_parameters(ids)
+        sw = SeededSweep(scenarios.config4, ids, P["E"], stride=2, features=scenarios.sweep_features(P))
+        pb, tags = sw.packed, sw.tags
+    else:
+        groups = scenarios.config4(scenario_ids)
+        pb, tags = builder.pack_groups(groups), [t for g in groups for t in g.tags]
     stats = torch.zeros((pb.count, 4), dtype=torch.float64)
     istats = torch.zeros((pb.count, 2), dtype=torch.int32)
     x = torch.zeros(len(pb.c), dtype=torch.float64)
@@ -41,16 +48,16 @@ def _rows_for(scenario_ids, tmax=744):
         istats[k, 0] = r["status"]
         on = int(pb.desc[k, 6])
         x[on:on + w["n"]] = torch.from_numpy(r["x"])
-    return parallel.result_rows(stats, istats, x, pb.desc, tmax), pb
+    return parallel.result_rows(stats, istats, x, pb.desc, tmax, tags=parallel.tag_array(tags)), pb
 
 
-def _worker(rank, world, port, total, out):
+def _worker(rank, world, port, total, out, seeded=False):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     a, b = parallel.shard(total, world, rank)
-    rows, _ = _rows_for(range(a, b))
+    rows, _ = _rows_for(range(a, b), seeded=seeded)
     counts = [12 * (lambda ab: ab[1] - ab[0])(parallel.shard(total, world, r)) for r in range(world)]
     g = parallel.gather_rows(rows, counts=counts if total % world == 0 else None)
     if rank == 0:
@@ -78,16 +85,37 @@ def test_two_rank_gloo_gather_matches_single_process(tmp_path):
     # single-process order: shard 0 = scenario 0 (then 1 on rank 1 ...): rebuild per shard and concatenate
     parts = [_rows_for(range(*parallel.shard(total, 2, r))) for r in range(2)]
     ref = torch.cat([p[0] for p in parts])
-    assert g.shape == (36, 6 + 3 * 744)
+    C = parallel.RESULT_COLS
+    assert g.shape == (36, C + 3 * 744)
     assert torch.equal(g, ref)
     assert (g[:, 4] == 0).all()
-    # the dispatch columns are the windows' ch / dis / ene
+    # the dispatch columns are the windows' ch / dis / ene; every row names its (scenario, window)
     d = parallel.rows_to_numpy(g)
+    o = parallel.by_tag(d)
+    assert np.array_equal(o["scenario"], np.repeat(np.arange(3), 12)) and np.array_equal(o["window"], np.tile(np.arange(12), 3))
     pb = parts[0][1]
     w = pb.window(5)
     T = w["m_eq"] - 1
-    assert np.array_equal(d["ch"][5, :T], ref.numpy()[5, 6:6 + T])
+    assert np.array_equal(d["ch"][5, :T], ref.numpy()[5, C:C + T])
     assert np.all(d["ene"][5, T:] == 0.0) or T == 744
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_gather_in_seeded_order_maps_back_by_tag(tmp_path):
+    """bench.py's N > 1 path: each rank packs its shard seed-first (SeededSweep); the gathered rows, re-ordered by
+    the (scenario, window) they carry, equal a single-process run's rows in (scenario, window) order -- no
+    SeededSweep rebuild on the consumer's side."""
+    total = 6
+    out = str(tmp_path / "g.pt")
+    mp.spawn(_worker, args=(2, _free_port(), total, out, True), nprocs=2, join=True)
+    g = parallel.by_tag(parallel.rows_to_numpy(torch.load(out, weights_only=True)))
+    ref = parallel.by_tag(parallel.rows_to_numpy(_rows_for(range(total))[0]))
+    assert np.array_equal(g["scenario"], np.repeat(np.arange(total), 12))
+    for k in ("status", "window", "ch", "dis", "ene"):
+        assert np.array_equal(g[k], ref[k]), k
+    # the objective constant c0 is a numpy row sum whose last bit depends on the group's size (a seed group of one
+    # scenario vs all of them): objectives agree to rounding, the dispatch bit for bit
+    assert np.allclose(g["obj"], ref["obj"], rtol=1e-14, atol=0.0)
 
 
 def test_weighted_shard_balances_cost_and_covers_once():

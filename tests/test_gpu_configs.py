@@ -306,19 +306,22 @@ def test_invalid_inputs_raise_with_message(gpu_solver):
 
 
 def _config3_da():
-    ri = scenarios.reference_inputs()
-    T = len(ri["fivemin_da_price"])
-    assert T == 105120
-    return scenarios.windows_by_period(2019, 1.0 / 12, np.zeros((1, T)), None, scenarios.template_battery(),
-                                       da_price=ri["fivemin_da_price"][None, :], n="year")
+    g = scenarios.config3("da")
+    assert g[0].T == 105120
+    return g
 
 
 def test_config3_annual_5min_window_large_path(gpu_solver):
-    """BASELINE config 3: one 105,120-step annual window (n = 315,360) on the grid-wide large-LP path."""
+    """BASELINE config 3: one 105,120-step annual window (n = 315,360) on the grid-wide large-LP path (the band
+    kernels off, so the medium tier is off too; the default route is the long team, tests/test_gpu_config3.py)."""
     lps = _lps(_config3_da())
     assert lps[0].n == 3 * 105120
-    res = gpu_solver.solve(lps)
-    assert gpu_solver.kernel_stats()["large_windows"] == 1
+    gpu_solver.set_kernel_path("ell")
+    try:
+        res = gpu_solver.solve(lps)
+        assert gpu_solver.kernel_stats()["large_windows"] == 1
+    finally:
+        gpu_solver.set_kernel_path("default")
     _check(lps, res, "config3")
 
 
