@@ -3,13 +3,20 @@ product path -- every window position solved on cuda:0 by the band kernel, capac
 profiles -- and against the same sweep solved by HiGHS: per-year avoided charges within 1e-5 relative, capacities
 within 1e-4 relative, and the reference's assertions (040: 2017 saves more than 2022; 041: equal, exactly).
 
-Why 1e-4 on capacities: rainflow counts the SOE path, not the objective; these retail-arbitrage windows have many
-optimal dispatches (equal prices hour after hour), so an interior-point-like PDHG optimum and HiGHS' vertex can count
-slightly different cycles at the same objective.  Measured: 3e-6 after 12 windows, 7e-6 after 24 (r03b)."""
+Every window position is first checked on its own: the GPU's objective against HiGHS on the same window built at the
+GPU's capacity (1e-5, the north_star bar).  The coupled trajectories are then compared.  Rainflow counts the SOE path,
+not the objective, and arbitrage windows have many optimal dispatches (equal prices hour after hour), so a PDHG
+optimum and HiGHS' vertex can count different cycles at the same objective, and the capacities drift apart window by
+window.  Measured: 040 3e-6 after 12 windows, 7e-6 after 24 (r03b) -- 1e-4 on capacities, 1e-5 on the avoided
+charges; 010 (DA arbitrage at 2,000 kW on 10,000 kWh, state of health 73 %) 1.1e-4 after the first window and 1.2e-3
+after the twelfth, 2.3e-4 on the year's DA revenue (the same drift with the CPU restatement of the GPU algorithm,
+oracle/cpu_pdhg.cpp, in this container) -- 2e-3 / 5e-4 there.  The reference asserts only that 010 runs
+(test_3battery.py:74-75) and that it ends below its rating without a replacement (replaceable 0)."""
 import numpy as np
 import pytest
 
 import degradation_ref as dr
+from dervet_hip.lp import builder
 
 pytestmark = pytest.mark.gpu
 
@@ -22,14 +29,20 @@ def test_reference_degradation_case_on_the_gpu(gpu_solver, name):
     assert all((p["status"] == 0).all() for p in res)
     assert gpu_solver.kernel_stats()["band_windows"] == 1
     hs, hb = dr.sweep(case)
+    # each position on its own: HiGHS on the window built at the GPU's capacity
+    lps = [builder.group_window_lps(hb(p["k"], p["capacity_before"])[0])[0] for p in res]
+    for p, h in zip(res, dr.HighsSolver().solve(lps)):
+        assert h.status == 0
+        assert float(p["obj"][0]) == pytest.approx(h.obj, rel=1e-5), (p["k"], float(p["obj"][0]), h.obj)
     av = dr.avoided_charges(case, sw, hb, res)     # terms evaluated on the host-built (bit-identical) windows
     href = hs.run(dr.HighsSolver(), device=None)
     hav = dr.avoided_charges(case, hs, hb, href)
+    cap_tol, av_tol = (2e-3, 5e-4) if name == "010" else (1e-4, 1e-5)
     for y in av:
-        assert av[y] == pytest.approx(hav[y], rel=1e-5), (y, av[y], hav[y])
+        assert av[y] == pytest.approx(hav[y], rel=av_tol), (y, av[y], hav[y])
     caps = np.array([p["capacity_before"][0] for p in res])
     hcaps = np.array([p["capacity_before"][0] for p in href])
-    assert np.allclose(caps, hcaps, rtol=1e-4, atol=0.0)
+    assert np.allclose(caps, hcaps, rtol=cap_tol, atol=0.0)
     if name == "040":
         assert av[2017] > av[2022]                   # test_2finances.py:67-69
     if name == "041":
