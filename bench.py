@@ -155,6 +155,9 @@ def main():
     ap.add_argument("--kkt-predict", type=int, default=4,
                     help="dvh_options.kkt_predict for cold solves (--schedule cold and the cold reference; the seeded "
                          "schedule's phases use sweep.SEED_OPTIONS / WARM_OPTIONS); 0 = every due KKT check runs")
+    ap.add_argument("--series", choices=("device", "host"), default="device",
+                    help="with --build device: the scenarios' series generated on the GPU (lp/gpu_series.py) or by "
+                         "numpy on the host (bit-identical)")
     ap.add_argument("--build", choices=("device", "host"), default="device",
                     help="window expansion: on the GPU from compact inputs (lp/gpu_builder.py) or by the host "
                          "builder + upload (bit-identical batches; untimed by the contract, reported as build)")
@@ -185,9 +188,16 @@ def main():
     solver = BatchSolver(local)
     t0 = time.time()
     sweep = None
-    make = functools.partial(scenarios.config4, spec=args.build == "device")
+    series = None
+    if args.build == "device" and args.series == "device":
+        # the scenarios' draws and every window's series generated in HBM, bit-identical to the host generator
+        from dervet_hip.lp import gpu_series
+        series = gpu_series.DeviceSeries(scen, solver, f"cuda:{local}")
+        make = series.config4
+    else:
+        make = functools.partial(scenarios.config4, spec=args.build == "device")
     if args.schedule == "seeded":
-        P = scenarios.sweep_parameters(scen)
+        P = series.parameters() if series is not None else scenarios.sweep_parameters(scen)
         sweep = SeededSweep(make, scen, P["E"], stride=args.seed_stride, features=scenarios.sweep_features(P))
         t1 = time.time()
         dev = sweep.to_device(solver, f"cuda:{local}")
@@ -211,8 +221,11 @@ def main():
         del hb
     torch.cuda.synchronize()
     build_s = time.time() - t0
-    build = {"kind": args.build, "s": round(build_s, 2), "host_inputs_s": round(t1 - t0, 2),
-             "expand_upload_s": round(time.time() - t1, 3)}
+    build = {"kind": args.build, "series": args.series if args.build == "device" else "host", "s": round(build_s, 2),
+             "inputs_s": round(t1 - t0, 3), "expand_s": round(time.time() - t1, 3),
+             "note": "inputs: per-scenario draws + series + the windows' builder inputs (device: dvh_series_draws / "
+                     "dvh_series_windows, host: numpy / scipy); expand: the windows' LPs in HBM (dvh_build_battery_group)"}
+    del series
     pb = dev  # windows are read back from the device for the CPU legs
     count = len(desc)
     opts = {k: v for k, v in (("check_every", args.check_every), ("kkt_every", args.kkt_every)) if v > 0}
@@ -398,6 +411,9 @@ def main():
         "gather": gather or None,
         "parity": parity,
         "build": build,
+        # inputs generated + windows expanded + one timed step, all on this GPU: what a sweep costs end to end
+        "end_to_end": {"windows_per_s": round(count / (build_s + el / args.steps), 1),
+                       "s": round(build_s + el / args.steps, 3)},
     }
     if rank == 0:
         print(json.dumps(line), flush=True)

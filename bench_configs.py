@@ -124,6 +124,9 @@ def main():
     ap.add_argument("--c4-scenarios", type=int, default=2000)
     ap.add_argument("--c5-scenarios", type=int, default=1000)
     ap.add_argument("--c5-years", type=int, default=20)
+    ap.add_argument("--c5-host-build", action="store_true",
+                    help="config 5: numpy series + host builder (default: lp/gpu_series.py + the device builder, "
+                         "bit-identical)")
     ap.add_argument("--c5-batch-years", type=int, default=10,
                     help="opt years per solver batch (1 = one batch per year)")
     ap.add_argument("--med-scenarios", type=int, default=1000)
@@ -313,23 +316,37 @@ def config5_horizon(s, ids, years, args):
     ms = scenarios.config5_min_soe(ids, s)
     minsoe_s = time.perf_counter() - t
     minsoe_kernel_ms = reliability.last_kernel_ms(s)
-    P5 = scenarios.sweep_parameters(ids)
+    series = floor = None
+    tb = time.perf_counter()
+    if not args.c5_host_build:
+        # the scenarios' series and every window generated / expanded on the GPU (bit-identical to the host build)
+        from dervet_hip.lp import gpu_series
+        series = gpu_series.DeviceSeries(ids, s)
+        floor = series.min_soe_floor(ms)
+        P5 = series.parameters()
+    else:
+        P5 = scenarios.sweep_parameters(ids)
+    series_s = time.perf_counter() - tb
     # windows whose requirement exceeds E somewhere (infeasible as stated -> clipped at E for the timed horizon)
     over = ms > P5["E"][:, None]
     month = np.concatenate([np.full(d, k) for k, d in enumerate([31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31])])
     month = np.repeat(month, 24)[:ms.shape[1]]
     clipped = int(sum(over[:, month == k].any(axis=1).sum() for k in range(12)))
     feats = scenarios.sweep_features(P5)
-    solve_s = build_s = 0.0
+    solve_s, build_s = 0.0, series_s
     iters, opt, windows, par = [], 0, 0, None
     yb = max(1, min(int(args.c5_batch_years), years))
     for y in range(0, years, yb):
         t = time.perf_counter()
-        mk = lambda v, y=y: scenarios.config5(v, years=min(yb, years - y), start_year=2017 + y,  # noqa: E731
-                                              min_soe=ms[np.searchsorted(ids, np.asarray(list(v)))],
-                                              cap_min_soe=True)
+        if series is not None:
+            mk = lambda v, y=y: series.config5(v, years=min(yb, years - y), start_year=2017 + y,  # noqa: E731
+                                               emin=floor)
+        else:
+            mk = lambda v, y=y: scenarios.config5(v, years=min(yb, years - y), start_year=2017 + y,  # noqa: E731
+                                                  min_soe=ms[np.searchsorted(ids, np.asarray(list(v)))],
+                                                  cap_min_soe=True)
         sw = SeededSweep(mk, ids, P5["E"], stride=32, features=feats)
-        dev = sw.packed.to_torch("cuda:0").alloc_outputs()
+        dev = sw.to_device(s, "cuda:0")
         build_s += time.perf_counter() - t
         if y == 0:
             sw.solve(s, dev)  # warm-up (workspace sizing)
@@ -341,10 +358,10 @@ def config5_horizon(s, ids, years, args):
         ist = dev.istats.cpu().numpy()
         iters.append(ist[:, 1])
         opt += int((ist[:, 0] == 0).sum())
-        windows += sw.packed.count
+        windows += dev.count
         if y == 0 and args.sample > 0:
-            par = _parity(sw.packed, dev.stats.cpu().numpy(), dev.x.cpu().numpy(), args.sample, args.procs)
-        del dev
+            par = _parity(dev, dev.stats.cpu().numpy(), dev.x.cpu().numpy(), args.sample, args.procs)
+        del dev, sw
     it = np.concatenate(iters)
     line = {"config": "config5", "workload": f"{len(ids)} scenarios x {years} opt years x 12 monthly windows: battery + "
                                              "PV + LP-relaxed ICE + DCM + retail + GPU reliability min-SOE requirement",
@@ -355,7 +372,10 @@ def config5_horizon(s, ids, years, args):
                         "note": "requirement clipped at E: unclipped, those windows have crossed ene bounds and "
                                 "the solver reports them PRIMAL_INFEASIBLE at setup (tests/test_gpu_outage.py)"},
             "solve_ms_total": round(solve_s * 1e3, 1), "windows_per_s": round(windows / solve_s, 1),
-            "scenario_years_per_s": round(len(ids) * years / solve_s, 1), "host_build_s": round(build_s, 1),
+            "scenario_years_per_s": round(len(ids) * years / solve_s, 1),
+            "build": {"kind": "host" if args.c5_host_build else "device series + device builder",
+                      "s": round(build_s, 2), "series_s": round(series_s, 3)},
+            "end_to_end_windows_per_s": round(windows / (minsoe_s + build_s + solve_s), 1),
             "iters_mean": round(float(it.mean()), 1), "iters_max": int(it.max()), "optimal": opt,
             "kernel_path_last_year": paths, "parity_year0": par}
     print(json.dumps(line), flush=True)

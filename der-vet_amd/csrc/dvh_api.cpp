@@ -66,6 +66,7 @@ struct dvh_handle {
   int n_chain_aborts = 0;                         // team launches that aborted (their unfinished windows ran grid-wide)
   DevBuf o_data, o_cases, o_len, o_hist, o_soe;  // reliability sweep
   DevBuf s_pairs, s_bad;                          // seeded-sweep warm transfer (dvh_sweep.hip)
+  DevBuf g_seeds, g_word;                         // scenario series generator (dvh_series.hip)
   double outage_ms = 0.0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   // per-chunk timing events: a pool created on first use and reused by every solve (destroyed with the handle), so
@@ -271,6 +272,54 @@ int dvh_warm_transfer(dvh_handle* h, const dvh_packed* b, const int32_t* pairs, 
   DVH_HIP(h, hipMemcpyAsync(&bad, h->s_bad.p, sizeof(int32_t), hipMemcpyDeviceToHost, s));
   DVH_HIP(h, hipStreamSynchronize(s));
   if (bad) return fail(h, DVH_ERR_ARG, "warm transfer: " + std::to_string(bad) + " pair(s) of different LP shape");
+  return DVH_OK;
+}
+
+int dvh_series_draws(dvh_handle* h, const dvh_sweep_draws* d) {
+  if (!h) return DVH_ERR_ARG;
+  if (!d || d->count < 0 || d->steps < 1 || d->n_uniform < 0)
+    return fail(h, DVH_ERR_ARG, "series draws: bad sizes");
+  if (d->count == 0) return DVH_OK;
+  if (!d->seeds || !d->z0 || !d->ar || (d->n_uniform > 0 && !d->uniform))
+    return fail(h, DVH_ERR_ARG, "series draws: null array");
+  DVH_HIP(h, hipSetDevice(h->device));
+  hipStream_t s = h->stream;
+  DVH_HIP(h, h->g_seeds.ensure(sizeof(uint64_t) * (size_t)d->count));
+  DVH_HIP(h, h->g_word.ensure(sizeof(int32_t)));
+  DVH_HIP(h, hipMemcpyAsync(h->g_seeds.p, d->seeds, sizeof(uint64_t) * (size_t)d->count, hipMemcpyHostToDevice, s));
+  DVH_HIP(h, hipMemsetAsync(h->g_word.p, 0, sizeof(int32_t), s));
+  hipError_t e = dvh::launch_series_draws(h->g_seeds.as<uint64_t>(), d->count, d->steps, d->n_uniform, d->a1,
+                                          d->innov, d->z0, d->ar, d->uniform, h->g_word.as<int32_t>(), s);
+  if (e != hipSuccess) return hip_fail(h, e, "launch_series_draws");
+  int32_t amb = 0;
+  DVH_HIP(h, hipMemcpyAsync(&amb, h->g_word.p, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  DVH_HIP(h, hipStreamSynchronize(s));
+  if (amb)
+    return fail(h, DVH_ERR_UNSUPPORTED, "series draws: " + std::to_string(amb) +
+                                            " scenario(s) met a ziggurat wedge test within 2^-40 of exp(); their "
+                                            "draws may differ from numpy's");
+  return DVH_OK;
+}
+
+int dvh_series_windows(dvh_handle* h, const dvh_window_series* w) {
+  if (!h) return DVH_ERR_ARG;
+  if (!w || w->G < 0 || w->T < 1 || w->t0 < 0 || w->rep < 1 || w->J < 0 || w->count < 1 || w->hours < 1 ||
+      !(w->dt > 0.0) || (int64_t)(w->t0 + w->T - 1) / w->rep >= w->hours)
+    return fail(h, DVH_ERR_ARG, "series windows: bad sizes (window past the series?)");
+  if (w->G == 0) return DVH_OK;
+  if (!w->rows || !w->ar || !w->site_load || !w->pv_profile || !w->price || !w->load_scale || !w->price_scale ||
+      !w->pv_rated || !w->hp || !w->c0_add || !w->base || !w->retail || !w->c0)
+    return fail(h, DVH_ERR_ARG, "series windows: null array");
+  DVH_HIP(h, hipSetDevice(h->device));
+  hipStream_t s = h->stream;
+  DVH_HIP(h, h->g_word.ensure(sizeof(int32_t)));
+  DVH_HIP(h, hipMemsetAsync(h->g_word.p, 0, sizeof(int32_t), s));
+  hipError_t e = dvh::launch_series_windows(*w, h->g_word.as<int32_t>(), s);
+  if (e != hipSuccess) return hip_fail(h, e, "launch_series_windows");
+  int32_t bad = 0;
+  DVH_HIP(h, hipMemcpyAsync(&bad, h->g_word.p, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  DVH_HIP(h, hipStreamSynchronize(s));
+  if (bad) return fail(h, DVH_ERR_ARG, "series windows: " + std::to_string(bad) + " row(s) outside 0 .. count - 1");
   return DVH_OK;
 }
 
@@ -504,7 +553,7 @@ extern "C" int dvh_build_battery_group(dvh_handle* h, const dvh_battery_group* g
   if ((g->mI > 0 && (!g->dcm_t || !g->dcm_j)) || !g->base || (g->J > 0 && !g->demand) || !g->E || !g->pch ||
       !g->pdis || !g->rte || !g->sdr || !g->soc_target || !g->ulsoc || !g->llsoc || !g->om || !g->c0 ||
       (g->has_retail && !g->retail) || (g->has_da && !g->da) || (g->has_emin && !g->emin) ||
-      (g->has_emax && !g->emax))
+      (g->has_emax && !g->emax) || (g->has_ice && (!g->ice_cap || !g->ice_pmin || !g->ice_cost)))
     return fail(h, DVH_ERR_ARG, "battery group: null input array");
   if (!b->desc || !b->indptr || !b->indices || !b->data || !b->c || !b->c0 || !b->q || !b->l || !b->u)
     return fail(h, DVH_ERR_ARG, "null device array in packed batch");
@@ -528,7 +577,9 @@ extern "C" int dvh_build_battery_group(dvh_handle* h, const dvh_battery_group* g
       return fail(h, DVH_ERR_ARG, "battery group: demand-charge row " + std::to_string(i) + " (step " +
                                       std::to_string(dt_[i]) + ", column " + std::to_string(dj_[i]) +
                                       ") outside T = " + std::to_string(g->T) + ", J = " + std::to_string(g->J));
-  const int64_t T = g->T, n = 3 * T + g->J, m = T + 1 + g->mI, nnz = 4 * T + 3 * (int64_t)g->mI;
+  const bool ice = g->has_ice != 0;
+  const int64_t T = g->T, n = (ice ? 5 : 3) * T + g->J, m = T + 1 + g->mI + (ice ? 2 * T : 0),
+                nnz = 4 * T + (ice ? 4 : 3) * (int64_t)g->mI + (ice ? 4 * T : 0);
   for (int w = 0; w < g->G; ++w) {
     const int64_t* d = &desc[8 * (size_t)w];
     if (d[0] != n || d[1] != m || d[2] != T + 1 || d[3] != nnz || d[4] < 0 || d[5] < 0 || d[6] < 0 || d[7] < 0 ||

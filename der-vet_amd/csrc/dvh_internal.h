@@ -5,6 +5,8 @@
 
 #include <string>
 
+struct dvh_window_series;  // include/dervet_hip.h
+
 namespace dvh {
 
 constexpr int kWave = 64;
@@ -145,6 +147,12 @@ hipError_t launch_chain(const Batch& b, const Work& w, const Chunk& ch, const Op
 // scaling) }; bad counts pairs whose windows differ in shape (skipped).
 hipError_t launch_warm_transfer(const int64_t* desc, const double* c, const double* u, double* x, double* y,
                                 const int32_t* pairs, int count, int32_t* bad, hipStream_t s);
+// Synthetic scenario series (dvh_series.hip): numpy-identical draws, one thread per scenario (ambiguous counts
+// scenarios with a wedge test too close to call), and the device builder's inputs of G windows (bad counts rows out of
+// range).
+hipError_t launch_series_draws(const uint64_t* seeds, int count, int steps, int n_unif, double a1, double innov,
+                               double* z0, double* ar, double* unif, int32_t* ambiguous, hipStream_t s);
+hipError_t launch_series_windows(const ::dvh_window_series& w, int32_t* bad, hipStream_t s);
 // Power iteration for ||Kt||_2 of the listed windows (generic path; the ELL kernel does its own on chip).
 hipError_t launch_power(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, const int32_t* list, int nlist,
                         hipStream_t s);

@@ -70,8 +70,25 @@ class BatteryGroup(ctypes.Structure):
                 ("has_emin", ctypes.c_int32), ("has_emax", ctypes.c_int32)] + \
                [(f, ctypes.c_void_p) for f in ("dcm_t", "dcm_j", "base", "retail", "da", "demand", "emin", "emax", "E",
                                                "pch", "pdis", "rte", "sdr", "soc_target", "ulsoc", "llsoc", "om",
-                                               "c0")]
+                                               "c0")] + \
+               [("has_ice", ctypes.c_int32), ("pad_ice", ctypes.c_int32)] + \
+               [(f, ctypes.c_void_p) for f in ("ice_cap", "ice_pmin", "ice_cost")]
 
+
+
+class SweepDraws(ctypes.Structure):
+    """dvh_sweep_draws (scenario series generator; seeds host, outputs device)."""
+    _fields_ = [("count", ctypes.c_int32), ("steps", ctypes.c_int32), ("n_uniform", ctypes.c_int32),
+                ("seeds", ctypes.c_void_p), ("a1", ctypes.c_double), ("innov", ctypes.c_double),
+                ("z0", ctypes.c_void_p), ("ar", ctypes.c_void_p), ("uniform", ctypes.c_void_p)]
+
+
+class WindowSeries(ctypes.Structure):
+    """dvh_window_series (the device builder's inputs cut from the scenarios' series; device pointers)."""
+    _fields_ = [(f, ctypes.c_int32) for f in ("G", "T", "t0", "rep", "J", "count", "hours")] + \
+               [("dt", ctypes.c_double)] + \
+               [(f, ctypes.c_void_p) for f in ("rows", "ar", "site_load", "pv_profile", "price", "load_scale",
+                                               "price_scale", "pv_rated", "hp", "c0_add", "base", "retail", "c0")]
 
 SYMBOLS = {
     "dvh_version": (ctypes.c_char_p, []),
@@ -89,6 +106,8 @@ SYMBOLS = {
     "dvh_build_battery_group": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(BatteryGroup), ctypes.POINTER(Packed),
                                                ctypes.c_int32]),
     "dvh_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
+    "dvh_series_draws": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(SweepDraws)]),
+    "dvh_series_windows": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(WindowSeries)]),
     "dvh_last_timing": (ctypes.c_int, [ctypes.c_void_p, c_double_p]),
     "dvh_last_stats": (ctypes.c_int, [ctypes.c_void_p, c_int32_p]),
     "dvh_last_path_counts": (ctypes.c_int, [ctypes.c_void_p, c_int32_p]),

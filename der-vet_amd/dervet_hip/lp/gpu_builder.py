@@ -6,8 +6,8 @@ T = 744 month) instead of the expanded LP (~170 KB: CSR, bounds, objective), and
 instead of numpy's.  Values are bit-identical to the host builder (tests/test_gpu_builder.py), which stays the
 parity reference (tests/test_builder.py pins it to the oracle).
 
-``battery_group_spec`` takes battery_group's arguments (the supported subset: no curtailable PV, ICE, POI rows or
-grid_charge = 0 -- those windows keep the host builder) and returns a ``BatteryGroupSpec``; ``pack_specs_device``
+``battery_group_spec`` takes battery_group's arguments (the supported subset: no curtailable PV, POI rows or
+grid_charge = 0 -- those windows keep the host builder; the LP-relaxed ICE of config 5 is built on the device too) and returns a ``BatteryGroupSpec``; ``pack_specs_device``
 lays a list of specs out as one device PackedBatch (group order, then window order, like ``pack_groups``) and
 builds every window in place.
 """
@@ -37,6 +37,7 @@ class BatteryGroupSpec:
     scal: dict               # name -> [G]
     c0: np.ndarray           # [G]
     tags: list = field(default_factory=list)
+    ice: dict = None         # LP-relaxed ICE: cap, pmin, cost [G] (battery_group `ice`)
 
     @property
     def G(self):
@@ -44,24 +45,23 @@ class BatteryGroupSpec:
 
     @property
     def n(self):
-        return 3 * self.T + self.J
+        return (5 if self.ice else 3) * self.T + self.J
 
     @property
     def m(self):
-        return self.T + 1 + len(self.dcm_t)
+        return self.T + 1 + len(self.dcm_t) + (2 * self.T if self.ice else 0)
 
     @property
     def nnz(self):
-        return 4 * self.T + 3 * len(self.dcm_t)
+        return 4 * self.T + (4 if self.ice else 3) * len(self.dcm_t) + (4 * self.T if self.ice else 0)
 
 
 def battery_group_spec(T, dt, base_load, bat, retail_price=None, da_price=None, demand_masks=None, demand_prices=None,
                        ene_min=None, ene_max=None, name="es", tags=None, pv_curtail_max=None, ice=None, poi=None,
                        grid_charge=True, pv_gen=None):
     """The inputs of ``builder.battery_group(...)`` for the device builder (same arguments and meaning)."""
-    if pv_curtail_max is not None or ice is not None or poi is not None or not grid_charge:
-        raise NotImplementedError("device builder: curtailable PV, ICE, POI rows and grid_charge = 0 use the host "
-                                  "builder")
+    if pv_curtail_max is not None or poi is not None or not grid_charge:
+        raise NotImplementedError("device builder: curtailable PV, POI rows and grid_charge = 0 use the host builder")
     base_load = np.atleast_2d(np.asarray(base_load, np.float64))
     G = base_load.shape[0]
     masks = np.zeros((0, T), bool) if demand_masks is None else np.asarray(demand_masks, bool)
@@ -91,15 +91,23 @@ def battery_group_spec(T, dt, base_load, bat, retail_price=None, da_price=None, 
     da = None if da is None else np.ascontiguousarray(da)
     c0 += _col(bat.get("fixedOM", 0.0), G) * pdis
     c0 += np.zeros(G)
+    if ice is not None:  # the ICE fuel term's constant
+        c0 += np.zeros(G)
     scal = dict(E=E, pch=pch, pdis=pdis, rte=_col(bat["rte"], G), sdr=_col(bat.get("sdr", 0.0), G) / 100.0,
                 soc_target=_col(bat.get("soc_target", 1.0), G), ulsoc=_col(bat.get("ulsoc", 1.0), G),
                 llsoc=_col(bat.get("llsoc", 0.0), G), om=_col(bat.get("OMexpenses", 0.0), G))
     demand = np.zeros((G, 0)) if not J else np.ascontiguousarray(np.asarray(demand_prices, np.float64).reshape(G, J))
+    ice_d = None
+    if ice is not None:  # battery_group's ICE rows / fuel term, the same products
+        ice_d = dict(cap=_col(ice["rated_power"], G) * _col(ice.get("n", 1.0), G),
+                     pmin=_col(ice.get("min_power", 0.0), G) * _col(ice.get("n", 1.0), G),
+                     cost=(_col(ice["efficiency"], G) * _col(ice["fuel_cost"], G)
+                           + _col(ice.get("variable_om_cost", 0.0), G)) * dt)
     return BatteryGroupSpec(T=T, J=J, dt=float(dt), dcm_t=dcm_t, dcm_j=dcm_j, base=np.ascontiguousarray(base),
                             retail=retail, da=da, demand=demand,
                             emin=None if ene_min is None else np.ascontiguousarray(_col(ene_min, G, T)),
                             emax=None if ene_max is None else np.ascontiguousarray(_col(ene_max, G, T)),
-                            scal=scal, c0=c0, tags=list(tags) if tags is not None else [None] * G)
+                            scal=scal, c0=c0, tags=list(tags) if tags is not None else [None] * G, ice=ice_d)
 
 
 def desc_of(specs):
@@ -140,6 +148,10 @@ def pack_specs_device(specs, solver, device="cuda:0"):
     def up(a, t=torch.float64):
         if a is None:
             return None
+        if isinstance(a, torch.Tensor):  # already on the device (lp/gpu_series.py)
+            if a.device != dev or a.dtype != t or not a.is_contiguous():
+                raise ValueError(f"device input must be a contiguous {t} tensor on {dev}")
+            return a.data_ptr()
         x = torch.as_tensor(np.ascontiguousarray(a)).to(device=dev, dtype=t)
         keep.append(x)
         return x.data_ptr()
@@ -156,6 +168,9 @@ def pack_specs_device(specs, solver, device="cuda:0"):
         for k, v in s.scal.items():
             setattr(g, k, up(v))
         g.c0 = up(s.c0)
+        if s.ice:
+            g.has_ice = 1
+            g.ice_cap, g.ice_pmin, g.ice_cost = up(s.ice["cap"]), up(s.ice["pmin"]), up(s.ice["cost"])
         torch.cuda.synchronize(dev)
         rc = solver._lib.dvh_build_battery_group(solver._h, ctypes.byref(g), ctypes.byref(p), first)
         if rc != 0:

@@ -257,7 +257,7 @@ def config5_min_soe(scenarios, solver, target_hours=4, count_ice=False):
     return np.stack(min_soe(config5_outage_cases(scenarios, count_ice), target_hours, solver))
 
 
-def config5(scenarios, years=20, start_year=2017, min_soe=None, cap_min_soe=False):
+def config5(scenarios, years=20, start_year=2017, min_soe=None, cap_min_soe=False, spec=False):
     """Battery + fixed PV + LP-relaxed ICE + 4-h reliability min-SOE, retail + DCM, monthly windows over
     `years` opt years (the 2017 profile re-used each year).  Perturbations as config 4 (same seeds) plus
     ICE fuel cost; ICE parameters from the Usecase3 ES+PV+DG model parameters (750 kW x 7 units,
@@ -267,7 +267,8 @@ def config5(scenarios, years=20, start_year=2017, min_soe=None, cap_min_soe=Fals
     battery's energy rating (the restated simulate_outage lets SOE climb past E while it "discharges" a negative
     net load, Reliability.py:543-556) give crossed ene bounds: those windows are infeasible as the reference
     states them and the solver reports PRIMAL_INFEASIBLE without iterating; cap_min_soe=True clips the requirement
-    at ulsoc * E instead (the bench's timed horizon, which reports how many windows the clip touched)."""
+    at ulsoc * E instead (the bench's timed horizon, which reports how many windows the clip touched).
+    spec: the device builder's inputs (gpu_builder.BatteryGroupSpec, ICE included) instead of host-built groups."""
     from scipy.signal import lfilter
     ri = reference_inputs()
     scen = list(scenarios)
@@ -294,7 +295,7 @@ def config5(scenarios, years=20, start_year=2017, min_soe=None, cap_min_soe=Fals
     for y in range(years):
         gy = windows_by_period(start_year + y, 1.0, load, gen, bat, tariff_def=tariff(),
                                demand_price_override=P["demand"], price_scale=P["price_scale"],
-                               ene_min=emin, ice=ice, tags_prefix=scen)
+                               ene_min=emin, ice=ice, tags_prefix=scen, spec=spec)
         if y > 0:  # window ids unique over the horizon (12 y + month): several opt years can share one sweep batch
             for g in gy:
                 g.tags = [(t[0], 12 * y + t[1]) for t in g.tags]

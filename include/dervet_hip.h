@@ -160,7 +160,7 @@ int dvh_solve_packed_device(dvh_handle* h, const dvh_packed* batch, void* stream
 /* ---- Device-side window builder (the LP that storagevet's
  * set_up_optimization builds for a battery + demand-charge + retail / DA window, MicrogridScenario.py:322-346).
  * Expands G windows' inputs (device pointers) into the packed batch's LP arrays, windows first .. first + G - 1,
- * whose descriptors the caller has set (n = 3T + J, m = T + 1 + mI, nnz = 4T + 3 mI, any offsets).  The values are
+ * whose descriptors the caller has set (n = 3T + J, m = T + 1 + mI, nnz = 4T + 3 mI, any offsets; ICE below).  The values are
  * exactly those of dervet_hip/lp/builder.py battery_group (same formulas, same summation order; bit-identical,
  * tests/test_gpu_builder.py), so a sweep ships its compact inputs to HBM instead of the expanded LPs.
  * Asynchronous on the handle's stream. */
@@ -187,9 +187,64 @@ typedef struct dvh_battery_group {
   const double* llsoc;             /* [G] fraction                                                               */
   const double* om;                /* [G] variable O&M, $/MWh                                                    */
   const double* c0;                /* [G] objective constant (the terms' constants, summed on the host)          */
+  /* LP-relaxed ICE (BASELINE config 5; builder.battery_group `ice`): columns elec_t, on_t after tau (n = 5T + J),
+   * elec_t in every demand-charge row (4 entries), two >= rows per step after them (m = 3T + 1 + mI,
+   * nnz = 8T + 4 mI): cap on_t - elec_t >= 0, elec_t - pmin on_t >= 0; elec in [0, inf), on in [0, 1].  */
+  int32_t has_ice, pad_ice;
+  const double* ice_cap;           /* [G] rated power x units, kW                                                */
+  const double* ice_pmin;          /* [G] minimum stable power x units, kW                                       */
+  const double* ice_cost;          /* [G] (efficiency x fuel cost + variable O&M) x dt, $/kW per step             */
 } dvh_battery_group;
 int dvh_build_battery_group(dvh_handle* h, const dvh_battery_group* group, const dvh_packed* batch, int32_t first);
 int dvh_synchronize(dvh_handle* h);
+
+/* ---- Synthetic scenario series on the device (BASELINE.json configs 4 / 5; no reference
+ * counterpart: the reference reads one time-series CSV per case, dervet/DERVET.py:75-83, and a sweep's perturbed
+ * series are this framework's workload generator, dervet_hip/lp/scenarios.py).  Draws, per scenario, exactly what
+ * numpy's np.random.Generator(np.random.PCG64(seed)) draws on the host: one standard normal (the lognormal load
+ * scale), `steps` standard normals filtered as scipy.signal.lfilter([1], [1, a1]) with the innovations after the
+ * first scaled by `innov`, then `n_uniform` next_double words (uniform(low, high) = low + (high - low) * u).
+ * seeds: host [count] SeedSequence entropy; z0 [count], ar [count * steps], uniform [count * n_uniform]: device.
+ * Bit-identical to the host generator (tests/test_gpu_series.py).  DVH_ERR_UNSUPPORTED if a wedge test of the
+ * ziggurat fell within 2^-40 of the device exp (its outcome could differ from the host libm's; not observed).
+ * Returns after the kernel completed. */
+typedef struct dvh_sweep_draws {
+  int32_t count, steps, n_uniform;
+  const uint64_t* seeds;
+  double a1;                       /* lfilter denominator coefficient a[1] (-phi)                              */
+  double innov;                    /* innovation scale of steps >= 1 (sqrt(1 - phi^2))                         */
+  double* z0;
+  double* ar;
+  double* uniform;
+} dvh_sweep_draws;
+int dvh_series_draws(dvh_handle* h, const dvh_sweep_draws* d);
+
+/* The device builder's inputs (dvh_battery_group base / retail / c0) of G windows cut from the scenarios' series:
+ * window k of scenario rows[k] covers steps t0 .. t0 + T - 1 (rep steps per hour of the hourly series);
+ *   base[k][t]   = (site_load[h] * load_scale[s]) * (1 + 0.05 * ar[s][h]) - pv_rated[s] * pv_profile[h] + hp[s],
+ *   retail[k][t] = price[t0 + t] * price_scale[s],                                  h = (t0 + t) / rep,
+ *   c0[k]        = the retail term's constant sum((retail * dt) * base) as numpy sums it (in step order; pairwise
+ *                  when G = 1), + c0_add[s]
+ * (J > 0: the window has demand-charge columns, which add zero constants).  All pointers device; rows are
+ * range-checked on the device (DVH_ERR_ARG).  Asynchronous on the handle's stream; returns after it completed. */
+typedef struct dvh_window_series {
+  int32_t G, T, t0, rep, J, count, hours;
+  double dt;
+  const int32_t* rows;             /* [G] scenario of each window, 0 <= rows[k] < count                        */
+  const double* ar;                /* [count * hours] (dvh_series_draws)                                       */
+  const double* site_load;         /* [hours] kW                                                                */
+  const double* pv_profile;        /* [hours] kW per rated kW (NaN as 0)                                        */
+  const double* price;             /* [>= t0 + T] energy price per step, $/kWh                                  */
+  const double* load_scale;        /* [count]                                                                   */
+  const double* price_scale;       /* [count]                                                                   */
+  const double* pv_rated;          /* [count] kW                                                                */
+  const double* hp;                /* [count] housekeeping power, kW                                            */
+  const double* c0_add;            /* [count] fixed O&M x discharge rating                                      */
+  double* base;                    /* out [G * T]                                                               */
+  double* retail;                  /* out [G * T]                                                               */
+  double* c0;                      /* out [G]                                                                   */
+} dvh_window_series;
+int dvh_series_windows(dvh_handle* h, const dvh_window_series* w);
 
 /* ---- Seeded scenario sweeps (dervet_hip/sweep.py; the sensitivity cases of dervet/DERVET.py:75 solve the same
  * windows for many perturbed scenarios; no reference counterpart: the reference solves every window cold).

@@ -7,8 +7,9 @@ through the C ABI.  Per window, benefit = original bill (site load alone, oracle
 benefits of the opt year against the golden pro forma's 2017 avoided charges; and the pro forma rebuilt from them
 (escalated at the value streams' growth rates) against the golden NPV row.
 
-Bars: per-window benefit within 2e-4 relative (the objective is solved to ~1e-6 of a 300 k$ window cost, and
-the benefit is ~4-40 k$), yearly avoided charges and NPVs within 1e-4.
+Bars: per-window benefit within 1e-4 relative (the objective is solved to ~1e-6 of a 300 k$ window cost, and
+the benefit is ~4-40 k$; measured at most 4.1e-5 with the same algorithm, oracle/cpu_pdhg.cpp, r03), yearly avoided
+charges and NPVs within 1e-4.
 """
 import numpy as np
 import pytest
@@ -52,7 +53,7 @@ def test_gpu_battery_benefit_matches_golden_bills_proforma_and_npv(name):
     gold_d = np.array(b["original_demand_charge"]) - b["demand_charge"]
     tot, gold = ben.sum(1), gold_e + gold_d
     rel = np.abs(tot - gold) / np.abs(gold)
-    assert rel.max() <= 2e-4, rel
+    assert rel.max() <= 1e-4, rel
     ae, ad = ben[:, 0].sum(), ben[:, 1].sum()
     assert ae + ad == pytest.approx(b["proforma"]["Avoided Energy Charge"][1] + b["proforma"]["Avoided Demand Charge"][1],
                                     rel=1e-4)

@@ -36,7 +36,7 @@ def _mixed_case(spec):
                                        da_price=da, n=96 * 7, ene_min=emin, ene_max=emax, spec=spec)
 
 
-@pytest.mark.parametrize("case", ["config4", "config1_da", "mixed"])
+@pytest.mark.parametrize("case", ["config4", "config1_da", "mixed", "config5_ice"])
 def test_device_builder_is_bit_identical_to_the_host_builder(gpu_solver, case):
     if case == "config4":
         host, spec = scenarios.config4(range(12)), scenarios.config4(range(12), spec=True)
@@ -46,6 +46,8 @@ def test_device_builder_is_bit_identical_to_the_host_builder(gpu_solver, case):
         spec = scenarios.windows_by_period(2017, 1.0, ri["hourly_site_load"][None, :], None,
                                            scenarios.template_battery(), tariff_def=scenarios.tariff("data_tariff"),
                                            da_price=ri["hourly_da_price"][None, :], spec=True)
+    elif case == "config5_ice":  # LP-relaxed ICE + reliability SOE floors, a leap year's calendar
+        host, spec = (scenarios.config5(range(5), years=1, start_year=2020, spec=f) for f in (False, True))
     else:
         host, spec = _mixed_case(False), _mixed_case(True)
     dev = gpu_builder.pack_specs_device(spec, gpu_solver)
