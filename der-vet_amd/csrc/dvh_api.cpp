@@ -67,6 +67,11 @@ struct dvh_handle {
   DevBuf o_data, o_cases, o_len, o_hist, o_soe;  // reliability sweep
   DevBuf s_pairs, s_bad;                          // seeded-sweep warm transfer (dvh_sweep.hip)
   DevBuf g_seeds, g_word;                         // scenario series generator (dvh_series.hip)
+  DevBuf d_route;                                 // cascade lists' counts / ELL widths (dvh_route.hip)
+  int32_t* route_host = nullptr;                  // their pinned host mirror (one small read-back per tier)
+  hipStream_t aux = nullptr;                      // the second ELL / generic size class runs here, concurrently
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+  int n_syncs = 0;                                // host waits on the stream in the last solve
   double outage_ms = 0.0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   // per-chunk timing events: a pool created on first use and reused by every solve (destroyed with the handle), so
@@ -86,6 +91,12 @@ struct dvh_handle {
   // thread per device, no inter-device traffic), results written straight into the caller's buffers.
   std::vector<dvh_handle*> peers;
 };
+
+// Every host wait on a solve's stream goes through here (dvh_last_host_syncs reports the count of the last solve).
+static hipError_t sync_stream(dvh_handle* h, hipStream_t s) {
+  ++h->n_syncs;
+  return hipStreamSynchronize(s);
+}
 
 static int fail(dvh_handle* h, int code, const std::string& msg) {
   if (h) h->err = msg;
@@ -226,8 +237,12 @@ int dvh_destroy(dvh_handle* h) {
                     &h->w_kval, &h->w_rowof, &h->w_perm, &h->w_dr, &h->w_dc, &h->w_cs, &h->w_ls, &h->w_us,
                     &h->w_qs, &h->w_vbuf, &h->w_wbuf, &h->w_tmpc, &h->w_tmpr, &h->w_longk, &h->w_longt, &h->w_scal,
                     &h->m_list, &h->m_plan, &h->m_pos, &h->m_xbuf, &h->m_abort, &h->o_data, &h->o_cases, &h->o_len, &h->o_hist, &h->o_soe,
-                    &h->s_pairs, &h->s_bad};
+                    &h->s_pairs, &h->s_bad, &h->g_seeds, &h->g_word, &h->d_route};
   for (DevBuf* b : bufs) b->release();
+  if (h->route_host) hipHostFree(h->route_host);
+  if (h->fork_ev) hipEventDestroy(h->fork_ev);
+  if (h->join_ev) hipEventDestroy(h->join_ev);
+  if (h->aux) hipStreamDestroy(h->aux);
   for (auto& e : h->ev)
     if (e) hipEventDestroy(e);
   for (auto& ce : h->chunk_events)
@@ -326,6 +341,12 @@ int dvh_series_windows(dvh_handle* h, const dvh_window_series* w) {
 int dvh_synchronize(dvh_handle* h) {
   if (!h) return DVH_ERR_ARG;
   DVH_HIP(h, hipStreamSynchronize(h->stream));
+  return DVH_OK;
+}
+
+int dvh_last_host_syncs(const dvh_handle* h, int32_t* out) {
+  if (!h || !out) return DVH_ERR_ARG;
+  *out = h->n_syncs;
   return DVH_OK;
 }
 
@@ -610,7 +631,7 @@ static int chain_pass(dvh_handle* h, const dvh::Batch& b, const dvh::Work& w, co
   if (e != hipSuccess) return hip_fail(h, e, "launch_chain_plan");
   std::vector<int32_t> head((size_t)nm * 4);  // {P, T, J, k} of every plan record
   DVH_HIP(h, hipMemcpy2DAsync(head.data(), 4 * I, h->m_plan.p, I * dvh::kPlanInts, 4 * I, nm, hipMemcpyDeviceToHost, s));
-  DVH_HIP(h, hipStreamSynchronize(s));
+  DVH_HIP(h, sync_stream(h, s));
   std::vector<int32_t> small_setup, accepted;
   for (int i = 0; i < nm; ++i) {
     const int P = head[4 * (size_t)i];
@@ -640,7 +661,7 @@ static int chain_pass(dvh_handle* h, const dvh::Batch& b, const dvh::Work& w, co
   for (size_t a = 0; a < accepted.size(); ++a)
     DVH_HIP(h, hipMemcpyAsync(&flag6[a], w.scal + (int64_t)(med[accepted[a]] - ch.first) * dvh::kScal + 6,
                               sizeof(double), hipMemcpyDeviceToHost, s));
-  DVH_HIP(h, hipStreamSynchronize(s));
+  DVH_HIP(h, sync_stream(h, s));
   std::vector<int32_t> groups[2];  // plan positions: [0] up to kChainMedMax segments, [1] longer
   int PTg[2] = {0, 0};
   for (size_t a = 0; a < accepted.size(); ++a) {
@@ -691,7 +712,7 @@ static int chain_pass(dvh_handle* h, const dvh::Batch& b, const dvh::Work& w, co
       if (e != hipSuccess) return hip_fail(h, e, "launch_chain");
       std::vector<int32_t> ab(dvh::chain_abort_bytes(S) / I);
       DVH_HIP(h, hipMemcpyAsync(ab.data(), h->m_abort.p, I * ab.size(), hipMemcpyDeviceToHost, s));
-      DVH_HIP(h, hipStreamSynchronize(s));
+      DVH_HIP(h, sync_stream(h, s));
       if (ab[0] != 0) {
         // a segment exchange outlasted the spin limit: the windows the launch finished keep their results, the
         // others (still marked pending) go to the grid-wide path; the diagnostics stay readable in dvh_last_error
@@ -725,6 +746,122 @@ static int chain_pass(dvh_handle* h, const dvh::Batch& b, const dvh::Work& w, co
 }
 
 // Solve a packed device batch given a host copy of its descriptors.
+// The default kernel cascade over one chunk's small windows, its lists formed on the device (dvh_route.hip): the
+// battery-banded kernel over the chunk -> its refusals (status -2) through the band-ICE form -> what that refuses
+// through the ELL kernels, in two size classes (the small market-day kernels' shapes, n <= 512 and m <= 768, and the
+// rest), each instantiation sized for its class -> their refusals (-1) through the generic CSR kernel, per class.
+// One small read-back per stage that ran ({count, ELL widths, max n / m / nnz} of the windows it hands on); a batch
+// the band kernel takes whole waits once.
+static int device_cascade(dvh_handle* h, const dvh::Batch& b, const dvh::Work& w, const dvh::Chunk& ch,
+                          const dvh::Opts& o, int nsmall, int wc, hipStream_t s) {
+  const size_t I = sizeof(int32_t);
+  int32_t* L[4];
+  for (int r = 0; r < 4; ++r) L[r] = h->d_list.as<int32_t>() + (size_t)r * wc;
+  int32_t* info = h->d_route.as<int32_t>();  // 8 ints per route: {count, wx, wy, max n, max m, max nnz}
+  int32_t* rh = h->route_host;
+  if (h->cus <= 0 && hipDeviceGetAttribute(&h->cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess)
+    h->cus = 256;
+  // band kernel form: three steps per lane (two windows per CU) once the windows outnumber the CUs; a window alone
+  // on its CU is faster in the one-step form (0.75 vs 0.97 us per iteration, profiles/r02x_band_forms.log)
+  const int forced_form = h->kernel_path == 3 ? 1 : h->kernel_path == 4 ? 3 : 0;
+  auto form_for = [&](int nl) { return forced_form ? forced_form : (nl <= h->cus ? 1 : 3); };
+  // route: the windows of `in` (or the chunk) with status `want` and size class `cls` -> L[out], info slot `slot`
+  auto route = [&](int slot, const int32_t* in, int n_in, int want, int cls, int out) -> hipError_t {
+    return dvh::launch_route(b.desc, b.istats, w.scal, ch.first, n_in, in, want, dvh::kSmallMax, cls, 512, 768,
+                             L[out], info + 8 * slot, s);
+  };
+  auto readback = [&](int slot0, int nslots) -> hipError_t {
+    hipError_t e = hipMemcpyAsync(rh + 8 * slot0, info + 8 * slot0, 8 * I * nslots, hipMemcpyDeviceToHost, s);
+    return e != hipSuccess ? e : sync_stream(h, s);
+  };
+  int variant = -1, bvar = -1;
+  DVH_HIP(h, dvh::launch_pdhg_band(b, w, ch, o, s, false, form_for(ch.count), nullptr, 0, &bvar));
+  DVH_HIP(h, route(0, nullptr, ch.count, -2, 0, 0));
+  DVH_HIP(h, readback(0, 1));
+  int cur = rh[0];
+  h->n_band += nsmall - cur;
+  if (nsmall - cur > 0) variant = bvar;
+  if (cur > 0) {  // pass 2: the band kernel's ICE form over pass 1's refusals, which it hands on by size class
+    DVH_HIP(h, dvh::launch_pdhg_band(b, w, ch, o, s, true, form_for(cur), L[0], cur, &bvar));
+    DVH_HIP(h, route(1, L[0], cur, -2, 1, 2));
+    DVH_HIP(h, route(2, L[0], cur, -2, 2, 3));
+    DVH_HIP(h, readback(1, 2));
+    const int left = rh[8] + rh[16];
+    h->n_band += cur - left;
+    if (cur - left > 0 && variant < 0) variant = bvar;
+    cur = left;
+  }
+  if (cur == 0) {
+    h->last_variant = variant;
+    return DVH_OK;
+  }
+  // ELL per size class (class c's windows in L[2 + c], info slot 1 + c; refusals -> L[c], the consumed lists), the
+  // two classes concurrently: class 0 on the solve's stream, class 1 on the handle's second stream (disjoint windows,
+  // workspace and lists), joined back into the solve's stream by an event
+  const bool both = rh[8] > 0 && rh[16] > 0;
+  if (both && !h->aux) {
+    DVH_HIP(h, hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking));
+    DVH_HIP(h, hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming));
+    DVH_HIP(h, hipEventCreateWithFlags(&h->join_ev, hipEventDisableTiming));
+  }
+  hipStream_t cs[2] = {s, both ? h->aux : s};
+  if (both) {
+    DVH_HIP(h, hipEventRecord(h->fork_ev, s));
+    DVH_HIP(h, hipStreamWaitEvent(h->aux, h->fork_ev, 0));
+  }
+  auto join = [&]() -> hipError_t {
+    if (!both) return hipSuccess;
+    hipError_t e = hipEventRecord(h->join_ev, h->aux);
+    return e != hipSuccess ? e : hipStreamWaitEvent(s, h->join_ev, 0);
+  };
+  int ran[2] = {0, 0};
+  for (int c = 0; c < 2; ++c) {
+    const int32_t* in = rh + 8 * (1 + c);
+    if (in[0] == 0) continue;
+    int ev = -1;
+    hipError_t e = dvh::launch_pdhg_ell(b, w, ch, o, in[3], in[4], in[1], in[2], cs[c], &ev, L[2 + c], in[0],
+                                        in[0] <= 2 * h->cus);
+    if (e == hipSuccess) {
+      if (variant < 0) variant = ev;
+      DVH_HIP(h, dvh::launch_route(b.desc, b.istats, w.scal, ch.first, in[0], L[2 + c], -1, dvh::kSmallMax, 0, 512,
+                                   768, L[c], info + 8 * (3 + c), cs[c]));
+      DVH_HIP(h, hipMemcpyAsync(rh + 8 * (3 + c), info + 8 * (3 + c), 8 * I, hipMemcpyDeviceToHost, cs[c]));
+      ran[c] = 1;
+    } else if (e == hipErrorInvalidValue) {  // no ELL instantiation holds this class: all generic
+      (void)hipGetLastError();
+    } else {
+      return hip_fail(h, e, "launch_pdhg_ell");
+    }
+  }
+  if (ran[0] || ran[1]) {
+    if (ran[1]) DVH_HIP(h, join());
+    DVH_HIP(h, sync_stream(h, s));
+  }
+  for (int c = 0; c < 2; ++c) {
+    const int32_t* in = rh + 8 * (1 + c);
+    if (in[0] == 0) continue;
+    const int32_t* g = ran[c] ? rh + 8 * (3 + c) : in;  // the generic kernel's windows and their sizes
+    const int32_t* gl = ran[c] ? L[c] : L[2 + c];
+    if (ran[c]) h->n_ell += in[0] - g[0];
+    if (g[0] == 0) continue;
+    if (c == 1 && ran[1]) {  // the second class ran ELL and was joined: fork again for its generic pass
+      DVH_HIP(h, hipEventRecord(h->fork_ev, s));
+      DVH_HIP(h, hipStreamWaitEvent(h->aux, h->fork_ev, 0));
+    }
+    DVH_HIP(h, dvh::launch_power(b, w, ch, o, gl, g[0], cs[c]));
+    int gv = -1;
+    hipError_t e = dvh::launch_pdhg(b, w, ch, o, g[3], g[4], g[5], cs[c], &gv, gl, g[0]);
+    if (e == hipErrorInvalidValue)
+      return fail(h, DVH_ERR_UNSUPPORTED, "window too large for the on-chip PDHG kernels (n or m > 4096)");
+    if (e != hipSuccess) return hip_fail(h, e, "launch_pdhg");
+    h->n_generic += g[0];
+    if (variant < 0) variant = gv;
+  }
+  DVH_HIP(h, join());  // everything on the second stream is ordered before the solve's stream goes on
+  h->last_variant = variant;
+  return DVH_OK;
+}
+
 static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<int64_t>& desc, hipStream_t s) {
   const int count = bt->count;
   dvh::Opts o;
@@ -832,7 +969,9 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
               h->w_cs.as<double>(), h->w_ls.as<double>(), h->w_us.as<double>(), h->w_qs.as<double>(),
               h->w_vbuf.as<double>(), h->w_wbuf.as<double>(), h->w_tmpc.as<double>(), h->w_tmpr.as<double>(),
               h->w_longk.as<int32_t>(), h->w_longt.as<int32_t>(), h->d_hinv.as<double>(), h->w_scal.as<double>()};
-  DVH_HIP(h, h->d_list.ensure(I * (size_t)wc));
+  DVH_HIP(h, h->d_list.ensure(I * 4 * (size_t)wc));  // the cascade's four device lists (dvh_route.hip)
+  DVH_HIP(h, h->d_route.ensure(I * 8 * 5));
+  if (!h->route_host) DVH_HIP(h, hipHostMalloc((void**)&h->route_host, I * 8 * 5, hipHostMallocDefault));
   h->n_ell = h->n_generic = h->n_large = h->n_band = h->n_chain = 0;
   h->large_ms[0] = h->large_ms[1] = 0.0f;
   h->chunk_used = 0;
@@ -864,10 +1003,18 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
       DVH_HIP(h, hipEventRecord(e2, s));
       continue;
     }
+    const bool fast = h->kernel_path != 1 && o.rho == 1.0;
+    if (fast && (h->kernel_path == 0 || h->kernel_path >= 3)) {
+      if (int rc = device_cascade(h, b, w, c.ch, o, c.nsmall, wc, s)) return rc;
+      if (int rc = chain_pass(h, b, w, c.ch, o, c.med, c.med_T, desc, med_done, s)) return rc;
+      DVH_HIP(h, hipEventRecord(e2, s));
+      continue;
+    }
+    // ---- A/B paths (generic only, ELL -> generic): lists formed on the host
     // ELL widths from the setup statistics (one small D2H per chunk)
     scal.resize((size_t)c.ch.count * dvh::kScal);
     DVH_HIP(h, hipMemcpyAsync(scal.data(), w.scal, sizeof(double) * scal.size(), hipMemcpyDeviceToHost, s));
-    DVH_HIP(h, hipStreamSynchronize(s));
+    DVH_HIP(h, sync_stream(h, s));
     int wx = 0, wy = 0;
     for (int k = 0; k < c.ch.count; ++k) {
       const double* sc = &scal[(size_t)k * dvh::kScal];
@@ -879,7 +1026,6 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
     // Kernel cascade: battery-banded kernel over the chunk -> ELL kernel over the windows it returned (status
     // -2) -> generic CSR kernel over the windows the ELL kernel returned (status -1).  The fast kernels are
     // specialised to reflection rho = 1 (the default); other values use the generic kernel.
-    const bool fast = h->kernel_path != 1 && o.rho == 1.0;
     std::vector<int32_t> ell_list;  // empty + ell_all: the whole chunk
     bool ell_all = true;
     if (fast && (h->kernel_path == 0 || h->kernel_path >= 3)) {
@@ -908,7 +1054,7 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
         r = hipMemcpyAsync(ist.data(), bt->istats + 2 * (size_t)c.ch.first, I * ist.size(), hipMemcpyDeviceToHost,
                            s);
         if (r != hipSuccess) return r;
-        r = hipStreamSynchronize(s);
+        r = sync_stream(h, s);
         if (r != hipSuccess) return r;
         out.clear();
         int nb = 0;
@@ -955,7 +1101,7 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
       ist.resize(2 * (size_t)c.ch.count);
       DVH_HIP(h, hipMemcpyAsync(ist.data(), bt->istats + 2 * (size_t)c.ch.first, I * ist.size(),
                                 hipMemcpyDeviceToHost, s));
-      DVH_HIP(h, hipStreamSynchronize(s));
+      DVH_HIP(h, sync_stream(h, s));
       int nl = 0;
       for (int k = 0; k < c.ch.count; ++k) {
         if (is_large(c.ch.first + k)) {
@@ -986,7 +1132,7 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
       if (e != hipSuccess) return hip_fail(h, e, "launch_pdhg");
       h->n_generic += (int)generic.size();
       if (variant < 0) variant = gv;
-      DVH_HIP(h, hipStreamSynchronize(s));  // d_list is reused by the next chunk
+      DVH_HIP(h, sync_stream(h, s));  // d_list is reused by the next chunk
     }
     if (int rc = chain_pass(h, b, w, c.ch, o, c.med, c.med_T, desc, med_done, s)) return rc;
     DVH_HIP(h, hipEventRecord(e2, s));
@@ -1007,7 +1153,7 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
 }
 
 static int finish_timing(dvh_handle* h, hipStream_t s) {
-  DVH_HIP(h, hipStreamSynchronize(s));
+  DVH_HIP(h, sync_stream(h, s));
   float t = 0;
   h->timing[0] = h->timing[1] = h->timing[2] = 0;
   if (hipEventElapsedTime(&t, h->ev[0], h->ev[3]) == hipSuccess) h->timing[0] = t;
@@ -1184,6 +1330,7 @@ static int solve_batch_one(dvh_handle* h, const dvh_lp* lps, int32_t count, dvh_
   bt.y = h->d_y.as<double>();
   bt.stats = h->d_stats.as<double>();
   bt.istats = h->d_istats.as<int32_t>();
+  h->n_syncs = 0;
   int rc = solve_packed(h, &bt, desc, s);
   if (rc != DVH_OK) return rc;
   std::vector<double> x(tn), y(tm), stats(4 * (size_t)count);
@@ -1217,9 +1364,10 @@ extern "C" int dvh_solve_packed_device(dvh_handle* h, const dvh_packed* bt, void
     return fail(h, DVH_ERR_ARG, "null device array in packed batch");
   DVH_HIP(h, hipSetDevice(h->device));
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->stream;
+  h->n_syncs = 0;
   std::vector<int64_t> desc(8 * (size_t)bt->count);
   DVH_HIP(h, hipMemcpyAsync(desc.data(), bt->desc, desc.size() * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  DVH_HIP(h, hipStreamSynchronize(s));
+  DVH_HIP(h, sync_stream(h, s));
   // host-side sanity of the descriptors (no device data is read beyond desc)
   for (int k = 0; k < bt->count; ++k) {
     const int64_t* d = &desc[8 * (size_t)k];

@@ -106,8 +106,10 @@ hipError_t launch_pdhg(const Batch& b, const Work& w, const Chunk& ch, const Opt
 // ELL fast-path kernel over the whole chunk, or over the listed windows (wx, wy: ELL widths for K^T and K).
 // Windows that do not fit its shape come back with istats status -1 (kNeedsGeneric) and must be re-run by
 // launch_pdhg.
+// latency: skip the several-windows-per-CU small variants (a list of at most two windows per CU).
 hipError_t launch_pdhg_ell(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n, int max_m,
-                           int wx, int wy, hipStream_t s, int* variant_out, const int32_t* list, int nlist);
+                           int wx, int wy, hipStream_t s, int* variant_out, const int32_t* list, int nlist,
+                           bool latency = false);
 // Battery-banded kernel (dvh_band.hip) over the whole chunk.  Windows whose CSR is not the battery + DCM
 // window shape come back with istats status -2 (kNeedsEll) and must be re-run by launch_pdhg_ell.
 // ice: the variant with LP-relaxed ICE columns (elec, on) and rows; list (nlist entries): global window indices,
@@ -153,6 +155,12 @@ hipError_t launch_warm_transfer(const int64_t* desc, const double* c, const doub
 hipError_t launch_series_draws(const uint64_t* seeds, int count, int steps, int n_unif, double a1, double innov,
                                double* z0, double* ar, double* unif, int32_t* ambiguous, hipStream_t s);
 hipError_t launch_series_windows(const ::dvh_window_series& w, int32_t* bad, hipStream_t s);
+// Cascade lists on the device (dvh_route.hip): the small windows of [first, first + count) -- or of in_list[0 ..
+// count) -- whose status is `want` (cls 1: and n <= lim_n, m <= lim_m; cls 2: the others; cls 0: any size), in order,
+// to out_list; out_info[0..5] = {their number, max ELL widths wx, wy, max n, m, nnz} over them.
+hipError_t launch_route(const int64_t* desc, const int32_t* istats, const double* scal, int first, int count,
+                        const int32_t* in_list, int want, int small_max, int cls, int lim_n, int lim_m,
+                        int32_t* out_list, int32_t* out_info, hipStream_t s);
 // Power iteration for ||Kt||_2 of the listed windows (generic path; the ELL kernel does its own on chip).
 hipError_t launch_power(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, const int32_t* list, int nlist,
                         hipStream_t s);

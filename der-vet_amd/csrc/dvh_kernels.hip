@@ -1791,8 +1791,12 @@ hipError_t small_dispatch(int max_n, int max_m, int wx, int wy, const Batch& b, 
 static bool small_enabled() { return small_variant() >= 0; }
 
 hipError_t launch_pdhg_ell(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n, int max_m,
-                           int wx, int wy, hipStream_t s, int* variant_out, const int32_t* list, int nlist) {
-  if (max_n <= 512 && max_m <= 768 && wx <= 6 && wy <= 8 && small_enabled()) {
+                           int wx, int wy, hipStream_t s, int* variant_out, const int32_t* list, int nlist,
+                           bool latency) {
+  // latency: few windows (at most two per CU) -- the small variants pack several windows per CU for throughput and
+  // lose to the one-window-per-CU kernels then (market days: 14.7 vs 11.0 ms for 365 windows, 15.3 vs 18.8 ms for
+  // 1,095, profiles/r03h_market_paths.log), so only the 512-thread ELL kernels or the generic kernel are tried
+  if (max_n <= 512 && max_m <= 768 && wx <= 6 && wy <= 8 && small_enabled() && !latency) {
     const hipError_t e = small_dispatch(max_n, max_m, wx, wy, b, w, ch, o, s, variant_out, list, nlist);
     if (e != hipErrorInvalidValue) return e;
     (void)hipGetLastError();  // no small variant covers the shape (e.g. DVH_SMALL forcing one): the 512-thread kernels

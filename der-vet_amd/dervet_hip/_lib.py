@@ -110,6 +110,7 @@ SYMBOLS = {
     "dvh_series_windows": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(WindowSeries)]),
     "dvh_last_timing": (ctypes.c_int, [ctypes.c_void_p, c_double_p]),
     "dvh_last_stats": (ctypes.c_int, [ctypes.c_void_p, c_int32_p]),
+    "dvh_last_host_syncs": (ctypes.c_int, [ctypes.c_void_p, c_int32_p]),
     "dvh_last_path_counts": (ctypes.c_int, [ctypes.c_void_p, c_int32_p]),
     "dvh_last_path_counts4": (ctypes.c_int, [ctypes.c_void_p, c_int32_p]),
     "dvh_last_path_counts5": (ctypes.c_int, [ctypes.c_void_p, c_int32_p]),

@@ -10,7 +10,7 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "..", "csrc")
 LIB = os.path.join(HERE, "libdervet_hip.so")
-SOURCES = ["dvh_kernels.hip", "dvh_band.hip", "dvh_chain.hip", "dvh_build.hip", "dvh_sweep.hip", "dvh_series.hip", "dvh_large.hip", "dvh_outage.hip",
+SOURCES = ["dvh_kernels.hip", "dvh_band.hip", "dvh_chain.hip", "dvh_build.hip", "dvh_sweep.hip", "dvh_series.hip", "dvh_route.hip", "dvh_large.hip", "dvh_outage.hip",
            "dvh_api.cpp", "dvh_validate.cpp"]
 HEADERS = ["dvh_internal.h", "dvh_device.h", "dvh_validate.h", "dvh_rng.h", "dvh_ziggurat.h", os.path.join("..", "..", "include", "dervet_hip.h")]
 

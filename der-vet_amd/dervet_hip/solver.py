@@ -148,6 +148,12 @@ class BatchSolver:
         return {"band_windows": c[3], "ell_windows": v[0], "generic_windows": v[1], "variant": v[2],
                 "generic_only": bool(v[3]), "large_windows": c[2], "chain_windows": c[4]}
 
+    def host_syncs(self):
+        """Host waits on the stream during the last solve (dvh_last_host_syncs)."""
+        v = ctypes.c_int32()
+        self._check(self._lib.dvh_last_host_syncs(self._h, ctypes.byref(v)), "dvh_last_host_syncs")
+        return int(v.value)
+
     _PATHS = {"default": 0, "generic": 1, "ell": 2, "band1": 3, "band3": 4}
 
     def set_kernel_path(self, path):

@@ -262,6 +262,10 @@ int dvh_warm_transfer(dvh_handle* h, const dvh_packed* batch, const int32_t* pai
  * [0] whole solve, [1] setup kernel (transpose + scaling + power iteration), [2] PDHG kernel. */
 int dvh_last_timing(const dvh_handle* h, double* ms3);
 
+/* Host waits on the stream during the most recent solve (dvh_solve_batch / dvh_solve_packed_device): the
+ * descriptors' read-back (device batches), one per kernel tier that ran (the cascade's lists are formed on the
+ * device, dvh_route.hip), the medium tier's hand-offs, and the final wait for the results and timing events. */
+int dvh_last_host_syncs(const dvh_handle* h, int32_t* out);
 /* Kernel-path diagnostics of the most recent solve: out4 = {windows solved by the ELL fast kernel,
  * windows solved by the generic CSR kernel, kernel variant code, generic_only flag}. */
 int dvh_last_stats(const dvh_handle* h, int32_t* out4);

@@ -389,6 +389,10 @@ int dvh_build_battery_group(dvh_handle*, const dvh_battery_group*, const dvh_pac
   return DVH_ERR_UNSUPPORTED;  // device-only entry
 }
 int dvh_series_draws(dvh_handle*, const dvh_sweep_draws*) { return DVH_ERR_UNSUPPORTED; }       // device-only
+int dvh_last_host_syncs(const dvh_handle*, int32_t* out) {
+  if (out) *out = 0;  // no device stream
+  return DVH_OK;
+}
 int dvh_series_windows(dvh_handle*, const dvh_window_series*) { return DVH_ERR_UNSUPPORTED; }   // device-only
 int dvh_last_path_counts5(const dvh_handle*, int32_t* out5) {
   if (out5) std::memset(out5, 0, 5 * sizeof(int32_t));
