@@ -69,8 +69,6 @@ struct dvh_handle {
   DevBuf g_seeds, g_word;                         // scenario series generator (dvh_series.hip)
   DevBuf d_route;                                 // cascade lists' counts / ELL widths (dvh_route.hip)
   int32_t* route_host = nullptr;                  // their pinned host mirror (one small read-back per tier)
-  hipStream_t aux = nullptr;                      // the second ELL / generic size class runs here, concurrently
-  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   int n_syncs = 0;                                // host waits on the stream in the last solve
   double outage_ms = 0.0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -240,9 +238,6 @@ int dvh_destroy(dvh_handle* h) {
                     &h->s_pairs, &h->s_bad, &h->g_seeds, &h->g_word, &h->d_route};
   for (DevBuf* b : bufs) b->release();
   if (h->route_host) hipHostFree(h->route_host);
-  if (h->fork_ev) hipEventDestroy(h->fork_ev);
-  if (h->join_ev) hipEventDestroy(h->join_ev);
-  if (h->aux) hipStreamDestroy(h->aux);
   for (auto& e : h->ev)
     if (e) hipEventDestroy(e);
   for (auto& ce : h->chunk_events)
@@ -749,7 +744,8 @@ static int chain_pass(dvh_handle* h, const dvh::Batch& b, const dvh::Work& w, co
 // The default kernel cascade over one chunk's small windows, its lists formed on the device (dvh_route.hip): the
 // battery-banded kernel over the chunk -> its refusals (status -2) through the band-ICE form -> what that refuses
 // through the ELL kernels, in two size classes (the small market-day kernels' shapes, n <= 512 and m <= 768, and the
-// rest), each instantiation sized for its class -> their refusals (-1) through the generic CSR kernel, per class.
+// rest), each instantiation sized for its class -> what they refuse (-1) or cannot hold through the generic CSR
+// kernel, both classes in one launch.
 // One small read-back per stage that ran ({count, ELL widths, max n / m / nnz} of the windows it hands on); a batch
 // the band kernel takes whole waits once.
 static int device_cascade(dvh_handle* h, const dvh::Batch& b, const dvh::Work& w, const dvh::Chunk& ch,
@@ -795,37 +791,17 @@ static int device_cascade(dvh_handle* h, const dvh::Batch& b, const dvh::Work& w
     h->last_variant = variant;
     return DVH_OK;
   }
-  // ELL per size class (class c's windows in L[2 + c], info slot 1 + c; refusals -> L[c], the consumed lists), the
-  // two classes concurrently: class 0 on the solve's stream, class 1 on the handle's second stream (disjoint windows,
-  // workspace and lists), joined back into the solve's stream by an event
-  const bool both = rh[8] > 0 && rh[16] > 0;
-  if (both && !h->aux) {
-    DVH_HIP(h, hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking));
-    DVH_HIP(h, hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming));
-    DVH_HIP(h, hipEventCreateWithFlags(&h->join_ev, hipEventDisableTiming));
-  }
-  hipStream_t cs[2] = {s, both ? h->aux : s};
-  if (both) {
-    DVH_HIP(h, hipEventRecord(h->fork_ev, s));
-    DVH_HIP(h, hipStreamWaitEvent(h->aux, h->fork_ev, 0));
-  }
-  auto join = [&]() -> hipError_t {
-    if (!both) return hipSuccess;
-    hipError_t e = hipEventRecord(h->join_ev, h->aux);
-    return e != hipSuccess ? e : hipStreamWaitEvent(s, h->join_ev, 0);
-  };
+  // ELL per size class (class c's windows in L[2 + c], info slot 1 + c; refusals -> L[c], the consumed lists)
   int ran[2] = {0, 0};
   for (int c = 0; c < 2; ++c) {
     const int32_t* in = rh + 8 * (1 + c);
     if (in[0] == 0) continue;
     int ev = -1;
-    hipError_t e = dvh::launch_pdhg_ell(b, w, ch, o, in[3], in[4], in[1], in[2], cs[c], &ev, L[2 + c], in[0],
+    hipError_t e = dvh::launch_pdhg_ell(b, w, ch, o, in[3], in[4], in[1], in[2], s, &ev, L[2 + c], in[0],
                                         in[0] <= 2 * h->cus);
     if (e == hipSuccess) {
       if (variant < 0) variant = ev;
-      DVH_HIP(h, dvh::launch_route(b.desc, b.istats, w.scal, ch.first, in[0], L[2 + c], -1, dvh::kSmallMax, 0, 512,
-                                   768, L[c], info + 8 * (3 + c), cs[c]));
-      DVH_HIP(h, hipMemcpyAsync(rh + 8 * (3 + c), info + 8 * (3 + c), 8 * I, hipMemcpyDeviceToHost, cs[c]));
+      DVH_HIP(h, route(3 + c, L[2 + c], in[0], -1, 0, c));
       ran[c] = 1;
     } else if (e == hipErrorInvalidValue) {  // no ELL instantiation holds this class: all generic
       (void)hipGetLastError();
@@ -833,31 +809,36 @@ static int device_cascade(dvh_handle* h, const dvh::Batch& b, const dvh::Work& w
       return hip_fail(h, e, "launch_pdhg_ell");
     }
   }
-  if (ran[0] || ran[1]) {
-    if (ran[1]) DVH_HIP(h, join());
-    DVH_HIP(h, sync_stream(h, s));
-  }
+  if (ran[0] || ran[1]) DVH_HIP(h, readback(3, 2));
+  // the generic kernel over what is left of both classes, in one launch (one window per CU; a window's time does not
+  // depend on the other windows', so the classes overlap inside the launch), sized for the windows it gets
+  int gn = 0, gm[3] = {0, 0, 0};
+  int32_t* gl = nullptr;
   for (int c = 0; c < 2; ++c) {
     const int32_t* in = rh + 8 * (1 + c);
     if (in[0] == 0) continue;
-    const int32_t* g = ran[c] ? rh + 8 * (3 + c) : in;  // the generic kernel's windows and their sizes
-    const int32_t* gl = ran[c] ? L[c] : L[2 + c];
+    const int32_t* g = ran[c] ? rh + 8 * (3 + c) : in;  // this class's windows for the generic kernel, their sizes
+    int32_t* l = ran[c] ? L[c] : L[2 + c];
     if (ran[c]) h->n_ell += in[0] - g[0];
     if (g[0] == 0) continue;
-    if (c == 1 && ran[1]) {  // the second class ran ELL and was joined: fork again for its generic pass
-      DVH_HIP(h, hipEventRecord(h->fork_ev, s));
-      DVH_HIP(h, hipStreamWaitEvent(h->aux, h->fork_ev, 0));
+    if (!gl) {
+      gl = l;
+    } else {  // append to the first class's list (disjoint subsets of the chunk: fits its wc slots)
+      DVH_HIP(h, hipMemcpyAsync(gl + gn, l, I * g[0], hipMemcpyDeviceToDevice, s));
     }
-    DVH_HIP(h, dvh::launch_power(b, w, ch, o, gl, g[0], cs[c]));
+    gn += g[0];
+    for (int u = 0; u < 3; ++u) gm[u] = std::max(gm[u], (int)g[3 + u]);
+  }
+  if (gn > 0) {
+    DVH_HIP(h, dvh::launch_power(b, w, ch, o, gl, gn, s));
     int gv = -1;
-    hipError_t e = dvh::launch_pdhg(b, w, ch, o, g[3], g[4], g[5], cs[c], &gv, gl, g[0]);
+    hipError_t e = dvh::launch_pdhg(b, w, ch, o, gm[0], gm[1], gm[2], s, &gv, gl, gn);
     if (e == hipErrorInvalidValue)
       return fail(h, DVH_ERR_UNSUPPORTED, "window too large for the on-chip PDHG kernels (n or m > 4096)");
     if (e != hipSuccess) return hip_fail(h, e, "launch_pdhg");
-    h->n_generic += g[0];
+    h->n_generic += gn;
     if (variant < 0) variant = gv;
   }
-  DVH_HIP(h, join());  // everything on the second stream is ordered before the solve's stream goes on
   h->last_variant = variant;
   return DVH_OK;
 }

@@ -79,6 +79,8 @@ def main():
         out["groups"][name] = {"windows": n, "sha256": h.hexdigest()[:32],
                                "optimal": int((ist[k:k + n, 0] == 0).sum())}
         k += n
+    del dev
+    s.close()  # release the handle before interpreter teardown (the profiler's exit hooks run after it)
     line = json.dumps(out)
     print(line, flush=True)
     if len(sys.argv) > 1:

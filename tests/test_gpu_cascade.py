@@ -37,8 +37,8 @@ def test_mixed_batch_takes_every_tier_with_one_wait_per_tier(gpu_solver):
     res = gpu_solver.solve(lps)
     ks = gpu_solver.kernel_stats()
     assert ks["band_windows"] == n["config4"] + n["config5"], ks
-    # the market days and the POI windows are few (<= two per CU): both run on the one-window-per-CU generic kernel,
-    # in their own size classes (concurrently, on two streams)
+    # the market days and the POI windows are few (<= two per CU): both size classes end on the one-window-per-CU
+    # generic kernel (the POI windows fit no ELL instantiation), in one launch
     assert ks["ell_windows"] == 0 and ks["generic_windows"] == n["market"] + n["poi"], ks
     assert ks["chain_windows"] == n["annual"] and ks["large_windows"] == 0, ks
     # band pass + ICE pass + ELL pass read-backs, the medium tier's plan / setup / team hand-offs, the final wait
