@@ -155,6 +155,9 @@ def main():
     ap.add_argument("--kkt-predict", type=int, default=4,
                     help="dvh_options.kkt_predict for cold solves (--schedule cold and the cold reference; the seeded "
                          "schedule's phases use sweep.SEED_OPTIONS / WARM_OPTIONS); 0 = every due KKT check runs")
+    ap.add_argument("--overlap-gather", type=int, default=1,
+                    help="N > 1: 1 = a step's result all-gather travels while the next step solves (one in flight; "
+                         "the last one completes inside the timed region), 0 = gather then the next solve")
     ap.add_argument("--series", choices=("device", "host"), default="device",
                     help="with --build device: the scenarios' series generated on the GPU (lp/gpu_series.py) or by "
                          "numpy on the host (bit-identical)")
@@ -248,8 +251,10 @@ def main():
         tg = sweep.tags if sweep is not None else [t for s_ in specs_tags for t in s_]
         tags_dev = torch.as_tensor(parallel.tag_array(tg), device=f"cuda:{local}")
 
+    pending = None  # the previous step's all-gather, still in flight (--overlap-gather)
+
     def step():
-        nonlocal gathered
+        nonlocal gathered, pending
         if sweep is not None:
             phase["timing"], phase["paths"] = sweep.solve(solver, dev)
         else:
@@ -260,17 +265,36 @@ def main():
             torch.cuda.synchronize()
             tg = time.perf_counter()
             rows = parallel.result_rows(dev.stats, dev.istats, dev.x, desc, tmax, runs, tags=tags_dev)
-            gathered = parallel.gather_rows(rows, counts=[count] * world)
-            torch.cuda.synchronize()
+            if args.overlap_gather:
+                # the rows are a copy: once it is made, the next step's solve may overwrite the batch's outputs
+                # while RCCL carries this step's rows over xGMI (at most one gather in flight)
+                torch.cuda.current_stream().synchronize()
+                tw = time.perf_counter()
+                if pending is not None:
+                    gathered = pending.wait()
+                gather.update(wait_ms=round(1e3 * (time.perf_counter() - tw), 2))
+                pending = parallel.gather_rows(rows, counts=[count] * world, async_op=True)
+            else:
+                gathered = parallel.gather_rows(rows, counts=[count] * world)
+                torch.cuda.synchronize()
             gather.update(ms=round(1e3 * (time.perf_counter() - tg), 2), bytes_per_rank=int(rows.numel() * 8),
-                          bytes_total=int(gathered.numel() * 8), cols=int(rows.shape[1]), tmax=int(tmax))
+                          bytes_total=int(rows.numel() * 8 * world), cols=int(rows.shape[1]), tmax=int(tmax),
+                          overlapped=bool(args.overlap_gather))
+
+    def drain():
+        nonlocal gathered, pending
+        if pending is not None:
+            gathered = pending.wait()
+            pending = None
 
     for _ in range(args.warmup):
         step()
+    drain()
     barrier()
     t = time.perf_counter()
     for _ in range(args.steps):
         step()
+    drain()  # the last step's rows have arrived on every rank inside the timed region
     barrier()
     el = time.perf_counter() - t
     if dist is not None:

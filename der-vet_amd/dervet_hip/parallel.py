@@ -111,13 +111,38 @@ def result_rows(stats, istats, x=None, desc=None, tmax=None, runs=None, tags=Non
     return rows
 
 
-def gather_rows(rows, group=None, counts=None):
+class PendingGather:
+    """An all-gather in flight (``gather_rows(..., async_op=True)``): ``wait()`` returns the gathered rows.  The
+    rows tensor it reads stays referenced until then."""
+
+    def __init__(self, work, out, rows):
+        self._work, self._out, self._rows = work, out, rows
+
+    def wait(self):
+        self._work.wait()
+        self._rows = None
+        return self._out
+
+
+def gather_rows(rows, group=None, counts=None, async_op=False):
     """All-gather a [k_r, w] float64 tensor of per-window result rows from every rank; returns the concatenation in
     rank order (identical on every rank).  counts: every rank's k_r when known on all ranks (weak scaling, a
-    deterministic shard): then the rows go out in ONE all-gather; otherwise the counts are exchanged first."""
+    deterministic shard): then the rows go out in ONE all-gather; otherwise the counts are exchanged first.
+    async_op (equal counts only): start the all-gather and return a ``PendingGather`` at once, so the caller can
+    solve the next batch while the rows travel (RCCL runs on its own stream)."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
+    if async_op:
+        if counts is None or any(n != rows.shape[0] for n in counts):
+            raise ValueError("an asynchronous gather needs every rank's count, all equal to this rank's")
+        pad = rows.contiguous()
+        out = torch.empty((world * pad.shape[0], pad.shape[1]), dtype=pad.dtype, device=pad.device)
+        if hasattr(dist, "all_gather_into_tensor") and dist.get_backend(group) != "gloo":
+            work = dist.all_gather_into_tensor(out, pad, group=group, async_op=True)
+        else:
+            work = dist.all_gather(list(out.chunk(world)), pad, group=group, async_op=True)
+        return PendingGather(work, out, pad)
     if counts is None:
         k = torch.tensor([rows.shape[0]], dtype=torch.int64, device=rows.device)
         ks = [torch.zeros_like(k) for _ in range(world)]

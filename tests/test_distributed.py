@@ -136,3 +136,38 @@ def test_weighted_shard_balances_cost_and_covers_once():
     big[0, 0] = 315360
     big[0, 3] = 735840
     assert parallel.window_cost(big)[0] == pytest.approx(735840 / 5208)
+
+
+def _async_worker(rank, world, port, out):
+    """bench.py --overlap-gather: each step's rows start their all-gather at once (async_op) and are collected at the
+    next step, while that step's rows are being made; the last gather is drained before the end."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    got, pending = [], None
+    for step in range(3):
+        rows = torch.full((5, parallel.RESULT_COLS + 6), float(100 * step + rank), dtype=torch.float64)
+        rows[:, 0] = torch.arange(5, dtype=torch.float64) + 10 * rank
+        if pending is not None:
+            got.append(pending.wait())
+        pending = parallel.gather_rows(rows, counts=[5] * world, async_op=True)
+        del rows  # the pending gather keeps its input alive
+    got.append(pending.wait())
+    if rank == 0:
+        torch.save(torch.stack(got), out)
+    with pytest.raises(ValueError):
+        parallel.gather_rows(torch.zeros((4, 3), dtype=torch.float64), counts=[4, 5], async_op=True)
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_two_rank_async_gather_overlapping_the_next_step(tmp_path):
+    out = str(tmp_path / "a.pt")
+    mp.spawn(_async_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    g = torch.load(out, weights_only=True)
+    assert g.shape == (3, 10, parallel.RESULT_COLS + 6)
+    for step in range(3):
+        assert torch.equal(g[step, :5, 1], torch.full((5,), 100.0 * step, dtype=torch.float64))
+        assert torch.equal(g[step, 5:, 1], torch.full((5,), 100.0 * step + 1, dtype=torch.float64))
+        assert torch.equal(g[step, :, 0], torch.cat([torch.arange(5.0), torch.arange(5.0) + 10]).double())
