@@ -164,6 +164,12 @@ def main():
                                         scenarios.template_battery(), da_price=ri["fivemin_da_price"][None, :],
                                         tariff_def=scenarios.tariff(), n="year")
         run("config3+dcm", "5-min annual window, DA + retailETS + 12 monthly DCM charges", P(g), s, args.reps, 0, 1)
+        # BASELINE config 3 as stated ("battery + PV year"): + the template's fixed PV, grid_charge 0 (scenarios.config3,
+        # the HiGHS golden of tests/test_gpu_config3.py)
+        run("config3+dcm+pv", "5-min annual window, DA + retailETS + 12 monthly DCM charges, site load less the template's "
+            "fixed PV (grid_charge 0)", P(scenarios.config3("dcm")), s, args.reps, 0, 1)
+        stitched(scenarios.config3("dcm")[0], scenarios.config3("dcm", n=288), s, args.reps, name="config3+dcm+pv",
+                 note="5-min annual window, DA + retailETS + 12 monthly DCM + fixed PV, started from its daily windows")
         for sub in (288,):  # measured: slower than cold for this variant; monthly subs: 2.9 s
             stitched(g[0], scenarios.windows_by_period(2019, 1.0 / 12, ri["fivemin_site_load"][None, :], None,
                                                        scenarios.template_battery(),
