@@ -58,7 +58,7 @@ struct dvh_handle {
   DevBuf d_desc, d_indptr, d_indices, d_data, d_c, d_c0, d_q, d_l, d_u, d_x, d_y, d_stats, d_istats;
   // workspace
   DevBuf w_tptr, w_tind, w_tval, w_kval, w_rowof, w_perm, w_dr, w_dc, w_cs, w_ls, w_us, w_qs, w_vbuf, w_wbuf,
-      w_tmpc, w_tmpr, w_longk, w_longt, w_scal;
+      w_tmpc, w_tmpr, w_longk, w_longt, w_scal, w_fc, w_fr;
   DevBuf d_list, d_hinv;
   DevBuf m_list, m_plan, m_pos, m_xbuf, m_abort;  // medium tier (dvh_chain.hip)
   int chain_cap = -1;                             // resident 768-thread workgroups (cooperative limit)
@@ -234,6 +234,7 @@ int dvh_destroy(dvh_handle* h) {
                     &h->d_u, &h->d_list, &h->d_hinv, &h->d_x, &h->d_y, &h->d_stats, &h->d_istats, &h->w_tptr, &h->w_tind, &h->w_tval,
                     &h->w_kval, &h->w_rowof, &h->w_perm, &h->w_dr, &h->w_dc, &h->w_cs, &h->w_ls, &h->w_us,
                     &h->w_qs, &h->w_vbuf, &h->w_wbuf, &h->w_tmpc, &h->w_tmpr, &h->w_longk, &h->w_longt, &h->w_scal,
+                    &h->w_fc, &h->w_fr,
                     &h->m_list, &h->m_plan, &h->m_pos, &h->m_xbuf, &h->m_abort, &h->o_data, &h->o_cases, &h->o_len, &h->o_hist, &h->o_soe,
                     &h->s_pairs, &h->s_bad, &h->g_seeds, &h->g_word, &h->d_route};
   for (DevBuf* b : bufs) b->release();
@@ -945,11 +946,14 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
   DVH_HIP(h, h->w_longk.ensure(I * (size_t)wc * dvh::kLMax));
   DVH_HIP(h, h->w_longt.ensure(I * (size_t)wc * dvh::kLMax));
   DVH_HIP(h, h->w_scal.ensure(D * (size_t)wc * dvh::kScal));
+  DVH_HIP(h, h->w_fc.ensure(sizeof(float) * wn));
+  DVH_HIP(h, h->w_fr.ensure(sizeof(float) * wm));
   dvh::Work w{h->w_tptr.as<int32_t>(), h->w_tind.as<int32_t>(), h->w_tval.as<double>(), h->w_kval.as<double>(),
               h->w_rowof.as<int32_t>(), h->w_perm.as<int32_t>(), h->w_dr.as<double>(), h->w_dc.as<double>(),
               h->w_cs.as<double>(), h->w_ls.as<double>(), h->w_us.as<double>(), h->w_qs.as<double>(),
               h->w_vbuf.as<double>(), h->w_wbuf.as<double>(), h->w_tmpc.as<double>(), h->w_tmpr.as<double>(),
-              h->w_longk.as<int32_t>(), h->w_longt.as<int32_t>(), h->d_hinv.as<double>(), h->w_scal.as<double>()};
+              h->w_longk.as<int32_t>(), h->w_longt.as<int32_t>(), h->d_hinv.as<double>(), h->w_scal.as<double>(),
+              h->w_fc.as<float>(), h->w_fr.as<float>()};
   DVH_HIP(h, h->d_list.ensure(I * 4 * (size_t)wc));  // the cascade's four device lists (dvh_route.hip)
   DVH_HIP(h, h->d_route.ensure(I * 8 * 5));
   if (!h->route_host) DVH_HIP(h, hipHostMalloc((void**)&h->route_host, I * 8 * 5, hipHostMallocDefault));

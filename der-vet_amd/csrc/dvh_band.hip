@@ -61,23 +61,28 @@ __host__ __device__ inline size_t band_lds_bytes(int B, int S, bool ice, int LF)
 }
 
 // KKT pieces of one column / one row (out of line: the KKT check runs every 128 iterations, and inlined it
-// would raise the whole kernel's register allocation).  d / dr: the column / row scaling, id / idr: their
-// reciprocals from the setup kernel (the unscaling is a multiplication, not a division)
+// would raise the whole kernel's register allocation).  Scale-free where the check compares large terms: the
+// objectives' sums c'x, q'y and the bound term l'lam+ + u'lam- are the same in the scaled space (c~ x~ = c x,
+// l~ lam~ = (l / d)(d lam) with lam~ = c~ - K~'y~ the scaled reduced cost, d > 0 keeping its sign), so the gap needs
+// no factor at all.  Only the residual norms and ||y|| are unscaled, with fd = the factor in single precision
+// (Work::fc / fr) and a 1-ulp v_rcp_f32 reciprocal: each term moves by a relative 2e-7 at most, i.e. each norm by a
+// relative 2e-7 of itself.  The outputs are unscaled with the exact factors.
 struct ColKkt {
   double rd2, cx, bt;
 };
-__device__ __noinline__ ColKkt col_kkt_fn(double kt, double cj, double loj, double hij, double xj, double d,
-                                          double id) {
-  const double rc = (cj - kt) * id;
+__device__ __noinline__ ColKkt col_kkt_fn(double kt, double cj, double loj, double hij, double xj, float fd) {
+  const double id = (double)__builtin_amdgcn_rcpf(fd);
+  const double rs = cj - kt;  // scaled reduced cost
   const bool fl = isfinite(loj), fh = isfinite(hij);
-  const double lam = (fl && fh) ? rc : (fl ? fmax(rc, 0.0) : (fh ? fmin(rc, 0.0) : 0.0));
-  const double rd = rc - lam;
-  return {rd * rd, cj * xj, (fl ? loj * d * fmax(lam, 0.0) : 0.0) + (fh ? hij * d * fmin(lam, 0.0) : 0.0)};
+  const double lam = (fl && fh) ? rs : (fl ? fmax(rs, 0.0) : (fh ? fmin(rs, 0.0) : 0.0));
+  const double rd = (rs - lam) * id;
+  return {rd * rd, cj * xj, (fl ? loj * fmax(lam, 0.0) : 0.0) + (fh ? hij * fmin(lam, 0.0) : 0.0)};
 }
 struct RowKkt {
   double rp2, y2;
 };
-__device__ __noinline__ RowKkt row_kkt_fn(double kv, double qi, double yi, double dr, double idr, int ge) {
+__device__ __noinline__ RowKkt row_kkt_fn(double kv, double qi, double yi, float fd, int ge) {
+  const double dr = (double)fd, idr = (double)__builtin_amdgcn_rcpf(fd);
   double r = (qi - kv) * idr;
   if (ge) r = fmax(r, 0.0);
   return {r * r, (yi * dr) * (yi * dr)};
@@ -800,14 +805,14 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
       lds_barrier();
       auto col_kkt = [&](int j, double kt, double cj, double loj, double hij, double xj) {
         const int jj = opaque(j);
-        const ColKkt r = col_kkt_fn(kt, cj, loj, hij, xj, dcv[jj], w.tmpc[W.wn + jj]);
+        const ColKkt r = col_kkt_fn(kt, cj, loj, hij, xj, w.fc[W.wn + jj]);
         acc[5] += r.rd2;
         acc[6] += r.cx;
         acc[8] += r.bt;
       };
       auto row_kkt = [&](int i, double kv, double qi, double yi, bool ge) {
         const int ii = opaque(i);
-        const RowKkt r = row_kkt_fn(kv, qi, yi, drv[ii], w.tmpr[W.wm + ii], ge);
+        const RowKkt r = row_kkt_fn(kv, qi, yi, w.fr[W.wm + ii], ge);
         acc[4] += r.rp2;
         acc[7] += qi * yi;
         acc[9] += r.y2;

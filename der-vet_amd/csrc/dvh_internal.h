@@ -87,6 +87,8 @@ struct Work {
   const double* hinv;  // [kHalpernTab] 1 / (k + 2), k = 0.. (Halpern anchor weights, exact IEEE quotients)
   double* scal;     // [count * kScal]  eta, w0, ||c||, ||q||, nlong(K), nlong(K^T), flag, ||K||,
                     //   max short row len K, K^T (<= 8), #rows > 8 in K, K^T
+  float* fc;        // [sum n]  Dc rounded to single precision (the band kernel's KKT checks)
+  float* fr;        // [sum m]  Dr rounded to single precision
 };
 
 struct Chunk {

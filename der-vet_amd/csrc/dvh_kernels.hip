@@ -308,10 +308,10 @@ __global__ __launch_bounds__(kSetupB) void setup_kernel(const Batch b, const Wor
     nrm[1] += qi * d * qi * d;
     nrm[3] += qi * qi;
   }
-  // reciprocal scalings for the band kernel's KKT checks (multiplications instead of divisions); the same thread
-  // owns index j / i in the Ruiz update above, so these overwrite factors nobody reads any more
-  for (int j = tid; j < n; j += kSetupB) tmpc[j] = 1.0 / Dc[j];
-  for (int i = tid; i < m; i += kSetupB) tmpr[i] = 1.0 / Dr[i];
+  // single-precision copies of the scalings for the band kernel's KKT checks: a check reads 4 bytes per row and
+  // column instead of Dc, Dr and their reciprocals (32), which with 64 windows per XCD do not stay in L2
+  for (int j = tid; j < n; j += kSetupB) w.fc[W.wn + j] = (float)Dc[j];
+  for (int i = tid; i < m; i += kSetupB) w.fr[W.wm + i] = (float)Dr[i];
   if (!MED) {
     for (int j = tid; j < n; j += kSetupB) gDc[j] = Dc[j];
     for (int i = tid; i < m; i += kSetupB) gDr[i] = Dr[i];
