@@ -743,14 +743,15 @@ static int chain_pass(dvh_handle* h, const dvh::Batch& b, const dvh::Work& w, co
 
 // Solve a packed device batch given a host copy of its descriptors.
 // The default kernel cascade over one chunk's small windows, its lists formed on the device (dvh_route.hip): the
-// battery-banded kernel over the chunk -> its refusals (status -2) through the band-ICE form -> what that refuses
+// battery-banded kernel over the chunk, scaling the windows it takes itself (no setup_kernel for them) -> its
+// refusals (status -2) set up (setup_kernel over the list) and through the band-ICE form -> what that refuses
 // through the ELL kernels, in two size classes (the small market-day kernels' shapes, n <= 512 and m <= 768, and the
 // rest), each instantiation sized for its class -> what they refuse (-1) or cannot hold through the generic CSR
 // kernel, both classes in one launch.
 // One small read-back per stage that ran ({count, ELL widths, max n / m / nnz} of the windows it hands on); a batch
 // the band kernel takes whole waits once.
 static int device_cascade(dvh_handle* h, const dvh::Batch& b, const dvh::Work& w, const dvh::Chunk& ch,
-                          const dvh::Opts& o, int nsmall, int wc, hipStream_t s) {
+                          const dvh::Opts& o, int nsmall, int wc, int mn, int mm, hipStream_t s) {
   const size_t I = sizeof(int32_t);
   int32_t* L[4];
   for (int r = 0; r < 4; ++r) L[r] = h->d_list.as<int32_t>() + (size_t)r * wc;
@@ -779,6 +780,8 @@ static int device_cascade(dvh_handle* h, const dvh::Batch& b, const dvh::Work& w
   h->n_band += nsmall - cur;
   if (nsmall - cur > 0) variant = bvar;
   if (cur > 0) {  // pass 2: the band kernel's ICE form over pass 1's refusals, which it hands on by size class
+    // (set up first: the ELL / generic kernels and the route statistics read setup_kernel's outputs)
+    DVH_HIP(h, dvh::launch_setup(b, w, ch, o, mn, mm, s, L[0], cur));
     DVH_HIP(h, dvh::launch_pdhg_band(b, w, ch, o, s, true, form_for(cur), L[0], cur, &bvar));
     DVH_HIP(h, route(1, L[0], cur, -2, 1, 2));
     DVH_HIP(h, route(2, L[0], cur, -2, 2, 3));
@@ -980,17 +983,19 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
     const hipEvent_t e0 = h->chunk_events[h->chunk_used][0], e1 = h->chunk_events[h->chunk_used][1],
                      e2 = h->chunk_events[h->chunk_used][2];
     ++h->chunk_used;
+    const bool fast = h->kernel_path != 1 && o.rho == 1.0;
+    const bool cascade = fast && (h->kernel_path == 0 || h->kernel_path >= 3);
     DVH_HIP(h, hipEventRecord(e0, s));
-    if (c.nsmall > 0) DVH_HIP(h, dvh::launch_setup(b, w, c.ch, o, c.mn, c.mm, s));
+    // (the device cascade sets up only what the band kernel refuses, inside device_cascade)
+    if (c.nsmall > 0 && !cascade) DVH_HIP(h, dvh::launch_setup(b, w, c.ch, o, c.mn, c.mm, s));
     DVH_HIP(h, hipEventRecord(e1, s));
     if (c.nsmall == 0) {
       if (int rc = chain_pass(h, b, w, c.ch, o, c.med, c.med_T, desc, med_done, s)) return rc;
       DVH_HIP(h, hipEventRecord(e2, s));
       continue;
     }
-    const bool fast = h->kernel_path != 1 && o.rho == 1.0;
-    if (fast && (h->kernel_path == 0 || h->kernel_path >= 3)) {
-      if (int rc = device_cascade(h, b, w, c.ch, o, c.nsmall, wc, s)) return rc;
+    if (cascade) {
+      if (int rc = device_cascade(h, b, w, c.ch, o, c.nsmall, wc, c.mn, c.mm, s)) return rc;
       if (int rc = chain_pass(h, b, w, c.ch, o, c.med, c.med_T, desc, med_done, s)) return rc;
       DVH_HIP(h, hipEventRecord(e2, s));
       continue;

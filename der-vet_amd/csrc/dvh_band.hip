@@ -104,7 +104,7 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
   const WinOff W = win_offsets(b, ch, k);
   const int n = W.n, m = W.m, meq = W.meq;
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const double* scal = w.scal + (int64_t)kl * kScal;
+  double* scal = w.scal + (int64_t)kl * kScal;
   const int T = meq - 1, J = n - (ICE ? 5 : 3) * T, MI = m - meq;
   const int MD = ICE ? MI - 2 * T : MI;  // DCM rows
   auto bail = [&]() {
@@ -113,8 +113,10 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
       b.istats[2 * k + 1] = 0;
     }
   };
-  if (scal[6] == 3.0) return;  // reported infeasible by the setup kernel
-  if (scal[6] != 0.0 || T < 1 || T > SB || J < 0 || J > kJMax || MD < 0 || MD > T || (J == 0 && MD > 0)) {
+  // the kernel scales its windows itself (below): it runs before, and instead of, setup_kernel, whose outputs it
+  // does not read; the windows it hands on are set up after it (dvh_api.cpp device_cascade)
+  if (n > kSmallMax || m > kSmallMax || T < 1 || T > SB || J < 0 || J > kJMax || MD < 0 || MD > T ||
+      (J == 0 && MD > 0)) {
     bail();
     return;
   }
@@ -147,13 +149,13 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
 
   const int32_t* gkp = b.indptr + W.row;
   const int32_t* gkc = b.indices + W.nz;
-  const double* gkv = w.kval + W.wz;
-  const double* cs = w.cs + W.wn;
-  const double* ls = w.ls + W.wn;
-  const double* us = w.us + W.wn;
-  const double* qs = w.qs + W.wm;
-  const double* dcv = w.dc + W.wn;
-  const double* drv = w.dr + W.wm;
+  const double* gkv = b.data + W.nz;  // the window's own (unscaled) data
+  const double* craw = b.c + W.on;
+  const double* lraw = b.l + W.on;
+  const double* uraw = b.u + W.on;
+  const double* qraw = b.q + W.om;
+  double* dcv = w.dc + W.wn;  // the factors this kernel computes (outputs are unscaled with them)
+  double* drv = w.dr + W.wm;
   double* xo_g = b.x + W.on;
   double* yo_g = b.y + W.om;
 
@@ -164,9 +166,10 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
     ice_b[u] = -1;
     ice_n[u] = 0;
   }
-  if (tid == 0) flag[0] = 0;
+  if (tid == 0) flag[0] = flag[1] = 0;
   __syncthreads();
-  int bad = 0;
+  int bad = 0, crossed = 0;
+  for (int j = tid; j < J; j += B) crossed |= lraw[3 * T + j] > uraw[3 * T + j];
   for (int r = tid; r <= T; r += B) {
     const int p0 = gkp[r], len = gkp[r + 1] - p0;
     if (r == 0) {
@@ -185,9 +188,13 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
       if (kind == 4 || ((seen >> kind) & 1u)) bad = 1;
       seen |= 1u << kind;
     }
-    // the kernel keeps no lower bound for ch / dis (/ elec / on)
-    bad |= ls[t] != 0.0 || ls[T + t] != 0.0;
-    if (ICE) bad |= ls[CE + t] != 0.0 || ls[CO + t] != 0.0;
+    // the kernel keeps no lower bound for ch / dis (/ elec / on); crossed bounds: infeasible as given
+    bad |= lraw[t] != 0.0 || lraw[T + t] != 0.0;
+    crossed |= lraw[t] > uraw[t] || lraw[T + t] > uraw[T + t] || lraw[2 * T + t] > uraw[2 * T + t];
+    if (ICE) {
+      bad |= lraw[CE + t] != 0.0 || lraw[CO + t] != 0.0;
+      crossed |= lraw[CE + t] > uraw[CE + t] || lraw[CO + t] > uraw[CO + t];
+    }
   }
   for (int i = meq + tid; i < m; i += B) {
     const int p0 = gkp[i], len = gkp[i + 1] - p0;
@@ -237,11 +244,22 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
     if (atomicCAS(&dcm[tc], -1, i * 8 + jj) != -1) bad = 1;  // at most one DCM row per step
   }
   if (bad) flag[0] = 1;
+  if (crossed) flag[1] = 1;
   __syncthreads();
   if (ICE)
     for (int u = tid; u < T; u += B)
       if (ice_n[u] != 2) flag[0] = 1;  // exactly two ICE rows per step
   __syncthreads();
+  if (flag[1] != 0) {  // crossed bounds, reported as setup_kernel reports them (no iterations)
+    if (tid == 0) {
+      scal[0] = 0.0;
+      scal[6] = 3.0;
+      b.istats[2 * k] = 1;  // DVH_PRIMAL_INFEASIBLE
+      b.istats[2 * k + 1] = 0;
+      for (int u = 0; u < 4; ++u) b.stats[4 * k + u] = u == 0 ? NAN : 0.0;
+    }
+    return;
+  }
   if (flag[0] != 0) {
     bail();
     return;
@@ -289,26 +307,11 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
   auto qv = [&](int s, int r) -> double { return LC ? cqa(3 + r, s) : q[s][r]; };
   auto hib = [&](int s, int v) -> double { return v < 3 ? hi[s][v] : ro(v - 1, s); };
   auto rhs = [&](int s, int r) -> double { return r < 2 ? qv(s, r) : ro(r + 2, s); };
+  // ---- the lane's coefficients (unscaled) and row maps
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     if (!val[s]) continue;
     const int t = t0 + s;
-#pragma unroll
-    for (int v = 0; v < NC; ++v) {
-      const int j = col(s, v);
-      if (v < 3) {
-        hi[s][v] = us[j];
-        if (LC)
-          cqa(v, s) = cs[j];
-        else
-          cc[s][v] = cs[j];
-      } else {
-        ro(v - 1, s) = us[j];
-        ro(v - 3, s) = cs[j];
-      }
-      x[s][v] = xa[s][v] = fmin(fmax(0.0, ls[j]), us[j]);
-    }
-    loe[s] = ls[2 * T + t];
     for (int p = gkp[t + 1]; p < gkp[t + 2]; ++p) {
       const int c = gkc[p];
       const double a = gkv[p];
@@ -320,10 +323,6 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
     if (s == 0)
       for (int p = gkp[t]; p < gkp[t + 1]; ++p)
         if (gkc[p] == 2 * T + t) kp0 = gkv[p];
-    if (LC)
-      cqa(3, s) = qs[t + 1];
-    else
-      q[s][0] = qs[t + 1];
     const int dv = dcm[t];
     if (dv >= 0) {
       drow[s] = dv >> 3;
@@ -336,36 +335,14 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
         else if (c < 3 * T + J) kd[s][2] = a;
         else kd[s][3] = a;
       }
-      if (LC)
-        cqa(4, s) = qs[drow[s]];
-      else
-        q[s][1] = qs[drow[s]];
     }
     if (ICE) {
       ra[s] = ice_a[t];
       rb[s] = ice_b[t];
       for (int p = gkp[ra[s]]; p < gkp[ra[s] + 1]; ++p) (gkc[p] < CO ? ka[s][0] : ka[s][1]) = gkv[p];
       for (int p = gkp[rb[s]]; p < gkp[rb[s] + 1]; ++p) (gkc[p] < CO ? kb[s][0] : kb[s][1]) = gkv[p];
-      ro(4, s) = qs[ra[s]];
-      ro(5, s) = qs[rb[s]];
-    }
-    if (o.warm) {  // warm start from the unscaled x / y in the output buffers
-#pragma unroll
-      for (int v = 0; v < NC; ++v) {
-        const int j = col(s, v);
-        x[s][v] = xa[s][v] = fmin(fmax(xo_g[j] / dcv[j], ls[j]), us[j]);
-      }
-      y[s][0] = ya[s][0] = yo_g[t + 1] / drv[t + 1];
-      if (drow[s] >= 0) y[s][1] = ya[s][1] = fmax(yo_g[drow[s]] / drv[drow[s]], 0.0);
-      if (ICE) {
-        y[s][2] = ya[s][2] = fmax(yo_g[ra[s]] / drv[ra[s]], 0.0);
-        y[s][3] = ya[s][3] = fmax(yo_g[rb[s]] / drv[rb[s]], 0.0);
-      }
     }
   }
-  int xta[S];
-#pragma unroll
-  for (int s = 0; s < S; ++s) xta[s] = lds_addr(XT + jt[s]);
   // row of step s's r-th row (SOE, DCM, ICE a, ICE b), or -1 where the step has none
   auto row_of = [&](int s, int r) -> int {
     return r == 0 ? (val[s] ? t0 + s + 1 : -1) : r == 1 ? drow[s] : (val[s] ? (r == 2 ? ra[s] : rb[s]) : -1);
@@ -376,21 +353,203 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
   static_assert(kJMax < kInitLane, "tau lanes and the init-row lane are distinct");
   const bool tlane = wid == 0 && lane < J, ilane = wid == 0 && lane == kInitLane;
   double sp[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+
+  // ---- scaling: setup_kernel's preconditioning (o.ruiz_iters Ruiz inf-norm passes, then one Pock-Chambolle
+  //      alpha = 1 pass, row and column factors of a pass both from the same scaled matrix) restated on the band
+  //      structure, every factor in the registers of the lane that owns the row / column: a row's entries are its
+  //      step's columns (+ the next step's ene: the next lane's, through XE; + its period's tau: XT), a column's
+  //      entries its step's rows (+ ene's previous SOE row: the previous lane's, through YS); the tau columns are
+  //      reduced through TP by wave 0, whose lane j holds tau j's factor (fsp), as lane kInitLane holds the init row's.
+  //      Factors 1 / sqrt(norm) by v_rsq_f64: a preconditioner needs no correctly rounded factor, and every scaled
+  //      quantity is formed from the same stored factor that unscales the results.
+  double fcv[S][NC], frv[S][NR], fsp = 1.0, kin0 = 0.0;  // kin0: the init row's coefficient (of ene_0)
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+#pragma unroll
+    for (int v = 0; v < NC; ++v) fcv[s][v] = 1.0;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) frv[s][r] = 1.0;
+  }
+  if (ilane) kin0 = gkv[gkp[0]];
+  auto factor = [](double a) { return a > 0.0 ? __builtin_amdgcn_rsq(a) : 1.0; };
+  auto exchange = [&]() {
+    XE[tid] = fcv[0][2];
+    YS[tid + 1] = frv[S - 1][0];
+    if (tid == 0) XE[B] = 1.0;  // (no step after the last lane's: its coefficient is 0)
+    if (tid < kJMax) XT[tid] = tlane ? fsp : 1.0;
+    if (ilane) YS[0] = fsp;
+  };
+  for (int pass = 0; pass <= o.ruiz_iters; ++pass) {
+    const bool pc = pass == o.ruiz_iters;
+    auto acc = [pc](double a, double v) { return pc ? a + v : fmax(a, v); };
+    exchange();
+    __syncthreads();
+    const double fen = XE[tid + 1], frp = YS[tid];
+    double nr[S][NR], nc[S][NC];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const double fe1 = s < S - 1 ? fcv[s < S - 1 ? s + 1 : s][2] : fen;
+      const double rp = s == 0 ? frp : frv[s > 0 ? s - 1 : 0][0];
+      const double kpr = s == 0 ? kp0 : ks[s > 0 ? s - 1 : 0][3];
+      const double r0 = frv[s][0], r1 = frv[s][1], ftj = XT[jt[s]];
+      nr[s][0] = acc(acc(acc(fabs(ks[s][0]) * r0 * fcv[s][0], fabs(ks[s][1]) * r0 * fcv[s][1]),
+                         fabs(ks[s][2]) * r0 * fcv[s][2]),
+                     fabs(ks[s][3]) * r0 * fe1);
+      nr[s][1] = acc(acc(fabs(kd[s][0]) * r1 * fcv[s][0], fabs(kd[s][1]) * r1 * fcv[s][1]), fabs(kd[s][2]) * r1 * ftj);
+      nc[s][0] = acc(fabs(ks[s][0]) * r0 * fcv[s][0], fabs(kd[s][0]) * r1 * fcv[s][0]);
+      nc[s][1] = acc(fabs(ks[s][1]) * r0 * fcv[s][1], fabs(kd[s][1]) * r1 * fcv[s][1]);
+      nc[s][2] = acc(fabs(kpr) * rp * fcv[s][2], fabs(ks[s][2]) * r0 * fcv[s][2]);
+      if constexpr (ICE) {
+        const double r2 = frv[s][NR > 2 ? 2 : 0], r3 = frv[s][NR > 3 ? 3 : 0];
+        const double f3 = fcv[s][NC > 3 ? 3 : 0], f4 = fcv[s][NC > 4 ? 4 : 0];
+        nr[s][1] = acc(nr[s][1], fabs(kd[s][3]) * r1 * f3);
+        nr[s][NR > 2 ? 2 : 0] = acc(fabs(ka[s][0]) * r2 * f3, fabs(ka[s][1]) * r2 * f4);
+        nr[s][NR > 3 ? 3 : 0] = acc(fabs(kb[s][0]) * r3 * f3, fabs(kb[s][1]) * r3 * f4);
+        nc[s][NC > 3 ? 3 : 0] = acc(acc(fabs(kd[s][3]) * r1 * f3, fabs(ka[s][0]) * r2 * f3), fabs(kb[s][0]) * r3 * f3);
+        nc[s][NC > 4 ? 4 : 0] = acc(fabs(ka[s][1]) * r2 * f4, fabs(kb[s][1]) * r3 * f4);
+      }
+    }
+    // tau columns: per-lane partials over the lane's DCM rows of each period (steps in order) -> wave 0
+    for (int j = 0; j < J; ++j) {
+      const double ftj = XT[j];
+      double a = 0.0;
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+        if (jt[s] == j) a = acc(a, fabs(kd[s][2]) * frv[s][1] * ftj);
+      TP[j * B + tid] = a;
+    }
+    double nsp = 0.0;
+    if (ilane) nsp = fabs(kin0) * fsp * XE[0];
+    __syncthreads();
+    if (wid == 0) {
+      for (int j = 0; j < J; ++j) {
+        double a = TP[j * B + lane];
+#pragma unroll
+        for (int r = 1; r < NW; ++r) a = acc(a, TP[j * B + r * kWave + lane]);
+        a = uniform(pc ? wave_sum_dpp(a) : wave_max(a));
+        if (lane == j) nsp = a;
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+#pragma unroll
+      for (int v = 0; v < NC; ++v) fcv[s][v] *= factor(nc[s][v]);
+#pragma unroll
+      for (int r = 0; r < NR; ++r) frv[s][r] *= factor(nr[s][r]);
+    }
+    if (tlane || ilane) fsp *= factor(nsp);
+    __syncthreads();  // every read of this pass's XE / YS / XT / TP is done
+  }
+  exchange();
+  __syncthreads();
+  {  // scaled coefficients (K Dr) Dc, as setup_kernel forms them
+    const double fen = XE[tid + 1], frp = YS[tid];
+    kp0 = kp0 * frp * fcv[0][2];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const double fe1 = s < S - 1 ? fcv[s < S - 1 ? s + 1 : s][2] : fen;
+      const double r0 = frv[s][0], r1 = frv[s][1];
+      ks[s][0] = ks[s][0] * r0 * fcv[s][0];
+      ks[s][1] = ks[s][1] * r0 * fcv[s][1];
+      ks[s][2] = ks[s][2] * r0 * fcv[s][2];
+      ks[s][3] = ks[s][3] * r0 * fe1;
+      kd[s][0] = kd[s][0] * r1 * fcv[s][0];
+      kd[s][1] = kd[s][1] * r1 * fcv[s][1];
+      kd[s][2] = kd[s][2] * r1 * XT[jt[s]];
+      if constexpr (ICE) {
+        const double r2 = frv[s][NR > 2 ? 2 : 0], r3 = frv[s][NR > 3 ? 3 : 0];
+        const double f3 = fcv[s][NC > 3 ? 3 : 0], f4 = fcv[s][NC > 4 ? 4 : 0];
+        kd[s][3] = kd[s][3] * r1 * f3;
+        ka[s][0] = ka[s][0] * r2 * f3;
+        ka[s][1] = ka[s][1] * r2 * f4;
+        kb[s][0] = kb[s][0] * r3 * f3;
+        kb[s][1] = kb[s][1] * r3 * f4;
+      }
+    }
+    if (ilane) kin0 = kin0 * fsp * XE[0];
+  }
+  // ---- costs, bounds and right-hand sides, scaled (c Dc, l / Dc, u / Dc, q Dr); the factors for the outputs and
+  //      the KKT checks; the norms for the primal weight and the relative KKT error
+  double nrm[4] = {0.0, 0.0, 0.0, 0.0};  // ||c~||^2, ||q~||^2, ||c||^2, ||q||^2
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    if (!val[s]) continue;
+    const int t = t0 + s;
+#pragma unroll
+    for (int v = 0; v < NC; ++v) {
+      const int j = col(s, v);
+      const double d = fcv[s][v], cj = craw[j];
+      const double csj = cj * d, lsj = lraw[j] / d, usj = uraw[j] / d;
+      if (v < 3) {
+        hi[s][v] = usj;
+        if (LC)
+          cqa(v, s) = csj;
+        else
+          cc[s][v] = csj;
+      } else {
+        ro(v - 1, s) = usj;
+        ro(v - 3, s) = csj;
+      }
+      if (v == 2) loe[s] = lsj;
+      x[s][v] = xa[s][v] = fmin(fmax(o.warm ? xo_g[j] / d : 0.0, lsj), usj);
+      nrm[0] += csj * csj;
+      nrm[2] += cj * cj;
+      dcv[j] = d;
+      w.fc[W.wn + j] = (float)d;
+    }
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const int i = row_of(s, r);
+      if (i < 0) continue;
+      const double d = frv[s][r], qi = qraw[i], qsi = qi * d;
+      if (r == 0) {
+        if (LC)
+          cqa(3, s) = qsi;
+        else
+          q[s][0] = qsi;
+      } else if (r == 1) {
+        if (LC)
+          cqa(4, s) = qsi;
+        else
+          q[s][1] = qsi;
+      } else {
+        ro(r + 2, s) = qsi;
+      }
+      if (o.warm) y[s][r] = ya[s][r] = r == 0 ? yo_g[i] / d : fmax(yo_g[i] / d, 0.0);
+      nrm[1] += qsi * qsi;
+      nrm[3] += qi * qi;
+      drv[i] = d;
+      w.fr[W.wm + i] = (float)d;
+    }
+  }
   if (tlane) {
-    const double l0 = ls[3 * T + lane], h0 = us[3 * T + lane];
-    sp[0] = sp[1] = sp[5] = fmin(fmax(0.0, l0), h0);
-    sp[2] = cs[3 * T + lane];
+    const int j = 3 * T + lane;
+    const double cj = craw[j], l0 = lraw[j] / fsp, h0 = uraw[j] / fsp;
+    sp[0] = sp[1] = sp[5] = fmin(fmax(o.warm ? xo_g[j] / fsp : 0.0, l0), h0);
+    sp[2] = cj * fsp;
     sp[3] = l0;
     sp[4] = h0;
+    nrm[0] += sp[2] * sp[2];
+    nrm[2] += cj * cj;
+    dcv[j] = fsp;
+    w.fc[W.wn + j] = (float)fsp;
   }
   if (ilane) {
-    sp[3] = qs[0];
-    sp[4] = gkv[gkp[0]];
+    const double q0 = qraw[0];
+    sp[3] = q0 * fsp;
+    sp[4] = kin0;
+    if (o.warm) sp[0] = sp[1] = sp[2] = yo_g[0] / fsp;
+    nrm[1] += sp[3] * sp[3];
+    nrm[3] += q0 * q0;
+    drv[0] = fsp;
+    w.fr[W.wm] = (float)fsp;
   }
-  if (o.warm) {
-    if (tlane) sp[0] = sp[1] = sp[5] = fmin(fmax(xo_g[3 * T + lane] / dcv[3 * T + lane], sp[3]), sp[4]);
-    if (ilane) sp[0] = sp[1] = sp[2] = yo_g[0] / drv[0];
-  }
+  block_sum<B, 4>(nrm, red);
+  const double ncs = sqrt(nrm[0]), nqs = sqrt(nrm[1]);
+  const double pw0 = (ncs > 1e-10 && nqs > 1e-10) ? ncs / nqs : 1.0;  // setup_kernel's primal weight
+  int xta[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) xta[s] = lds_addr(XT + jt[s]);
   if constexpr (IS) __syncthreads();  // anchors / images overwrite the step -> row maps: every lane has read them
   if constexpr (LA) {
 #pragma unroll
@@ -509,7 +668,7 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
   };
 
   // ---- ||Kt||_2 by power iteration (as the ELL kernel: v <- Kt'(Kt v), sigma^2 = |v_P| / |v_{P-1}|)
-  double eta = scal[0];
+  double eta = o.step_safety;  // Pock-Chambolle bound ||K~|| <= 1, refined by the power iteration
   if (o.power_iters > 0) {
     const int P = o.power_iters;
     const double v0 = 1.0 / sqrt((double)n);
@@ -573,8 +732,8 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
     __syncthreads();
   }
   eta = uniform(eta);
-  double pw = uniform(scal[1]);
-  const double cnorm = uniform(scal[2]), qnorm = uniform(scal[3]), c0 = uniform(b.c0[k]);
+  double pw = uniform(pw0);
+  const double cnorm = uniform(sqrt(nrm[2])), qnorm = uniform(sqrt(nrm[3])), c0 = uniform(b.c0[k]);
   int it = 0, kin = 0, status = kIterLimit;
   double r0 = -1.0, rprev = -1.0;
   double* fin = red + kNRed * NW;

@@ -98,8 +98,9 @@ struct Chunk {
 };
 
 // Launchers (dvh_kernels.hip).  Return hipError_t.
+// list (nlist entries): global window indices, or null for the whole chunk.
 hipError_t launch_setup(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n, int max_m,
-                        hipStream_t s);
+                        hipStream_t s, const int32_t* list = nullptr, int nlist = 0);
 // Solve kernel selection is made from the chunk maxima; returns hipErrorInvalidValue when no
 // instantiation covers the sizes (the caller reports DVH_ERR_UNSUPPORTED).
 // Generic (CSR) kernel; list = optional device list of window ids (nlist blocks) instead of the whole chunk.

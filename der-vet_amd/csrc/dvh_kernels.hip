@@ -79,7 +79,7 @@ __global__ __launch_bounds__(kSetupB) void setup_kernel(const Batch b, const Wor
   __shared__ double red[(kSetupB / kWave + 1) * 4];
   __shared__ int sh_cnt[2];
   __shared__ int sh_wt[kSetupB / kWave];
-  const int k = MED ? list[blockIdx.x] : ch.first + (int)blockIdx.x;
+  const int k = list ? list[blockIdx.x] : ch.first + (int)blockIdx.x;  // (MED: always listed)
   const int kl = k - ch.first;
   const WinOff W = win_offsets(b, ch, k);
   const int n = W.n, m = W.m, nnz = W.nnz;
@@ -1707,14 +1707,16 @@ size_t setup_lds_bytes(int max_n, int max_m) {
 }
 
 hipError_t launch_setup(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n, int max_m,
-                        hipStream_t s) {
+                        hipStream_t s, const int32_t* list, int nlist) {
   const size_t lds = setup_lds_bytes(max_n, max_m);
   Opts o2 = o;
   o2.setup_segments = setup_segments(max_n);
   hipError_t e = hipFuncSetAttribute((const void*)setup_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(setup_kernel<false>, dim3(ch.count), dim3(kSetupB), lds, s, b, w, ch, o2, (const int32_t*)nullptr);
+  const int nb = list ? nlist : ch.count;
+  if (nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(setup_kernel<false>, dim3(nb), dim3(kSetupB), lds, s, b, w, ch, o2, list);
   return hipGetLastError();
 }
 
