@@ -743,18 +743,19 @@ static int chain_pass(dvh_handle* h, const dvh::Batch& b, const dvh::Work& w, co
 
 // Solve a packed device batch given a host copy of its descriptors.
 // The default kernel cascade over one chunk's small windows, its lists formed on the device (dvh_route.hip): the
-// battery-banded kernel over the chunk, scaling the windows it takes itself (no setup_kernel for them) -> its
-// refusals (status -2) set up (setup_kernel over the list) and through the band-ICE form -> what that refuses
-// through the ELL kernels, in two size classes (the small market-day kernels' shapes, n <= 512 and m <= 768, and the
+// battery-banded kernel over the chunk -> its refusals (status -2) through the band-ICE form (both scale the windows
+// they take themselves: no setup_kernel for them) -> what that refuses, set up (setup_kernel over the list), through
+// the ELL kernels, in two size classes (the small market-day kernels' shapes, n <= 512 and m <= 768, and the
 // rest), each instantiation sized for its class -> what they refuse (-1) or cannot hold through the generic CSR
 // kernel, both classes in one launch.
-// One small read-back per stage that ran ({count, ELL widths, max n / m / nnz} of the windows it hands on); a batch
-// the band kernel takes whole waits once.
+// One small read-back per stage that ran ({count, ELL widths, max n / m / nnz} of the windows it hands on; two after
+// the ICE form when it refuses windows: their count, then their size classes once they are set up); a batch the band
+// kernel takes whole waits once.
 static int device_cascade(dvh_handle* h, const dvh::Batch& b, const dvh::Work& w, const dvh::Chunk& ch,
                           const dvh::Opts& o, int nsmall, int wc, int mn, int mm, hipStream_t s) {
   const size_t I = sizeof(int32_t);
-  int32_t* L[4];
-  for (int r = 0; r < 4; ++r) L[r] = h->d_list.as<int32_t>() + (size_t)r * wc;
+  int32_t* L[5];
+  for (int r = 0; r < 5; ++r) L[r] = h->d_list.as<int32_t>() + (size_t)r * wc;
   int32_t* info = h->d_route.as<int32_t>();  // 8 ints per route: {count, wx, wy, max n, max m, max nnz}
   int32_t* rh = h->route_host;
   if (h->cus <= 0 && hipDeviceGetAttribute(&h->cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess)
@@ -779,17 +780,22 @@ static int device_cascade(dvh_handle* h, const dvh::Batch& b, const dvh::Work& w
   int cur = rh[0];
   h->n_band += nsmall - cur;
   if (nsmall - cur > 0) variant = bvar;
-  if (cur > 0) {  // pass 2: the band kernel's ICE form over pass 1's refusals, which it hands on by size class
-    // (set up first: the ELL / generic kernels and the route statistics read setup_kernel's outputs)
-    DVH_HIP(h, dvh::launch_setup(b, w, ch, o, mn, mm, s, L[0], cur));
+  if (cur > 0) {  // pass 2: the band kernel's ICE form over pass 1's refusals
     DVH_HIP(h, dvh::launch_pdhg_band(b, w, ch, o, s, true, form_for(cur), L[0], cur, &bvar));
-    DVH_HIP(h, route(1, L[0], cur, -2, 1, 2));
-    DVH_HIP(h, route(2, L[0], cur, -2, 2, 3));
-    DVH_HIP(h, readback(1, 2));
-    const int left = rh[8] + rh[16];
+    DVH_HIP(h, route(1, L[0], cur, -2, 0, 4));
+    DVH_HIP(h, readback(1, 1));
+    const int left = rh[8];
     h->n_band += cur - left;
     if (cur - left > 0 && variant < 0) variant = bvar;
     cur = left;
+    if (cur > 0) {
+      // what the band kernels refused, set up (the ELL / generic kernels and the ELL widths of the route statistics
+      // read setup_kernel's outputs) and handed on by size class
+      DVH_HIP(h, dvh::launch_setup(b, w, ch, o, mn, mm, s, L[4], cur));
+      DVH_HIP(h, route(1, L[4], cur, -2, 1, 2));
+      DVH_HIP(h, route(2, L[4], cur, -2, 2, 3));
+      DVH_HIP(h, readback(1, 2));
+    }
   }
   if (cur == 0) {
     h->last_variant = variant;
@@ -957,7 +963,7 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
               h->w_vbuf.as<double>(), h->w_wbuf.as<double>(), h->w_tmpc.as<double>(), h->w_tmpr.as<double>(),
               h->w_longk.as<int32_t>(), h->w_longt.as<int32_t>(), h->d_hinv.as<double>(), h->w_scal.as<double>(),
               h->w_fc.as<float>(), h->w_fr.as<float>()};
-  DVH_HIP(h, h->d_list.ensure(I * 4 * (size_t)wc));  // the cascade's four device lists (dvh_route.hip)
+  DVH_HIP(h, h->d_list.ensure(I * 5 * (size_t)wc));  // the cascade's five device lists (dvh_route.hip)
   DVH_HIP(h, h->d_route.ensure(I * 8 * 5));
   if (!h->route_host) DVH_HIP(h, hipHostMalloc((void**)&h->route_host, I * 8 * 5, hipHostMallocDefault));
   h->n_ell = h->n_generic = h->n_large = h->n_band = h->n_chain = 0;
