@@ -732,7 +732,29 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
     __syncthreads();
   }
   eta = uniform(eta);
-  double pw = uniform(pw0);
+  // A warm start's primal weight: the geometric mean of the data's (||c~|| / ||q~||) and the starting point's own
+  // ||y~0|| / ||x~0|| (PDLP's weight is a ratio of dual to primal movement; the start carries the seed's balance).
+  // Bench: PDHG 524.5 -> 520.2 ms per step, warm iterations 2,037.5 -> 2,035.5 (profiles/r03q_ab_warm_pw.log); the
+  // start's ratio alone: 523.9 ms.
+  double pwi = pw0;
+  if (o.warm) {
+    double nv[2] = {0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+#pragma unroll
+      for (int v = 0; v < NC; ++v) nv[0] += x[s][v] * x[s][v];
+#pragma unroll
+      for (int r = 0; r < NR; ++r) nv[1] += y[s][r] * y[s][r];
+    }
+    if (tlane) nv[0] += sp[0] * sp[0];
+    if (ilane) nv[1] += sp[0] * sp[0];
+    block_sum<B, 2>(nv, red);
+    if (nv[0] > 1e-20 && nv[1] > 1e-20) {
+      const double ratio = sqrt(nv[1] / nv[0]);
+      pwi = sqrt(ratio * pw0);
+    }
+  }
+  double pw = uniform(pwi);
   const double cnorm = uniform(sqrt(nrm[2])), qnorm = uniform(sqrt(nrm[3])), c0 = uniform(b.c0[k]);
   int it = 0, kin = 0, status = kIterLimit;
   double r0 = -1.0, rprev = -1.0;
