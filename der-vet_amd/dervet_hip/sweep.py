@@ -62,12 +62,31 @@ def seed_split(keys, stride, features=None, cover=False):
             mask = np.ones(S, bool)
             mask[seeds] = False
             rest = np.nonzero(mask)[0]
-        pick = np.empty(len(rest), np.int64)
-        fs = f[seeds]
-        for a in range(0, len(rest), 4096):  # blocked nearest-seed search
-            d = ((f[rest[a:a + 4096], None, :] - fs[None, :, :]) ** 2).sum(-1)
-            pick[a:a + 4096] = d.argmin(1)
+        pick = _nearest(f[rest], f[seeds])
     return seeds, rest, pick
+
+
+def _nearest(fr, fs):
+    """Index of the nearest row of fs for every row of fr: np.argmin of the exact squared distances
+    ((fr_i - fs_j) ** 2).sum() (the first of equal minima).  Ranked by the expanded form |b|^2 - 2 a.b (one small
+    GEMM, in place) instead of an [rest, seeds, d] difference array (10,000 scenarios: ~20 ms instead of ~190 ms);
+    rows whose best two candidates lie within the expanded form's rounding margin are re-ranked exactly."""
+    fr = np.ascontiguousarray(fr, np.float64)
+    fs = np.ascontiguousarray(fs, np.float64)
+    if len(fr) == 0:
+        return np.zeros(0, np.int64)
+    bb = (fs * fs).sum(1)
+    g = fr @ fs.T
+    g *= -2.0
+    g += bb[None, :]
+    j0 = g.argmin(1)
+    rows = np.arange(len(fr))
+    tol = 1e-9 * ((fr * fr).sum(1) + bb.max() + 1.0)
+    close = ((g <= (g[rows, j0] + tol)[:, None]).sum(1) > 1).nonzero()[0]
+    for a in range(0, len(close), 1024):  # near ties: the exact distances, np.argmin's first-minimum rule
+        i = close[a:a + 1024]
+        j0[i] = ((fr[i, None, :] - fs[None, :, :]) ** 2).sum(-1).argmin(1)
+    return j0
 
 
 # dvh_options for the warm phase: restart checks every 64 iterations, KKT every 2nd check (the cold default is
