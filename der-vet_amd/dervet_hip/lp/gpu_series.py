@@ -160,6 +160,7 @@ class DeviceSeries:
         Eb = P["E"] if E is None else np.asarray(E, np.float64)
         rep, wins, price = self._plan(n, dt, year)
         rows_d = torch.as_tensor(rows.astype(np.int32), device=self.dev)
+        id_list = ids.tolist()
         pdis = P["E"] / P["duration"]
         col = lambda v: np.broadcast_to(np.asarray(v, np.float64), (G,)).astype(np.float64, copy=True)
         scal = dict(E=col(Eb), pch=col(pdis), pdis=col(pdis), rte=col(P["rte"]), sdr=col(0.0) / 100.0,
@@ -191,7 +192,8 @@ class DeviceSeries:
                 raise NotImplementedError("SOE floors are hourly (dt = 1)")
             g = BatteryGroupSpec(T=T, J=J, dt=float(dt), dcm_t=dcm_t, dcm_j=dcm_j, base=base, retail=retail, da=None,
                                  demand=demand, emin=em, emax=None, scal=scal, c0=c0,
-                                 tags=[(int(s), w) for s in ids], ice=ice)
+                                 tags=[(s, w) for s in id_list], ice=ice)
             g.index = sel
+            g.scen = ids
             specs.append(g)
         return specs

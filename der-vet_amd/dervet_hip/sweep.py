@@ -119,6 +119,15 @@ class _Transfer:
     w_seed: int = 0      # and of the seed group's
 
 
+def _scenarios_of(g):
+    """The group's scenario ids (tag[0] of each window), from the `scen` array the device series attach, else from
+    the tags."""
+    s = getattr(g, "scen", None)
+    if s is not None:
+        return np.asarray(s, np.int64)
+    return np.fromiter((t[0] for t in g.tags), np.int64, len(g.tags))
+
+
 def _window_id(tag):
     return tag[1] if isinstance(tag, tuple) and len(tag) > 1 else tag
 
@@ -145,6 +154,12 @@ def plan(seed_groups, rest_groups, partner_of):
         on += g.G * g.n
         om += g.G * g.m
         wk += g.G
+    # partner_of as sorted arrays: rest scenario -> seed scenario, looked up for a whole group at once
+    pk = np.fromiter(partner_of.keys(), np.int64, len(partner_of))
+    pv = np.fromiter(partner_of.values(), np.int64, len(partner_of))
+    po = np.argsort(pk, kind="stable")
+    pk, pv = pk[po], pv[po]
+    cols = {}
     for g in rest_groups:
         wid = _window_id(g.tags[0])
         if wid not in seed_at:
@@ -152,8 +167,21 @@ def plan(seed_groups, rest_groups, partner_of):
         sg, son, som, swk = seed_at[wid]
         if not _same_pattern(sg, g):
             raise ValueError(f"seed and rest groups of window {wid!r} differ in pattern")
-        col = {t[0]: i for i, t in enumerate(sg.tags)}
-        local = np.array([col[partner_of[t[0]]] for t in g.tags], np.int64)
+        rs = _scenarios_of(g)
+        i = np.minimum(np.searchsorted(pk, rs), max(len(pk) - 1, 0))
+        if len(rs) and (len(pk) == 0 or not np.array_equal(pk[i], rs)):
+            raise KeyError("a rest scenario has no partner seed")
+        key = id(sg)
+        if key not in cols:  # the seed group's scenarios, sorted, and their positions in the group
+            ss = _scenarios_of(sg)
+            so = np.argsort(ss, kind="stable")
+            cols[key] = (ss[so], so)
+        ss, so = cols[key]
+        want = pv[i]
+        j = np.minimum(np.searchsorted(ss, want), max(len(ss) - 1, 0))
+        if len(want) and (len(ss) == 0 or not np.array_equal(ss[j], want)):
+            raise KeyError(f"a partner seed is not in the seed group of window {wid!r}")
+        local = so[j].astype(np.int64)
         out.append(_Transfer(on, om, son, som, g.n, g.m, g.G, sg.G, local,
                              g.n == 3 * g.T + 1 and g.J == 1, g.T, wk, swk))
         on += g.G * g.n
