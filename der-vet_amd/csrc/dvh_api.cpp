@@ -1019,81 +1019,17 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
       wx = std::max(wx, (int)sc[9]);
     }
     int variant = -1;
-    // Kernel cascade: battery-banded kernel over the chunk -> ELL kernel over the windows it returned (status
-    // -2) -> generic CSR kernel over the windows the ELL kernel returned (status -1).  The fast kernels are
-    // specialised to reflection rho = 1 (the default); other values use the generic kernel.
-    std::vector<int32_t> ell_list;  // empty + ell_all: the whole chunk
-    bool ell_all = true;
-    if (fast && (h->kernel_path == 0 || h->kernel_path >= 3)) {
-      // battery band kernel form: three steps per lane (two windows per CU) once the windows outnumber the CUs;
-      // a window alone on its CU is faster in the one-step form (0.75 vs 0.97 us per iteration,
-      // profiles/r02x_band_forms.log), e.g. one scenario's 12-36 monthly windows
-      if (h->cus <= 0 && hipDeviceGetAttribute(&h->cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess)
-        h->cus = 256;
-      const int forced_form = h->kernel_path == 3 ? 1 : h->kernel_path == 4 ? 3 : 0;
-      // pass 1: battery (+ DCM) windows over the whole chunk; pass 2: the ICE variant over what pass 1 returned
-      auto band_pass = [&](bool ice, const std::vector<int32_t>* in, std::vector<int32_t>& out) -> hipError_t {
-        hipError_t r;
-        int bvar = -1;
-        const int nl = in ? (int)in->size() : c.ch.count;
-        const int band_form = forced_form ? forced_form : (nl <= h->cus ? 1 : 3);
-        if (in) {
-          r = hipMemcpyAsync(h->d_list.p, in->data(), I * in->size(), hipMemcpyHostToDevice, s);
-          if (r != hipSuccess) return r;
-          r = dvh::launch_pdhg_band(b, w, c.ch, o, s, ice, band_form, h->d_list.as<int32_t>(), (int)in->size(),
-                                    &bvar);
-        } else {
-          r = dvh::launch_pdhg_band(b, w, c.ch, o, s, ice, band_form, nullptr, 0, &bvar);
-        }
-        if (r != hipSuccess) return r;
-        ist.resize(2 * (size_t)c.ch.count);
-        r = hipMemcpyAsync(ist.data(), bt->istats + 2 * (size_t)c.ch.first, I * ist.size(), hipMemcpyDeviceToHost,
-                           s);
-        if (r != hipSuccess) return r;
-        r = sync_stream(h, s);
-        if (r != hipSuccess) return r;
-        out.clear();
-        int nb = 0;
-        auto visit = [&](int kg) {
-          if (is_large(kg)) return;
-          if (ist[2 * (size_t)(kg - c.ch.first)] == -2)
-            out.push_back(kg);
-          else
-            ++nb;
-        };
-        if (in) {
-          for (int kg : *in) visit(kg);
-        } else {
-          for (int k = 0; k < c.ch.count; ++k) visit(c.ch.first + k);
-        }
-        h->n_band += nb;
-        if (nb > 0 && variant < 0) variant = bvar;  // band kernel (steps per lane, ICE, waves per window)
-        return hipSuccess;
-      };
-      ell_all = false;
-      DVH_HIP(h, band_pass(false, nullptr, ell_list));
-      if (!ell_list.empty()) {
-        std::vector<int32_t> rest;
-        DVH_HIP(h, band_pass(true, &ell_list, rest));
-        ell_list.swap(rest);
-      }
-    }
-    hipError_t e = hipSuccess;
-    const int n_ell_in = ell_all ? c.ch.count : (int)ell_list.size();
-    if (n_ell_in > 0) {
-      if (!ell_all)
-        DVH_HIP(h, hipMemcpyAsync(h->d_list.p, ell_list.data(), I * ell_list.size(), hipMemcpyHostToDevice, s));
+    // ELL kernel over the chunk -> generic CSR kernel over the windows it returned (status -1), or the generic kernel
+    // alone (kernel path 1, or reflection rho != 1: the fast kernels are specialised to rho = 1).  The band kernels
+    // run in the device cascade only.
+    hipError_t e = hipErrorInvalidValue;
+    if (fast) {
       int ev = -1;
-      e = !fast ? hipErrorInvalidValue
-                : dvh::launch_pdhg_ell(b, w, c.ch, o, c.mn, c.mm, wx, wy, s, &ev,
-                                       ell_all ? nullptr : h->d_list.as<int32_t>(), (int)ell_list.size());
-      if (e == hipSuccess && variant < 0) variant = ev;
+      e = dvh::launch_pdhg_ell(b, w, c.ch, o, c.mn, c.mm, wx, wy, s, &ev, nullptr, 0);
+      if (e == hipSuccess) variant = ev;
     }
     std::vector<int32_t> generic;
-    if (n_ell_in == 0) {
-      // every window was solved by the band kernel (or is large)
-    } else if (e == hipSuccess) {
-      h->n_ell += n_ell_in;
+    if (e == hipSuccess) {
       ist.resize(2 * (size_t)c.ch.count);
       DVH_HIP(h, hipMemcpyAsync(ist.data(), bt->istats + 2 * (size_t)c.ch.first, I * ist.size(),
                                 hipMemcpyDeviceToHost, s));
@@ -1101,20 +1037,16 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
       int nl = 0;
       for (int k = 0; k < c.ch.count; ++k) {
         if (is_large(c.ch.first + k)) {
-          if (ell_all) ++nl;
+          ++nl;
           continue;
         }
         if (ist[2 * (size_t)k] == -1) generic.push_back(c.ch.first + k);
       }
-      h->n_ell -= (int)generic.size() + nl;
-    } else if (e == hipErrorInvalidValue) {  // no ELL instantiation covers the chunk's sizes
+      h->n_ell += c.ch.count - (int)generic.size() - nl;
+    } else if (e == hipErrorInvalidValue) {  // the generic path, or no ELL instantiation covers the chunk's sizes
       (void)hipGetLastError();
-      if (ell_all) {
-        for (int k = 0; k < c.ch.count; ++k)
-          if (!is_large(c.ch.first + k)) generic.push_back(c.ch.first + k);
-      } else {
-        generic = ell_list;
-      }
+      for (int k = 0; k < c.ch.count; ++k)
+        if (!is_large(c.ch.first + k)) generic.push_back(c.ch.first + k);
     } else {
       return hip_fail(h, e, "launch_pdhg_ell");
     }

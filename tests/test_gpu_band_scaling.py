@@ -1,0 +1,67 @@
+"""GPU: the band kernels scale the windows they take themselves (csrc/dvh_band.hip, round 3) instead of reading
+setup_kernel's outputs; the ELL path (dvh_set_kernel_path("ell")) still scales through setup_kernel.  Both are
+setup_kernel's preconditioner (Ruiz inf-norm passes + one Pock-Chambolle pass), so the two paths solve the same
+windows to the same optimum -- also on a badly scaled copy (costs x 1e4, the SOE rows in Wh) -- and agree with HiGHS.
+A band window with crossed bounds is reported PRIMAL_INFEASIBLE with no iterations, as setup_kernel reports it."""
+import dataclasses
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from dervet_hip.lp import builder, scenarios
+from oracle import window_lp
+
+pytestmark = pytest.mark.gpu
+
+
+def _badly_scaled(lp):
+    T = lp.m_eq - 1
+    data, q = lp.data.copy(), lp.q.copy()
+    rows = np.repeat(np.arange(lp.m), np.diff(lp.indptr))
+    soe = (rows >= 1) & (rows <= T)  # the SOE recurrence rows, in Wh
+    data[soe] *= 1e3
+    q[1:T + 1] *= 1e3
+    return dataclasses.replace(lp, data=data, q=q, c=lp.c * 1e4, c0=lp.c0 * 1e4)
+
+
+def _highs(lp):
+    o = dict(K=sp.csr_matrix((lp.data, lp.indices, lp.indptr), shape=(lp.m, lp.n)), q=lp.q, c=lp.c, c0=lp.c0,
+             l=lp.l, u=lp.u, m_eq=lp.m_eq)
+    return o, window_lp.solve_highs(o)
+
+
+def test_band_kernel_scaling_matches_the_setup_kernel_path_and_highs(gpu_solver):
+    base = [lp for g in scenarios.config4(range(3)) for lp in builder.group_window_lps(g)]
+    lps = base + [_badly_scaled(lp) for lp in base[::3]]
+    band = gpu_solver.solve(lps)
+    assert gpu_solver.kernel_stats()["band_windows"] == len(lps)
+    try:
+        gpu_solver.set_kernel_path("ell")
+        ell = gpu_solver.solve(lps)
+        assert gpu_solver.kernel_stats()["band_windows"] == 0
+    finally:
+        gpu_solver.set_kernel_path("default")
+    for i, (lp, a, b) in enumerate(zip(lps, band, ell)):
+        assert a.status == 0 and b.status == 0, (i, a.status_name, b.status_name)
+        assert abs(a.obj - b.obj) <= 2e-6 * abs(b.obj), (i, a.obj, b.obj)
+    for i in (0, 5, 11, len(base), len(lps) - 1):
+        o, h = _highs(lps[i])
+        assert h["status"] == 0
+        assert abs(band[i].obj - h["obj"]) <= 1e-5 * abs(h["obj"]), (i, band[i].obj, h["obj"])
+        assert window_lp.primal_residual_rel(o, band[i].x)[0] <= 1e-6
+
+
+def test_band_kernel_reports_crossed_bounds_without_iterating(gpu_solver):
+    lps = [lp for g in scenarios.config4(range(2)) for lp in builder.group_window_lps(g)]
+    k = 5
+    T = lps[k].m_eq - 1
+    l = lps[k].l.copy()
+    l[2 * T + 7] = lps[k].u[2 * T + 7] + 1.0  # ene_7 above the energy rating
+    lps[k] = dataclasses.replace(lps[k], l=l)
+    res = gpu_solver.solve(lps)
+    assert res[k].status_name == "infeasible" and res[k].iters == 0, (res[k].status_name, res[k].iters)
+    assert all(r.status == 0 for i, r in enumerate(res) if i != k)
+    # reported by the band pass itself: no window was handed on to setup_kernel / the ELL or generic kernels
+    ks = gpu_solver.kernel_stats()
+    assert ks["band_windows"] == len(lps) and ks["ell_windows"] == 0 and ks["generic_windows"] == 0, ks
