@@ -195,3 +195,16 @@ def test_config5_multi_year_seeded_sweep_on_gpu_matches_highs():
     err = np.abs(st[:, 0] - hobj) / np.maximum(np.abs(hobj), 1.0)
     assert err.max() <= 1e-5, (int(err.argmax()), float(err.max()))
     assert st[:, 1].max() <= 1e-6
+
+
+def test_nearest_seed_search_equals_the_exact_argmin_with_ties():
+    """sweep._nearest ranks by the expanded |b|^2 - 2 a.b form and re-ranks near ties exactly: the partners are
+    np.argmin of the exact squared distances (first of equal minima), including exact ties and duplicate seeds."""
+    from dervet_hip.sweep import _nearest
+    rng = np.random.default_rng(11)
+    fs = rng.normal(0, 1, (300, 5))
+    fs[7] = fs[3]                                  # duplicate seeds: the first index wins
+    fr = np.concatenate([rng.normal(0, 1, (4000, 5)), fs[:50] + 1e-13, (fs[10] + fs[11])[None] / 2.0])
+    ref = ((fr[:, None, :] - fs[None, :, :]) ** 2).sum(-1).argmin(1)
+    assert np.array_equal(_nearest(fr, fs), ref)
+    assert np.array_equal(_nearest(fr[:3], fs[:2]), ((fr[:3, None] - fs[None, :2]) ** 2).sum(-1).argmin(1))
