@@ -145,6 +145,12 @@ void solve_one(const dvh_lp& lp, const dvh_options& o, const double* x0, const d
   for (int c = 0; c < n; ++c) x[c] = std::min(std::max(x0 ? x0[c] / Dc[c] : 0.0, lt[c]), ut[c]);
   if (y0)
     for (int r = 0; r < m; ++r) y[r] = r >= me ? std::max(y0[r] / Dr[r], 0.0) : y0[r] / Dr[r];
+  if (x0) {  // the band kernels' warm-start weight: geometric mean of the data's and the start's ||y~|| / ||x~||
+    double nx = 0, ny = 0;
+    for (double v : x) nx += v * v;
+    for (double v : y) ny += v * v;
+    if (nx > 1e-20 && ny > 1e-20) w = std::sqrt(std::sqrt(ny / nx) * w);
+  }
   xa = x;
   ya = y;
   auto T = [&](const std::vector<double>& xi, const std::vector<double>& yi) {
