@@ -24,8 +24,18 @@ DATA = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
 SEED0 = 20250217
 
 
+@functools.lru_cache(maxsize=1)
+def _reference_arrays():
+    with np.load(os.path.join(DATA, "reference_inputs.npz")) as z:
+        out = {k: z[k] for k in z.files}
+    for v in out.values():
+        v.setflags(write=False)  # shared by every caller: read-only
+    return out
+
+
 def reference_inputs():
-    return dict(np.load(os.path.join(DATA, "reference_inputs.npz")))
+    """The reference's input series (data/reference_inputs.npz), loaded once per process (read-only arrays)."""
+    return dict(_reference_arrays())
 
 
 def tariff(name="data_tariff"):
