@@ -4,9 +4,11 @@
 Workload (N=1): BASELINE.json configs[3] -- the synthetic scenario sweep, 10,000 perturbations of the
 config-2 battery + PV + demand-charge + retail scenario (data/multi_der_hourly_timeseries.csv,
 data/tariff.csv) x 12 monthly windows (T = 672..744 hourly steps) = 120,000 window LPs per GPU.
-Multi-GPU (one process per GPU, torchrun): every rank solves its own 10,000-scenario shard (global
-scenario ids rank*S .. rank*S+S-1, weak scaling); no traffic during the solve, then ONE RCCL all-gather
-returns every window's {objective, residuals, status, iterations} to all ranks.
+Multi-GPU (one process per GPU): `bench.py --gpus N` starts its N ranks itself (child processes, rendezvous on
+127.0.0.1) unless an outside launcher (torch.distributed.run) already set WORLD_SIZE, which must then equal N.
+Every rank solves its own 10,000-scenario shard (global scenario ids rank*S .. rank*S+S-1, weak scaling); no
+traffic during the solve, then ONE RCCL all-gather returns every window's {objective, residuals, status,
+iterations, (scenario, window) tag, ch / dis / ene dispatch} to all ranks, overlapped with the next step's solve.
 
 A step = one solve of the rank's whole batch, already resident in HBM (setup kernel: transpose +
 scaling + ||K|| estimate; PDHG kernel: the iterations), plus the result all-gather when N > 1.
@@ -134,6 +136,147 @@ def roofline_object(alg, pdhg_s, prof, kname, launches, copy_gbps):
     return r
 
 
+# the full-population certification of the bench kernel: every one of the 120,000 windows, seeded and cold, re-solved
+# by HiGHS on the host (scripts/certify_dump.py + scripts/certify_highs.py)
+CERTIFICATION = "profiles/r03q_certify.json (all 120,000 windows vs HiGHS, seeded and cold)"
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n):
+    """``--gpus N`` with no outside launcher (WORLD_SIZE unset): start N child processes of this script, one rank per
+    GPU (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1), before this process makes any GPU call.
+    Rank 0 prints the JSON line; the others print nothing.  A rank that fails ends the others (they would wait in a
+    collective forever).  Returns the worst exit status.  The reference's own loop over cases
+    (dervet/DERVET.py:75-83) is what the ranks' shards replace."""
+    import signal
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [None] * n
+    try:
+        while any(rc is None for rc in rcs):
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    rcs[i] = p.poll()
+            if any(rc not in (None, 0) for rc in rcs):
+                for i, p in enumerate(procs):
+                    if rcs[i] is None:
+                        p.send_signal(signal.SIGTERM)
+                for i, p in enumerate(procs):
+                    if rcs[i] is None:
+                        try:
+                            rcs[i] = p.wait(timeout=30)
+                        except subprocess.TimeoutExpired:
+                            p.kill()
+                            rcs[i] = p.wait()
+                break
+            time.sleep(0.05)
+    except KeyboardInterrupt:
+        for p in procs:
+            p.kill()
+        raise
+    bad = [rc for rc in rcs if rc != 0]
+    if bad:
+        sys.stderr.write(f"bench.py: rank exit statuses {rcs}\n")
+        # a signal death (negative) is reported as 128 + signal, as a shell would
+        return max(128 - rc if rc < 0 else rc for rc in bad)
+    return 0
+
+
+def rank_counts(dist, count, device):
+    """Every rank's window count, on every rank (one small all-gather)."""
+    t = torch.tensor([count], dtype=torch.int64, device=device)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [int(v.item()) for v in out]
+
+
+def dry_run(args, world, rank):
+    """The N > 1 plumbing of ``main`` without a GPU (the CPU test of ``--gpus N``): gloo process group, the weak shard
+    of scenarios, tagged result rows of a stub solve (every window 'optimal' at 0 iterations, dispatch zero), the
+    overlapped all-gather, barrier-bracketed timing with the max over ranks, and the JSON line from rank 0."""
+    import torch.distributed as dist
+    from dervet_hip import parallel
+    dist_on = world > 1
+    if os.environ.get("DVH_DRY_RUN_FAIL_RANK") == str(rank):  # test hook: a rank that dies before the rendezvous
+        raise SystemExit(3)
+    if dist_on:
+        dist.init_process_group("gloo")
+    S = args.scenarios
+    scen = range(*parallel.weak_shard(S, rank))
+    tags = [(s, w) for s in scen for w in range(12)]
+    count = len(tags)
+    stats = torch.zeros((count, 4), dtype=torch.float64)
+    stats[:, 0] = torch.arange(count, dtype=torch.float64) + rank * count
+    istats = torch.zeros((count, 2), dtype=torch.int32)
+    tg = torch.as_tensor(parallel.tag_array(tags, offset=rank * count))
+    per_rank = rank_counts(dist, count, "cpu") if dist_on else [count]
+    pending, gathered, gather = None, None, {}
+
+    def step():
+        nonlocal pending, gathered
+        rows = parallel.result_rows(stats, istats, tags=tg)
+        if dist_on:
+            if pending is not None:
+                gathered = pending.wait()
+            pending = parallel.gather_rows(rows, counts=per_rank, async_op=True)
+        else:
+            gathered = rows
+
+    def drain():
+        nonlocal pending, gathered
+        if pending is not None:
+            gathered = pending.wait()
+            pending = None
+
+    for _ in range(args.warmup):
+        step()
+    drain()
+    if dist_on:
+        dist.barrier()
+    t = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    drain()
+    if dist_on:
+        dist.barrier()
+    el = time.perf_counter() - t
+    if dist_on:
+        tt = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    g = parallel.by_tag(parallel.rows_to_numpy(gathered))
+    gather.update(per_rank_windows=per_rank, rows=int(len(g["obj"])),
+                  scenarios=sorted(set(int(v) for v in g["scenario"])) if len(g["obj"]) <= 1200 else None)
+    line = {"metric": METRIC, "value": None, "unit": "windows/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1e3 * el / max(args.steps, 1), 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "dry run (stub solve, no GPU)",
+            "config": {"workload": f"dry run: {S} scenarios x 12 windows per rank", "scenarios_per_gpu": S,
+                       "windows_per_gpu": count, "parallelism": f"dp{world} (gloo, dry run)"},
+            "rank_pids": None, "gather": gather}
+    pids = [None] * world
+    if dist_on:
+        dist.all_gather_object(pids, os.getpid())
+        dist.destroy_process_group()
+    else:
+        pids = [os.getpid()]
+    line["rank_pids"] = pids
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    return 0
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -164,20 +307,37 @@ def main():
     ap.add_argument("--build", choices=("device", "host"), default="device",
                     help="window expansion: on the GPU from compact inputs (lp/gpu_builder.py) or by the host "
                          "builder + upload (bit-identical batches; untimed by the contract, reported as build)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: every rank runs the launch, sharding, tagged result rows, the overlapped gather "
+                         "(gloo) and the max-over-ranks timing with a stub solve; for the CPU test of --gpus N")
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # --gpus N without an outside launcher: N rank processes of this script, started before this process touches
+        # the GPU (children, never an exec of this process)
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} from the launcher but --gpus {args.gpus}: refusing a run whose "
+                         "rank count differs from the GPUs it would report")
+    if args.dry_run:
+        return dry_run(args, world, rank)
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (the solver has no CPU fallback)")
-    local = local % torch.cuda.device_count()  # one rank per GPU; wraps only in a several-ranks-per-GPU rehearsal
+    # RCCL over xGMI; DVH_BENCH_BACKEND=gloo only to rehearse several ranks on one GPU (RCCL refuses that)
+    backend = os.environ.get("DVH_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    if world > 1 and backend == "nccl" and world > ndev:
+        raise SystemExit(f"bench.py: {world} ranks over RCCL need {world} GPUs, {ndev} visible")
+    local = local % ndev  # one rank per GPU; wraps only in a several-ranks-per-GPU (gloo) rehearsal
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        # RCCL over xGMI; DVH_BENCH_BACKEND=gloo only to rehearse several ranks on one GPU (RCCL refuses that)
-        backend = os.environ.get("DVH_BENCH_BACKEND", "nccl")
         dist.init_process_group(backend, **({"device_id": torch.device("cuda", local)} if backend == "nccl" else {}))
 
     from dervet_hip import BatchSolver
@@ -247,9 +407,13 @@ def main():
     tmax = max(r[4] for r in runs) if runs else 0
     gather = {}
     tags_dev = None
+    per_rank = None
     if dist is not None:  # every gathered row carries its (scenario, window): no packing-order rebuild downstream
         tg = sweep.tags if sweep is not None else [t for s_ in specs_tags for t in s_]
-        tags_dev = torch.as_tensor(parallel.tag_array(tg), device=f"cuda:{local}")
+        tags_dev = torch.as_tensor(parallel.tag_array(tg, offset=rank * count), device=f"cuda:{local}")
+        per_rank = rank_counts(dist, count, f"cuda:{local}")
+        if len(set(per_rank)) != 1:
+            raise SystemExit(f"bench.py: unequal windows per rank {per_rank} under weak scaling")
 
     pending = None  # the previous step's all-gather, still in flight (--overlap-gather)
 
@@ -304,6 +468,7 @@ def main():
     ms_per_step = 1e3 * el / args.steps
     if gather:  # the all-gather's share of a step (this rank's last step)
         gather["frac"] = round(gather["ms"] / ms_per_step, 4)
+        gather["per_rank_windows"] = per_rank
     windows_total = count * world
     value = windows_total / (el / args.steps)
 
@@ -398,7 +563,7 @@ def main():
                   "frac_obj_rel_err_le_1e-5": float(np.mean(rel <= 1e-5)) if ok.any() else None,
                   "max_benefit_rel_err": float(ben_rel.max()) if ok.any() else None,
                   "median_benefit_usd": float(np.median(ben_h)) if ok.any() else None,
-                  "full_population": "profiles/r02zzi_certify.json (all 120,000 windows vs HiGHS, seeded and cold)"}
+                  "full_population": CERTIFICATION}
 
     line = {
         "metric": METRIC,

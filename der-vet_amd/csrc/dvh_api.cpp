@@ -63,7 +63,9 @@ struct dvh_handle {
   DevBuf m_list, m_plan, m_pos, m_xbuf, m_abort;  // medium tier (dvh_chain.hip)
   int chain_cap = -1;                             // resident 768-thread workgroups (cooperative limit)
   long long spin_ticks = 0;                       // chain kernel: longest exchange wait (wall-clock ticks)
-  int n_chain_aborts = 0;                         // team launches that aborted (their unfinished windows ran grid-wide)
+  int n_chain_aborts = 0;                         // team launches of the last solve that aborted (unfinished windows
+                                                  // ran grid-wide); dvh_last_chain_aborts
+  std::string warn;                               // diagnostics of the last solve's fallbacks (dvh_last_warning)
   DevBuf o_data, o_cases, o_len, o_hist, o_soe;  // reliability sweep
   DevBuf s_pairs, s_bad;                          // seeded-sweep warm transfer (dvh_sweep.hip)
   DevBuf g_seeds, g_word;                         // scenario series generator (dvh_series.hip)
@@ -252,6 +254,7 @@ int dvh_destroy(dvh_handle* h) {
 }
 
 const char* dvh_last_error(const dvh_handle* h) { return h ? h->err.c_str() : "null handle"; }
+const char* dvh_last_warning(const dvh_handle* h) { return h ? h->warn.c_str() : "null handle"; }
 
 int dvh_warm_transfer(dvh_handle* h, const dvh_packed* b, const int32_t* pairs, int32_t count) {
   if (!h) return DVH_ERR_ARG;
@@ -300,12 +303,13 @@ int dvh_series_draws(dvh_handle* h, const dvh_sweep_draws* d) {
   DVH_HIP(h, hipMemcpyAsync(h->g_seeds.p, d->seeds, sizeof(uint64_t) * (size_t)d->count, hipMemcpyHostToDevice, s));
   DVH_HIP(h, hipMemsetAsync(h->g_word.p, 0, sizeof(int32_t), s));
   hipError_t e = dvh::launch_series_draws(h->g_seeds.as<uint64_t>(), d->count, d->steps, d->n_uniform, d->a1,
-                                          d->innov, d->z0, d->ar, d->uniform, h->g_word.as<int32_t>(), s);
+                                          d->innov, d->z0, d->ar, d->uniform, h->g_word.as<int32_t>(), d->ambiguous,
+                                          s);
   if (e != hipSuccess) return hip_fail(h, e, "launch_series_draws");
   int32_t amb = 0;
   DVH_HIP(h, hipMemcpyAsync(&amb, h->g_word.p, sizeof(int32_t), hipMemcpyDeviceToHost, s));
   DVH_HIP(h, hipStreamSynchronize(s));
-  if (amb)
+  if (amb && !d->ambiguous)
     return fail(h, DVH_ERR_UNSUPPORTED, "series draws: " + std::to_string(amb) +
                                             " scenario(s) met a ziggurat wedge test within 2^-40 of exp(); their "
                                             "draws may differ from numpy's");
@@ -360,6 +364,12 @@ int dvh_last_path_counts(const dvh_handle* h, int32_t* out3) {
   out3[0] = h->n_ell;
   out3[1] = h->n_generic;
   out3[2] = h->n_large;
+  return DVH_OK;
+}
+
+int dvh_last_chain_aborts(const dvh_handle* h, int32_t* out) {
+  if (!h || !out) return DVH_ERR_ARG;
+  *out = h->n_chain_aborts;
   return DVH_OK;
 }
 
@@ -677,6 +687,12 @@ static int chain_pass(dvh_handle* h, const dvh::Batch& b, const dvh::Work& w, co
     int khz = 0;
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device) != hipSuccess || khz <= 0) khz = 100000;
     h->spin_ticks = (long long)khz * 1000 * 2;  // 2 s: a partner's hand-off normally takes microseconds
+    // DVH_CHAIN_SPIN_TICKS (tests): another limit; < 0 aborts at the first exchange that has to wait, forcing the
+    // abort -> grid-wide hand-over path
+    if (const char* v = getenv("DVH_CHAIN_SPIN_TICKS")) {
+      const long long t = atoll(v);
+      if (t != 0) h->spin_ticks = t;
+    }
   }
   const int S = h->chain_cap / 8;  // resident slots per XCD
   for (int g = 0; g < 2; ++g) {
@@ -722,7 +738,7 @@ static int chain_pass(dvh_handle* h, const dvh::Batch& b, const dvh::Work& w, co
           snprintf(buf, sizeof buf, " %d: %d %d %d 0x%x 0x%x 0x%x;", gb, d[0], d[1], d[2], d[3], d[4], d[5]);
           msg += buf;
         }
-        h->err = msg;
+        h->warn += msg;
         ++h->n_chain_aborts;
         std::vector<int32_t> st(2);
         for (int q = 0; q < np; ++q) {
@@ -967,6 +983,8 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
   DVH_HIP(h, h->d_route.ensure(I * 8 * 5));
   if (!h->route_host) DVH_HIP(h, hipHostMalloc((void**)&h->route_host, I * 8 * 5, hipHostMallocDefault));
   h->n_ell = h->n_generic = h->n_large = h->n_band = h->n_chain = 0;
+  h->n_chain_aborts = 0;
+  h->warn.clear();
   h->large_ms[0] = h->large_ms[1] = 0.0f;
   h->chunk_used = 0;
   DVH_HIP(h, hipEventRecord(h->ev[0], s));
@@ -1134,7 +1152,8 @@ extern "C" int dvh_solve_batch(dvh_handle* h, const dvh_lp* lps, int32_t count, 
     if (b[i + 1] > b[i]) th.emplace_back([&, i] { rc[i] = solve_batch_one(hs[i], lps + b[i], b[i + 1] - b[i], out + b[i]); });
   if (b[1] > b[0]) rc[0] = solve_batch_one(h, lps, b[1], out);
   for (auto& t : th) t.join();
-  int nell = 0, ngen = 0, nlarge = 0, nband = 0, nchain = 0;
+  int nell = 0, ngen = 0, nlarge = 0, nband = 0, nchain = 0, naborts = 0;
+  std::string warn;
   double setup = 0.0, pdhg = 0.0;
   for (int i = 0; i < P; ++i) {
     if (rc[i] != DVH_OK) {
@@ -1147,6 +1166,8 @@ extern "C" int dvh_solve_batch(dvh_handle* h, const dvh_lp* lps, int32_t count, 
     nlarge += hs[i]->n_large;
     nband += hs[i]->n_band;
     nchain += hs[i]->n_chain;
+    naborts += hs[i]->n_chain_aborts;
+    warn += hs[i]->warn;
     setup = std::max(setup, hs[i]->timing[1]);
     pdhg = std::max(pdhg, hs[i]->timing[2]);
   }
@@ -1155,6 +1176,8 @@ extern "C" int dvh_solve_batch(dvh_handle* h, const dvh_lp* lps, int32_t count, 
   h->n_large = nlarge;
   h->n_band = nband;
   h->n_chain = nchain;
+  h->n_chain_aborts = naborts;
+  h->warn = warn;
   h->timing[0] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   h->timing[1] = setup;
   h->timing[2] = pdhg;

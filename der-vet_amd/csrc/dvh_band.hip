@@ -440,6 +440,22 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
     if (tlane || ilane) fsp *= factor(nsp);
     __syncthreads();  // every read of this pass's XE / YS / XT / TP is done
   }
+  {  // the KKT checks unscale with single-precision copies of the factors: a window whose factors leave
+     // [2^-100, 2^100] (far inside float's normal range) goes to the ELL / generic path, which keeps them in double
+    auto oor = [](double f) { return !(f >= 0x1p-100 && f <= 0x1p100); };
+    bool out = oor(fsp);
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+#pragma unroll
+      for (int v = 0; v < NC; ++v) out |= oor(fcv[s][v]);
+#pragma unroll
+      for (int r = 0; r < NR; ++r) out |= oor(frv[s][r]);
+    }
+    if (__syncthreads_or(out)) {
+      bail();
+      return;
+    }
+  }
   exchange();
   __syncthreads();
   {  // scaled coefficients (K Dr) Dc, as setup_kernel forms them

@@ -26,12 +26,15 @@
 // by relaxed agent-scope loads (MI355X_MICROARCH.md, inter-workgroup visibility: granules need no fence); tags are
 // (window ordinal, round), so no flag or buffer ever needs resetting inside a launch, and every buffer is
 // double-buffered by round parity (a producer can be at most one round ahead of any consumer, because it needs the
-// consumer's data of the round in between).  Teams are persistent: a cooperative launch of NT x PT workgroups, all
-// resident, team t taking windows t, t + NT, ...; every spin is bounded and an expired one aborts the launch (the
-// host then reports an error), so a fault can never leave waves spinning.
+// consumer's data of the round in between).  Teams are persistent: one launch of the device's resident capacity of
+// workgroups, team t taking windows t, t + NT, ...; every spin is bounded and an expired one aborts the launch (the
+// host hands the unfinished windows to the grid-wide path), so a fault can never leave waves spinning.
 //
 // Same algorithm, scaling, steps and checks as the band kernel (restated in oracle/pdlp_ref.py); a segment's
 // arithmetic is the band kernel's for its steps, so results agree with the on-chip kernels to rounding.
+#include <stdlib.h>
+#include <string.h>
+
 #include <algorithm>
 #include <type_traits>
 
@@ -481,7 +484,8 @@ struct ChainArgs {
   int* abort_word;           // zeroed before the launch (with the diagnostics); [0] abort, [8] next window
   int PT, NT;
   int S;                     // workgroup slots per XCD (grid = 8 S)
-  long long spin_ticks;      // longest wait for a partner's exchange (wall-clock ticks) before the launch aborts
+  long long spin_ticks;      // longest wait for a partner's exchange (wall-clock ticks) before the launch aborts;
+                             // < 0 (tests): abort at the first poll that has to wait
 };
 
 // Team and segment of workgroup b: blocks b and b + 8 share an XCD (round-robin dispatch, MI355X_MICROARCH.md --
@@ -565,7 +569,7 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
                 pval[e0 + base + lane] = (unsigned)xv;
               }
             }
-            if ((++spins & 1023u) == 0) {
+            if ((++spins & 1023u) == 0 || a.spin_ticks < 0) {
               const bool late = bounded && wall_clock64() - t0 > a.spin_ticks;
               if (late || __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
                 if (lane == 0) {
@@ -703,7 +707,7 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
           if (__all(ok)) break;
           ++spins;
           bool late = false;
-          if ((spins & 1023u) == 0 && ((late = wall_clock64() - tw > a.spin_ticks) ||
+          if (((spins & 1023u) == 0 || a.spin_ticks < 0) && ((late = wall_clock64() - tw > a.spin_ticks) ||
                                        __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
             // diagnostics per workgroup (abort_word[16 + 8 blockIdx]): {1 = timed out / 2 = saw the abort, list
             // start, round, entry, expected tag, tag seen}
@@ -973,7 +977,7 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
               }
             }
             bool late = false;
-            if ((++spins & 1023u) == 0 && ((late = wall_clock64() - tw > a.spin_ticks) ||
+            if (((++spins & 1023u) == 0 || a.spin_ticks < 0) && ((late = wall_clock64() - tw > a.spin_ticks) ||
                                            __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
               if (lane == 0) {
                 const int d[6] = {late ? 1 : 2, -1, cC, r, (int)tag, 0};
@@ -1413,7 +1417,20 @@ hipError_t launch_chain(const Batch& b, const Work& w, const Chunk& ch, const Op
   Chunk cc = ch;
   Opts oo = o;
   void* args[] = {&bb, &ww, &cc, &oo, &a};
-  return hipLaunchCooperativeKernel((const void*)pdhg_chain_kernel, dim3(8 * S), dim3(kCB), args, (unsigned)lds, s);
+  // An ordinary launch of the capacity-sized grid (chain_capacity: occupancy x CUs, so every workgroup is placed at
+  // once on an otherwise idle device).  Residency is not guaranteed by the launch, and need not be: every spin is
+  // bounded, so a grid that is not resident aborts and its unfinished windows go to the grid-wide path
+  // (tests/test_gpu_medium.py forces that path).  The cooperative launch (DVH_CHAIN_LAUNCH=coop) guarantees residency
+  // but makes the HIP runtime's exit-time teardown fault under rocprofv3 (SIGSEGV in libhsa-runtime64 called from
+  // libamdhip64's exit handler, after the profiler's finalisation; profiles/r04a_chain_exit_crash.txt), same speed.
+  static const bool coop = [] {
+    const char* v = getenv("DVH_CHAIN_LAUNCH");
+    return v && strcmp(v, "coop") == 0;
+  }();
+  if (coop)
+    return hipLaunchCooperativeKernel((const void*)pdhg_chain_kernel, dim3(8 * S), dim3(kCB), args, (unsigned)lds, s);
+  hipLaunchKernelGGL(pdhg_chain_kernel, dim3(8 * S), dim3(kCB), lds, s, bb, ww, cc, oo, a);
+  return hipGetLastError();
 }
 
 namespace {

@@ -87,7 +87,8 @@ struct Work {
   const double* hinv;  // [kHalpernTab] 1 / (k + 2), k = 0.. (Halpern anchor weights, exact IEEE quotients)
   double* scal;     // [count * kScal]  eta, w0, ||c||, ||q||, nlong(K), nlong(K^T), flag, ||K||,
                     //   max short row len K, K^T (<= 8), #rows > 8 in K, K^T
-  float* fc;        // [sum n]  Dc rounded to single precision (the band kernel's KKT checks)
+  float* fc;        // [sum n]  Dc rounded to single precision (the band kernel's KKT checks; written by the band
+                    //          kernels, whose factors stay within [2^-100, 2^100])
   float* fr;        // [sum m]  Dr rounded to single precision
 };
 
@@ -156,7 +157,8 @@ hipError_t launch_warm_transfer(const int64_t* desc, const double* c, const doub
 // scenarios with a wedge test too close to call), and the device builder's inputs of G windows (bad counts rows out of
 // range).
 hipError_t launch_series_draws(const uint64_t* seeds, int count, int steps, int n_unif, double a1, double innov,
-                               double* z0, double* ar, double* unif, int32_t* ambiguous, hipStream_t s);
+                               double* z0, double* ar, double* unif, int32_t* ambiguous, int32_t* amb_rows,
+                               hipStream_t s);
 hipError_t launch_series_windows(const ::dvh_window_series& w, int32_t* bad, hipStream_t s);
 // Cascade lists on the device (dvh_route.hip): the small windows of [first, first + count) -- or of in_list[0 ..
 // count) -- whose status is `want` (cls 1: and n <= lim_n, m <= lim_m; cls 2: the others; cls 0: any size), in order,

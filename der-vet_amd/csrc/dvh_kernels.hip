@@ -308,10 +308,8 @@ __global__ __launch_bounds__(kSetupB) void setup_kernel(const Batch b, const Wor
     nrm[1] += qi * d * qi * d;
     nrm[3] += qi * qi;
   }
-  // single-precision copies of the scalings for the band kernel's KKT checks: a check reads 4 bytes per row and
-  // column instead of Dc, Dr and their reciprocals (32), which with 64 windows per XCD do not stay in L2
-  for (int j = tid; j < n; j += kSetupB) w.fc[W.wn + j] = (float)Dc[j];
-  for (int i = tid; i < m; i += kSetupB) w.fr[W.wm + i] = (float)Dr[i];
+  // (the single-precision factor copies Work::fc / fr are the band kernels' own: they scale their windows themselves
+  // and never run after this kernel, so none are written here)
   if (!MED) {
     for (int j = tid; j < n; j += kSetupB) gDc[j] = Dc[j];
     for (int i = tid; i < m; i += kSetupB) gDr[i] = Dr[i];

@@ -613,15 +613,30 @@ struct LargeSolver {
   int32_t* pinned_status = nullptr;
   hipStream_t cap = nullptr;  // graph-capture stream (capture never executes work)
   hipEvent_t poll[2] = {nullptr, nullptr};
+  hipEvent_t tev[3] = {nullptr, nullptr, nullptr};  // setup / PDHG timing brackets, reused by every solve
   ~LargeSolver() {
     for (Buf* b : {&ints, &dbls, &st})
       if (b->p) (void)hipFree(b->p);
     if (pinned_status) (void)hipHostFree(pinned_status);
     for (hipEvent_t e : poll)
       if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : tev)
+      if (e) (void)hipEventDestroy(e);
     if (cap) (void)hipStreamDestroy(cap);
   }
 };
+
+namespace {
+// one check period's graph and its executable, destroyed on every return path
+struct GraphGuard {
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  ~GraphGuard() {
+    if (exec) (void)hipGraphExecDestroy(exec);
+    if (graph) (void)hipGraphDestroy(graph);
+  }
+};
+}  // namespace
 
 LargeSolver* large_create() { return new LargeSolver(); }
 void large_destroy(LargeSolver* ls) { delete ls; }
@@ -748,6 +763,8 @@ hipError_t large_solve(LargeSolver* ls, const Batch& b, int k, const int64_t* d,
   if (!ls->cap) LG_TRY(hipStreamCreateWithFlags(&ls->cap, hipStreamNonBlocking));
   for (hipEvent_t& e : ls->poll)
     if (!e) LG_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  for (hipEvent_t& e : ls->tev)
+    if (!e) LG_TRY(hipEventCreate(&e));
   hipStream_t cap = ls->cap;
   double* db = ls->dbls.as<double>();
 
@@ -782,10 +799,7 @@ hipError_t large_solve(LargeSolver* ls, const Batch& b, int k, const int64_t* d,
     a.c0 = c0;
   }
 
-  hipEvent_t e0, e1, e2;
-  LG_TRY(hipEventCreate(&e0));
-  LG_TRY(hipEventCreate(&e1));
-  LG_TRY(hipEventCreate(&e2));
+  hipEvent_t e0 = ls->tev[0], e1 = ls->tev[1], e2 = ls->tev[2];
   LG_TRY(hipEventRecord(e0, s));
   // ---- setup: scaling, scaled data, norms, power iteration, start point
   lg_ones<<<nbe, LB, 0, s>>>(a);
@@ -814,8 +828,7 @@ hipError_t large_solve(LargeSolver* ls, const Batch& b, int k, const int64_t* d,
   LG_TRY(hipEventRecord(e1, s));
 
   // ---- one check period as a graph: chk iterations (the last one is the check iteration) + check
-  hipGraph_t graph = nullptr;
-  hipGraphExec_t exec = nullptr;
+  GraphGuard gg;
   LG_TRY(hipStreamBeginCapture(cap, hipStreamCaptureModeRelaxed));
   for (int i = 0; i < a.chk; ++i) {
     if (i + 1 < a.chk) {
@@ -830,12 +843,13 @@ hipError_t large_solve(LargeSolver* ls, const Batch& b, int k, const int64_t* d,
   lg_kkt_cols<<<nbc + nlc, LB, 0, cap>>>(a);
   lg_check<<<1, 1024, 0, cap>>>(a);
   lg_restart<<<nbe, LB, 0, cap>>>(a);
-  hipError_t ce = hipStreamEndCapture(cap, &graph);
+  hipError_t ce = hipStreamEndCapture(cap, &gg.graph);
   if (ce != hipSuccess) {
     if (err) *err = std::string("graph capture: ") + hipGetErrorString(ce);
     return ce;
   }
-  LG_TRY(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+  LG_TRY(hipGraphInstantiate(&gg.exec, gg.graph, nullptr, nullptr, 0));
+  hipGraphExec_t exec = gg.exec;
   // replays: every kPoll replays the status is copied to pinned memory behind an event; the host waits on
   // the PREVIOUS poll's event, so kPoll..2*kPoll replays stay queued and the GPU never idles on the host
   constexpr int kPoll = 4;
@@ -861,8 +875,6 @@ hipError_t large_solve(LargeSolver* ls, const Batch& b, int k, const int64_t* d,
   if (ge == hipSuccess) ge = hipGetLastError();
   if (ge == hipSuccess) ge = hipEventRecord(e2, s);
   if (ge == hipSuccess) ge = hipStreamSynchronize(s);
-  hipGraphExecDestroy(exec);
-  hipGraphDestroy(graph);
   if (ge != hipSuccess) {
     if (err) *err = std::string("large-LP PDHG: ") + hipGetErrorString(ge);
     return ge;
@@ -872,9 +884,6 @@ hipError_t large_solve(LargeSolver* ls, const Batch& b, int k, const int64_t* d,
   (void)hipEventElapsedTime(&t2, e1, e2);
   if (setup_ms) *setup_ms += t1;
   if (pdhg_ms) *pdhg_ms += t2;
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
-  hipEventDestroy(e2);
   return hipSuccess;
 }
 

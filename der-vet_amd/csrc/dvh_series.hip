@@ -32,7 +32,8 @@ struct DeviceExp {
 
 __global__ __launch_bounds__(kDrawB) void series_draws_kernel(const uint64_t* seeds, int count, int steps, int n_unif,
                                                              double a1, double innov, double* z0, double* ar,
-                                                             double* unif, int32_t* ambiguous) {
+                                                             double* unif, int32_t* ambiguous,
+                                                             int32_t* amb_rows) {
   const int i = blockIdx.x * kDrawB + threadIdx.x;
   if (i >= count) return;
   rng::Pcg64 g = rng::seed_pcg64(seeds[i]);
@@ -49,6 +50,7 @@ __global__ __launch_bounds__(kDrawB) void series_draws_kernel(const uint64_t* se
     out[t] = y;
   }
   for (int k = 0; k < n_unif; ++k) unif[(int64_t)i * n_unif + k] = rng::next_double(g);
+  if (amb_rows) amb_rows[i] = amb ? 1 : 0;
   if (amb) atomicAdd(ambiguous, 1);
 }
 
@@ -160,10 +162,11 @@ __global__ __launch_bounds__(kWinB) void series_windows_kernel(const dvh_window_
 }  // namespace
 
 hipError_t launch_series_draws(const uint64_t* seeds, int count, int steps, int n_unif, double a1, double innov,
-                               double* z0, double* ar, double* unif, int32_t* ambiguous, hipStream_t s) {
+                               double* z0, double* ar, double* unif, int32_t* ambiguous, int32_t* amb_rows,
+                               hipStream_t s) {
   if (count <= 0) return hipSuccess;
   hipLaunchKernelGGL(series_draws_kernel, dim3((count + kDrawB - 1) / kDrawB), dim3(kDrawB), 0, s, seeds, count,
-                     steps, n_unif, a1, innov, z0, ar, unif, ambiguous);
+                     steps, n_unif, a1, innov, z0, ar, unif, ambiguous, amb_rows);
   return hipGetLastError();
 }
 

@@ -80,7 +80,8 @@ class SweepDraws(ctypes.Structure):
     """dvh_sweep_draws (scenario series generator; seeds host, outputs device)."""
     _fields_ = [("count", ctypes.c_int32), ("steps", ctypes.c_int32), ("n_uniform", ctypes.c_int32),
                 ("seeds", ctypes.c_void_p), ("a1", ctypes.c_double), ("innov", ctypes.c_double),
-                ("z0", ctypes.c_void_p), ("ar", ctypes.c_void_p), ("uniform", ctypes.c_void_p)]
+                ("z0", ctypes.c_void_p), ("ar", ctypes.c_void_p), ("uniform", ctypes.c_void_p),
+                ("ambiguous", ctypes.c_void_p)]
 
 
 class WindowSeries(ctypes.Structure):
@@ -114,6 +115,8 @@ SYMBOLS = {
     "dvh_last_path_counts": (ctypes.c_int, [ctypes.c_void_p, c_int32_p]),
     "dvh_last_path_counts4": (ctypes.c_int, [ctypes.c_void_p, c_int32_p]),
     "dvh_last_path_counts5": (ctypes.c_int, [ctypes.c_void_p, c_int32_p]),
+    "dvh_last_chain_aborts": (ctypes.c_int, [ctypes.c_void_p, c_int32_p]),
+    "dvh_last_warning": (ctypes.c_char_p, [ctypes.c_void_p]),
     "dvh_set_kernel_path": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "dvh_outage_coverage": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(OutageCase), ctypes.c_int32, c_int32_p,
                                            c_double_p]),

@@ -72,29 +72,30 @@ def dispatch_runs(desc):
     return runs
 
 
-def tag_array(tags):
+def tag_array(tags, offset=0):
     """[count, 2] float64 (scenario, window) of packed windows' tags ((scenario, window) tuples; any other tag:
-    (-1, its position))."""
+    (-1, offset + its position)).  offset: the shard's first global window, so that untagged rows stay distinct
+    after a gather (every rank's local positions start at 0)."""
     out = np.empty((len(tags), 2), np.float64)
     for i, t in enumerate(tags):
         if isinstance(t, tuple) and len(t) == 2 and all(isinstance(v, (int, np.integer)) for v in t):
             out[i] = t
         else:
-            out[i] = (-1, i)
+            out[i] = (-1, offset + i)
     return out
 
 
-def result_rows(stats, istats, x=None, desc=None, tmax=None, runs=None, tags=None):
+def result_rows(stats, istats, x=None, desc=None, tmax=None, runs=None, tags=None, offset=0):
     """Per-window result rows (float64): {obj, primal_res_rel, dual_res_rel, gap_rel, status, iters, scenario,
     window} and, with x / desc, the window's dispatch ch, dis, ene in a fixed stride of 3 * tmax (zero padded).
     tags: [count, 2] (scenario, window) per window (``tag_array``; a tensor on the rows' device, or numpy); None:
-    (-1, local position).  Works on device or host tensors (strided copies per run of equal windows; no index
-    tensors)."""
+    (-1, offset + local position), offset = the shard's first global window.  Works on device or host tensors
+    (strided copies per run of equal windows; no index tensors)."""
     import torch
     k = stats.shape[0]
     if tags is None:
         tg = torch.stack([torch.full((k,), -1.0, dtype=torch.float64, device=stats.device),
-                          torch.arange(k, dtype=torch.float64, device=stats.device)], dim=1)
+                          torch.arange(offset, offset + k, dtype=torch.float64, device=stats.device)], dim=1)
     else:
         tg = torch.as_tensor(tags, dtype=torch.float64).to(stats.device)
     base = torch.cat([stats.to(torch.float64), istats.to(torch.float64), tg], dim=1)

@@ -145,8 +145,15 @@ class BatchSolver:
         self._check(self._lib.dvh_last_stats(self._h, v), "dvh_last_stats")
         c = (ctypes.c_int32 * 5)()
         self._check(self._lib.dvh_last_path_counts5(self._h, c), "dvh_last_path_counts5")
+        a = ctypes.c_int32()
+        self._check(self._lib.dvh_last_chain_aborts(self._h, ctypes.byref(a)), "dvh_last_chain_aborts")
         return {"band_windows": c[3], "ell_windows": v[0], "generic_windows": v[1], "variant": v[2],
-                "generic_only": bool(v[3]), "large_windows": c[2], "chain_windows": c[4]}
+                "generic_only": bool(v[3]), "large_windows": c[2], "chain_windows": c[4],
+                "chain_aborts": int(a.value)}
+
+    def last_warning(self):
+        """Diagnostics of the last solve's fallbacks (a medium-tier team launch that aborted), or ''."""
+        return (self._lib.dvh_last_warning(self._h) or b"").decode()
 
     def host_syncs(self):
         """Host waits on the stream during the last solve (dvh_last_host_syncs)."""

@@ -216,6 +216,10 @@ typedef struct dvh_sweep_draws {
   double* z0;
   double* ar;
   double* uniform;
+  /* optional [count] int32 (device): 1 for a scenario whose ziggurat wedge test landed within 2^-40 of exp() (its
+   * draws may differ from numpy's), else 0.  Given, such scenarios are only flagged (the caller regenerates them on
+   * the host) and the call returns DVH_OK; NULL: any such scenario fails the call with DVH_ERR_UNSUPPORTED. */
+  int32_t* ambiguous;
 } dvh_sweep_draws;
 int dvh_series_draws(dvh_handle* h, const dvh_sweep_draws* d);
 
@@ -279,6 +283,13 @@ int dvh_last_path_counts4(const dvh_handle* h, int32_t* out4);
  * 769 .. 12,288 steps -- the annual hourly window n = "year", sub-hourly monthly windows -- solved as a batch, a
  * team of one workgroup per <= 768-step segment per window, dvh_chain.hip)}. */
 int dvh_last_path_counts5(const dvh_handle* h, int32_t* out5);
+/* Medium-tier team launches of the most recent solve that aborted (a segment exchange outlasted the spin limit): the
+ * windows such a launch had finished keep their results, the others were solved on the grid-wide path, and the solve
+ * still returns DVH_OK.  out = that count (0 when nothing aborted); reset by every solve. */
+int dvh_last_chain_aborts(const dvh_handle* h, int32_t* out);
+/* Diagnostics of a successful solve that took a fallback (a medium-tier abort: the workgroups' exchange state), or
+ * "" -- dvh_last_error is left to errors.  Reset by every solve. */
+const char* dvh_last_warning(const dvh_handle* h);
 /* ---- Post-facto reliability sweep.
  * Replaces Reliability.load_coverage_probability (dervet/MicrogridValueStreams/Reliability.py:876-967) and the
  * serial recursion it drives (data_process :447-487, simulate_outage :489-570): for every case, an outage is

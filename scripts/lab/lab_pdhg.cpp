@@ -1,3 +1,5 @@
+// ALGORITHM LAB (dev study, not the product, not the oracle): a copy of oracle/cpu_pdhg.cpp with experimental knobs
+// read from the environment (LAB_*), for iteration-count studies on host cores.  Original header follows.
 // ORACLE / CPU BASELINE (test infrastructure, not the product): the batched PDHG of libdervet_hip restated in plain
 // C++ for host cores, behind the same C ABI (include/dervet_hip.h; the core entry points -- create / destroy /
 // options / dvh_solve_batch / timing; device-only entry points return DVH_ERR_UNSUPPORTED).
@@ -10,15 +12,24 @@
 #include <omp.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <chrono>
 #include <cmath>
 #include <cstring>
 #include <string>
 #include <vector>
 
-#include "../include/dervet_hip.h"
-// the product's host-side input validation (plain C++, der-vet_amd/csrc/dvh_validate.cpp), compiled in by build()
-#include "../der-vet_amd/csrc/dvh_validate.h"
+#include "../../include/dervet_hip.h"
+#include "../../der-vet_amd/csrc/dvh_validate.h"
+
+static double envd(const char* k, double d) {
+  const char* v = getenv(k);
+  return v ? atof(v) : d;
+}
+// per-window trajectory: first iteration at which max(pres, dres, gap) <= 1e-3, 1e-4, 1e-5 (lab output)
+thread_local int g_first[3];
+static int* g_traj = nullptr;  // [count][3]
+thread_local bool g_trace = false;
 
 struct dvh_handle {
   dvh_options opts;
@@ -111,8 +122,21 @@ void solve_one(const dvh_lp& lp, const dvh_options& o, const double* x0, const d
       rmax[r] += a;
       cmax[K.j[k]] += a;
     }
-  for (int r = 0; r < m; ++r) Dr[r] /= std::sqrt(rmax[r] > 0 ? rmax[r] : 1.0);
-  for (int c = 0; c < n; ++c) Dc[c] /= std::sqrt(cmax[c] > 0 ? cmax[c] : 1.0);
+  const double pca = envd("LAB_PC_ALPHA", 1.0);  // Pock-Chambolle alpha: rows by sum |a|^(2-alpha), cols by sum |a|^alpha
+  if (pca != 1.0) {
+    std::fill(rmax.begin(), rmax.end(), 0.0);
+    std::fill(cmax.begin(), cmax.end(), 0.0);
+    for (int r = 0; r < m; ++r)
+      for (int k = K.p[r]; k < K.p[r + 1]; ++k) {
+        const double a = Dr[r] * std::fabs(K.v[k]) * Dc[K.j[k]];
+        rmax[r] += std::pow(a, 2.0 - pca);
+        cmax[K.j[k]] += std::pow(a, pca);
+      }
+  }
+  if (envd("LAB_NO_PC", 0) == 0) {
+    for (int r = 0; r < m; ++r) Dr[r] /= std::sqrt(rmax[r] > 0 ? rmax[r] : 1.0);
+    for (int c = 0; c < n; ++c) Dc[c] /= std::sqrt(cmax[c] > 0 ? cmax[c] : 1.0);
+  }
   Csr Kt = K;
   for (int r = 0; r < m; ++r)
     for (int k = K.p[r]; k < K.p[r + 1]; ++k) Kt.v[k] = Dr[r] * K.v[k] * Dc[K.j[k]];
@@ -124,6 +148,20 @@ void solve_one(const dvh_lp& lp, const dvh_options& o, const double* x0, const d
     ut[c] = lp.u[c] / Dc[c];
   }
   for (int r = 0; r < m; ++r) qt[r] = Dr[r] * lp.q[r];
+  // bound-objective rescaling (PDLP / cuPDLPx): x scaled by 1 / (||q~|| + 1), y by 1 / (||c~|| + 1); folded into the
+  // diagonal scalings so every unscaled quantity stays exact
+  if (envd("LAB_BOR", 0) != 0) {
+    const double bs = 1.0 / (norm2(qt) + 1.0), cs = 1.0 / (norm2(ct) + 1.0);
+    for (int c = 0; c < n; ++c) {
+      ct[c] *= cs;
+      lt[c] *= bs;
+      ut[c] *= bs;
+    }
+    for (int r = 0; r < m; ++r) qt[r] *= bs;
+    // the unscaled x = Dc x~ / bs, y = Dr y~ / cs
+    for (int c = 0; c < n; ++c) Dc[c] /= bs;
+    for (int r = 0; r < m; ++r) Dr[r] /= cs;
+  }
   // ---- ||Kt||_2: v <- Kt'(Kt v) from 1/sqrt(n), sigma^2 = |v_P| / |v_{P-1}|
   std::vector<double> v(n, 1.0 / std::sqrt((double)n)), prev(n), tmpm(m), tmpn(n);
   for (int it = 0; it < o.power_iters; ++it) {
@@ -206,6 +244,10 @@ void solve_one(const dvh_lp& lp, const dvh_options& o, const double* x0, const d
   };
   int it = 0, kin = 0;
   double r0 = -1.0, rprev = -1.0;
+  const double kp = envd("LAB_KP", -1.0), ki = envd("LAB_KI", 0.0), kd = envd("LAB_KD", 0.0);
+  double esum = 0.0, eprev = 0.0;
+  bool ehave = false;
+  g_first[0] = g_first[1] = g_first[2] = -1;
   Kkt last{};
   bool have = false;
   std::vector<double> lx = x, ly = y;
@@ -220,6 +262,11 @@ void solve_one(const dvh_lp& lp, const dvh_options& o, const double* x0, const d
       if (it % (o.check_every * o.kkt_every) == 0 || it + o.check_every > o.max_iters) {
         last = kkt();
         have = true;
+        {
+          const double worst = std::max(last.pres, std::max(last.dres, last.gap));
+          for (int u = 0; u < 3; ++u)
+            if (g_first[u] < 0 && worst <= std::pow(10.0, -3 - u)) g_first[u] = it;
+        }
         lx = xp;
         ly = yp;
         const bool obj_ok = !(o.eps_obj > 0.0) ||
@@ -234,6 +281,9 @@ void solve_one(const dvh_lp& lp, const dvh_options& o, const double* x0, const d
         }
       }
       if (r0 < 0.0) r0 = r;
+      if (g_trace)
+        fprintf(stderr, "TRACE it %d kin %d r %.3e r0 %.3e w %.4e pres %.2e dres %.2e gap %.2e\n", it, kin, r, r0, w,
+                last.pres, last.dres, last.gap);
       const bool restart = (r <= o.restart_sufficient * r0) || (r <= o.restart_necessary * r0 && rprev >= 0.0 && r > rprev) ||
                            (kin + 1 >= o.restart_artificial * it);
       if (restart) {
@@ -242,8 +292,18 @@ void solve_one(const dvh_lp& lp, const dvh_options& o, const double* x0, const d
         for (int rr = 0; rr < m; ++rr) ddy += (yp[rr] - ya[rr]) * (yp[rr] - ya[rr]);
         ddx = std::sqrt(ddx);
         ddy = std::sqrt(ddy);
-        if (ddx > 1e-10 && ddy > 1e-10)
-          w = std::exp(o.primal_weight_theta * std::log(ddy / ddx) + (1.0 - o.primal_weight_theta) * std::log(w));
+        if (ddx > 1e-10 && ddy > 1e-10) {
+          if (kp >= 0.0) {  // PID on the log error e = log(ddy / ddx) - log w
+            const double e = std::log(ddy / ddx) - std::log(w);
+            esum += e;
+            const double d = ehave ? e - eprev : 0.0;
+            w = std::exp(std::log(w) + kp * e + ki * esum + kd * d);
+            eprev = e;
+            ehave = true;
+          } else {
+            w = std::exp(o.primal_weight_theta * std::log(ddy / ddx) + (1.0 - o.primal_weight_theta) * std::log(w));
+          }
+        }
         x = xp;
         y = yp;
         xa = xp;
@@ -354,6 +414,7 @@ int dvh_solve_batch(dvh_handle* h, const dvh_lp* lps, int32_t count, dvh_result*
 #pragma omp parallel for schedule(dynamic, 1)
   for (int k = 0; k < count; ++k) {
     Out r;
+    g_trace = getenv("LAB_TRACE") && atoi(getenv("LAB_TRACE")) == k;
     solve_one(lps[k], o, o.warm_start ? out[k].x : nullptr, o.warm_start ? out[k].y : nullptr, r);
     if (out[k].x) std::memcpy(out[k].x, r.x.data(), sizeof(double) * r.x.size());
     if (out[k].y && !r.y.empty()) std::memcpy(out[k].y, r.y.data(), sizeof(double) * r.y.size());
@@ -363,6 +424,8 @@ int dvh_solve_batch(dvh_handle* h, const dvh_lp* lps, int32_t count, dvh_result*
     out[k].gap_rel = r.gap;
     out[k].status = r.status;
     out[k].iters = r.iters;
+    if (g_traj)
+      for (int u = 0; u < 3; ++u) g_traj[3 * k + u] = g_first[u];
   }
   h->timing[0] = h->timing[2] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   h->timing[1] = 0.0;
@@ -410,6 +473,7 @@ int dvh_last_chain_aborts(const dvh_handle*, int32_t* out) {
 }
 const char* dvh_last_warning(const dvh_handle*) { return ""; }
 int dvh_set_kernel_path(dvh_handle*, int) { return DVH_OK; }
+void lab_set_traj(int* t) { g_traj = t; }
 int dvh_outage_coverage(dvh_handle*, const dvh_outage_case*, int32_t, int32_t*, double*) { return DVH_ERR_UNSUPPORTED; }
 int dvh_outage_min_soe(dvh_handle*, const dvh_outage_case*, int32_t, const int32_t*, double*) {
   return DVH_ERR_UNSUPPORTED;

@@ -1,6 +1,6 @@
 #!/bin/bash
-# One PMC counter over one config-3 cold solve (after a warm-up) on the GPU box; the process may abort in teardown
-# under the profiler after writing its output (the long team's cooperative launch), so run one pass per call.
+# One PMC counter pass over one config-3 cold solve (after a warm-up) on the GPU box.  (Round 3's exit crash under the
+# profiler came from the team kernel's cooperative launch, now an ordinary launch: profiles/r04a_chain_exit_crash.txt.)
 # Usage: scripts/pmc_config3.sh <tag> <FETCH_SIZE|WRITE_SIZE> [variant]
 set -o pipefail
 TAG=${1:-r03}; C=${2:-FETCH_SIZE}; V=${3:-dcm_nopv}

@@ -28,3 +28,8 @@ print(json.dumps({"variant": variant, "timing": s.timing(), "paths": s.kernel_st
                   "m": int(pb.desc[0, 1]), "nnz": int(pb.desc[0, 3])}), flush=True)
 del dev
 s.close()
+torch.cuda.synchronize()
+maps = os.environ.get("DVH_DUMP_MAPS")
+if maps:  # the process's mappings, to resolve the PCs of a teardown crash under the profiler
+    with open("/proc/self/maps") as f, open(maps, "w") as g:
+        g.write(f.read())

@@ -138,6 +138,53 @@ def test_weighted_shard_balances_cost_and_covers_once():
     assert parallel.window_cost(big)[0] == pytest.approx(735840 / 5208)
 
 
+def _bench(args, env=None, timeout=240):
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, env=e, capture_output=True,
+                          text=True, timeout=timeout)
+
+
+@pytest.mark.timeout(300)
+def test_bench_gpus_2_launches_two_ranks_itself():
+    """`bench.py --gpus 2` with no outside launcher starts 2 rank processes (gloo here, RCCL on the GPU box), shards
+    the scenarios, gathers every rank's tagged rows and prints ONE line from rank 0 with n_gpus 2."""
+    import json
+    r = _bench(["--gpus", "2", "--dry-run", "--scenarios", "3", "--steps", "2", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    j = json.loads(lines[0])
+    assert j["n_gpus"] == 2 and len(set(j["rank_pids"])) == 2
+    assert j["gather"]["per_rank_windows"] == [36, 36] and j["gather"]["rows"] == 72
+    assert j["gather"]["scenarios"] == list(range(6))  # rank r owns scenarios 3r .. 3r + 2 (weak scaling)
+
+
+@pytest.mark.timeout(300)
+def test_bench_launcher_failure_and_world_mismatch():
+    r = _bench(["--gpus", "2", "--dry-run", "--scenarios", "2"], env={"DVH_DRY_RUN_FAIL_RANK": "1"}, timeout=120)
+    assert r.returncode != 0 and "rank exit statuses" in r.stderr  # rank 0 is ended, not left waiting
+    r = _bench(["--gpus", "1", "--dry-run"], env={"WORLD_SIZE": "2", "RANK": "0"}, timeout=120)
+    assert r.returncode != 0 and "refusing" in r.stderr
+    r = _bench(["--gpus", "1", "--dry-run", "--scenarios", "2", "--steps", "1"])
+    assert r.returncode == 0 and '"n_gpus": 1' in r.stdout
+
+
+def test_untagged_rows_stay_distinct_across_ranks():
+    tags = ["a", "b", "c"]
+    t0 = parallel.tag_array(tags, offset=0)
+    t1 = parallel.tag_array(tags, offset=3)
+    keys = {tuple(r) for r in np.concatenate([t0, t1])}
+    assert len(keys) == 6
+    st = torch.zeros((3, 4), dtype=torch.float64)
+    ist = torch.zeros((3, 2), dtype=torch.int32)
+    rows = parallel.result_rows(st, ist, offset=3)
+    assert rows[:, 7].tolist() == [3.0, 4.0, 5.0]
+
+
 def _async_worker(rank, world, port, out):
     """bench.py --overlap-gather: each step's rows start their all-gather at once (async_op) and are collected at the
     next step, while that step's rows are being made; the last gather is drained before the end."""

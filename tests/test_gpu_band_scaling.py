@@ -65,3 +65,21 @@ def test_band_kernel_reports_crossed_bounds_without_iterating(gpu_solver):
     # reported by the band pass itself: no window was handed on to setup_kernel / the ELL or generic kernels
     ks = gpu_solver.kernel_stats()
     assert ks["band_windows"] == len(lps) and ks["ell_windows"] == 0 and ks["generic_windows"] == 0, ks
+
+
+def test_factors_outside_single_precision_range_leave_the_band_kernel(gpu_solver):
+    """A row scaled by 1e-70 (right-hand side with it: the same LP) needs a row factor near 1e70, which the band
+    kernel's single-precision check copies cannot hold: the band kernel hands the window on (the ELL / generic path
+    keeps its factors in double) and it is still solved to the unscaled window's HiGHS objective."""
+    lps = [lp for g in scenarios.config4([2]) for lp in builder.group_window_lps(g)][:3]
+    lp = lps[1]
+    i = lp.m_eq  # the first DCM (>=) row
+    data, q = lp.data.copy(), lp.q.copy()
+    data[lp.indptr[i]:lp.indptr[i + 1]] *= 1e-70
+    q[i] *= 1e-70
+    lps[1] = dataclasses.replace(lp, data=data, q=q)
+    res = gpu_solver.solve(lps)
+    ks = gpu_solver.kernel_stats()
+    assert ks["band_windows"] == 2 and ks["ell_windows"] + ks["generic_windows"] == 1, ks
+    o, h = _highs(lp)
+    assert res[1].status == 0 and abs(res[1].obj - h["obj"]) <= 1e-5 * abs(h["obj"]), (res[1].obj, h["obj"])

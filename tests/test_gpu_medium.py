@@ -90,3 +90,22 @@ def test_crossed_bounds_medium_window_is_reported_infeasible(gpu_solver):
     assert res[1].status_name == "infeasible" and res[1].iters == 0
     assert res[0].status == 0
     assert gpu_solver.kernel_stats()["chain_windows"] == 1
+
+
+def test_team_launch_abort_hands_windows_to_the_grid_wide_path(monkeypatch):
+    """A team whose exchange outlasts the spin limit (forced here: the test limit aborts at the first wait) aborts: the
+    windows it had not finished are solved on the grid-wide path, every window still comes back OPTIMAL and within
+    1e-5 of HiGHS, the solve returns OK, the abort count is reported (dvh_last_chain_aborts) and the diagnostics go to
+    dvh_last_warning, not dvh_last_error; the next solve resets both."""
+    lps = _lps(scenarios.config4([11], dt=0.25))[:2]
+    monkeypatch.setenv("DVH_CHAIN_SPIN_TICKS", "-1")  # abort at the first exchange that has to wait
+    with BatchSolver(0) as s:
+        res = s.solve(lps)
+        ks = s.kernel_stats()
+        assert ks["chain_aborts"] >= 1, ks
+        assert ks["chain_windows"] + ks["large_windows"] == 2, ks
+        assert "timed out" in s.last_warning()
+        for lp, r in zip(lps, res):
+            _highs_check(lp, r)
+        s.solve(lps[:0] + [lp for lp in _lps(scenarios.config4([11]))[:1]])  # a band-only solve resets them
+        assert s.kernel_stats()["chain_aborts"] == 0 and s.last_warning() == ""

@@ -103,3 +103,21 @@ def test_config5_specs_equal_the_host_specs(gpu_solver):
         assert torch.equal(getattr(a, f), getattr(b, f)), f
     gpu_solver.solve_packed(a)
     assert gpu_solver.kernel_stats()["band_windows"] == a.count == 72  # the band-ICE kernel takes every window
+
+
+def test_host_regenerated_rows_equal_the_host_generator(gpu_solver):
+    """The fallback for scenarios whose wedge test the device reports as undecided (dvh_sweep_draws.ambiguous):
+    their draws and series are regenerated on the host; the sweep stays bit-identical to the host generator."""
+    ids = np.arange(40) * 3 + 1
+    ds = gpu_series.DeviceSeries(ids, gpu_solver)
+    assert len(ds.host_rows) == 0
+    ds.ar[5].zero_()  # what the host path must overwrite
+    ds.P["E"][[5, 17]] = 0.0
+    ds.regenerate_on_host([5, 17])
+    P = scenarios.sweep_parameters(ids)
+    for k, v in ds.P.items():
+        assert np.array_equal(_bits(v), _bits(P[k])), k
+    e = P["eps"]
+    e[:, 1:] *= np.sqrt(1.0 - 0.9 * 0.9)
+    from scipy.signal import lfilter
+    assert np.array_equal(_bits(ds.ar), _bits(lfilter([1.0], [1.0, -0.9], e, axis=1)))
