@@ -246,6 +246,8 @@ void solve_one(const dvh_lp& lp, const dvh_options& o, const double* x0, const d
   double r0 = -1.0, rprev = -1.0;
   const double kp = envd("LAB_KP", -1.0), ki = envd("LAB_KI", 0.0), kd = envd("LAB_KD", 0.0);
   double esum = 0.0, eprev = 0.0;
+  const double wguard = envd("LAB_WGUARD", 0.0);
+  const double wclamp = envd("LAB_WCLAMP", 0.0), wbal = envd("LAB_WBAL", 0.0), wbal_max = envd("LAB_WBAL_MAX", 10.0);
   bool ehave = false;
   g_first[0] = g_first[1] = g_first[2] = -1;
   Kkt last{};
@@ -301,8 +303,18 @@ void solve_one(const dvh_lp& lp, const dvh_options& o, const double* x0, const d
             eprev = e;
             ehave = true;
           } else {
+            const double w_old = w;
             w = std::exp(o.primal_weight_theta * std::log(ddy / ddx) + (1.0 - o.primal_weight_theta) * std::log(w));
+            if (wclamp > 1.0) w = std::min(std::max(w, w_old / wclamp), w_old * wclamp);
+            if (wguard > 0.0 && have && last.pres > 0 && last.dres > 0) {  // no move that worsens the imbalance
+              const double ratio = last.pres / last.dres;
+              if ((ratio > wguard && w < w_old) || (ratio < 1.0 / wguard && w > w_old)) w = w_old;
+            }
           }
+        }
+        if (wbal > 0.0 && have && last.pres > 0 && last.dres > 0) {  // residual balancing on the last KKT
+          const double f = std::pow(last.pres / last.dres, wbal);
+          w *= std::min(std::max(f, 1.0 / wbal_max), wbal_max);
         }
         x = xp;
         y = yp;
