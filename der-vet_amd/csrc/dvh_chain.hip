@@ -907,6 +907,9 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
     };
     // ... and, after it, collect the sharers' and return the totals (lanes u < nsl); false in ok: abort
     auto collect_a = [&](double own, bool& ok) -> double {
+#ifdef DVH_CHAIN_PROBE_NO_TAU_XCHG  // timing probe only (wrong results): the segment's own partials as the totals
+      return own;
+#endif
       if (!poll(0, nA, cA)) {
         ok = false;
         return 0.0;
@@ -932,6 +935,9 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
     // before the dual half-step: wave wl takes the next segment's first ene into XE[L]; wave 0 the previous
     // segment's last step (for the ghost row, in pval[kPollU ..]).  Sets the dead flag on an abort.
     auto poll_b = [&]() {
+#ifdef DVH_CHAIN_PROBE_NO_HOP  // timing probe only (wrong results): no boundary exchange
+      return;
+#endif
       if (!last && wid == wl) {
         if (poll(kPollD, 2, cB)) {
           if (lane == 0) XE[L] = pv64(kPollD);
