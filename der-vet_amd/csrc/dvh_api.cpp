@@ -725,6 +725,12 @@ static int chain_pass(dvh_handle* h, const dvh::Batch& b, const dvh::Work& w, co
       std::vector<int32_t> ab(dvh::chain_abort_bytes(S) / I);
       DVH_HIP(h, hipMemcpyAsync(ab.data(), h->m_abort.p, I * ab.size(), hipMemcpyDeviceToHost, s));
       DVH_HIP(h, sync_stream(h, s));
+      if (getenv("DVH_CHAIN_PROBE_DUMP")) {  // timing probe builds: wave 0's waits per workgroup (wall-clock ticks)
+        for (int gb = 0; gb < 8 * S; ++gb)
+          if (ab[16 + 8 * (size_t)gb + 6] || ab[16 + 8 * (size_t)gb + 7])
+            fprintf(stderr, "PROBE block %d tauwait %d hopwait %d\n", gb, ab[16 + 8 * (size_t)gb + 6],
+                    ab[16 + 8 * (size_t)gb + 7]);
+      }
       if (ab[0] != 0) {
         // a segment exchange outlasted the spin limit: the windows the launch finished keep their results, the
         // others (still marked pending) go to the grid-wide path; the diagnostics stay readable in dvh_last_error

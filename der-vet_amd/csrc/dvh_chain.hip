@@ -44,6 +44,11 @@ namespace dvh {
 namespace {
 
 constexpr int kCB = kChainB;  // threads (and maximum steps) per segment
+#ifndef DVH_CHAIN_TAU_WAVE
+#define DVH_CHAIN_TAU_WAVE 1
+#endif
+constexpr int kTauWave = DVH_CHAIN_TAU_WAVE;  // the wave holding the tau slots (wave 0 holds the init / ghost row)
+static_assert(kTauWave >= 0 && kTauWave < kCB / kWave, "the tau wave exists");
 constexpr int kJSeg = kChainJSeg;  // tau columns per segment
 constexpr int kXSeg = 140;    // granules per segment in the exchange buffer
 // granule offsets inside a segment's area (p = round parity)
@@ -643,6 +648,9 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
     double* xo_g = b.x + W.on;
     double* yo_g = b.y + W.om;
     int cA = 0, cB = 0, cK = 0, cC = 0;  // rounds of each exchange kind (identical in every segment and wave)
+#ifdef DVH_CHAIN_PROBE_TIMING
+    long long t_probe[2] = {0, 0};  // wave 0's waits: tau partials, boundary (timing probe builds only)
+#endif
 
     // ---- poll lists (offset at parity 0 in the low 16 bits, parity stride above): A = the tau partials of the
     //      other segments sharing a slot (by slot, then segment); K = {first-ene image from s+1} + tau image
@@ -705,6 +713,9 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
             }
           }
           if (__all(ok)) break;
+#ifdef DVH_CHAIN_POLL_SLEEP
+          __builtin_amdgcn_s_sleep(DVH_CHAIN_POLL_SLEEP);
+#endif
           ++spins;
           bool late = false;
           if (((spins & 1023u) == 0 || a.spin_ticks < 0) && ((late = wall_clock64() - tw > a.spin_ticks) ||
@@ -728,10 +739,18 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
       return true;
     };
     auto pv64 = [&](int e) { return __hiloint2double((int)pval[e], (int)pval[e + 1]); };
-    // tau total of slot u from this segment's partial and the polled ones (entries at e0 + rel[u] ..), summed in
-    // segment order -- the same additions in every segment holding the slot's rows
+    // tau total of slot u from this segment's partial and the polled ones (entries at e0 + rel[u] ..), the same
+    // additions in every segment holding the slot's rows: lane i holds the partial of segment rlo + i and the wave sums
+    // them with one fixed DPP tree (lane 0's result), so every sharer gets the same bits.  (Summed one after another in
+    // segment order, the ~12 dependent LDS reads and adds of a 5-minute month sat on wave 0's critical path.)
     auto tau_total = [&](int u, double own, int e0) -> double {
       const int rlo = misc[12 + u], rhi = misc[16 + u];
+      if (rhi - rlo < kWave) {
+        const int r = rlo + lane, base = e0 + misc[8 + u];
+        double v = 0.0;
+        if (r <= rhi) v = r == seg ? own : pv64(base + 2 * (r < seg ? lane : lane - 1));
+        return uniform(wave_sum_dpp(v));
+      }
       int e = e0 + misc[8 + u];
       double s = 0.0;
       for (int r = rlo; r <= rhi; ++r) {
@@ -816,7 +835,9 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
     // init row (segment 0: {y, ya, y+, q, coefficient}) or the ghost boundary row ({y, ya, y+, q}, GK)
     constexpr int kRowLane = kWave - 1;
     static_assert(kJSeg < kRowLane, "tau lanes and the row lane are distinct");
-    const bool tlane = wid == 0 && lane < nsl, rlane = wid == 0 && lane == kRowLane;
+    // the tau slots live in wave kTauWave, the init / ghost row in wave 0: their serial work (the tau partials'
+    // reduction, exchange and update; the ghost row's boundary poll and dual step) runs in two waves side by side
+    const bool tlane = wid == kTauWave && lane < nsl, rlane = wid == 0 && lane == kRowLane;
     const bool ilane = rlane && first, glane = rlane && !first;
     int jg0 = 0;
     bool town = false;  // this segment owns the slot (the lowest segment holding its rows): KKT / norm terms
@@ -910,7 +931,14 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
 #ifdef DVH_CHAIN_PROBE_NO_TAU_XCHG  // timing probe only (wrong results): the segment's own partials as the totals
       return own;
 #endif
+#ifdef DVH_CHAIN_PROBE_TIMING
+      const long long c0_ = wall_clock64();
+      const bool pok_ = poll(0, nA, cA);
+      t_probe[0] += wall_clock64() - c0_;
+      if (!pok_) {
+#else
       if (!poll(0, nA, cA)) {
+#endif
         ok = false;
         return 0.0;
       }
@@ -945,7 +973,13 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
           misc[0] = 1;
         }
       }
+#ifdef DVH_CHAIN_PROBE_TIMING
+      const long long c0_ = wall_clock64();
+#endif
       if (!first && wid == 0 && !poll(kPollU, 6, cB) && lane == 0) misc[0] = 1;
+#ifdef DVH_CHAIN_PROBE_TIMING
+      t_probe[1] += wall_clock64() - c0_;
+#endif
     };
     // check reduction: this segment's NV partials (identical in every lane on entry) -> the sums over all segments
     // in segment order, in every lane; false: abort.  A leader reduction: every other segment publishes its partials,
@@ -1039,7 +1073,7 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
       for (int pi = 0; pi <= PI; ++pi) {
         if (pi > 0) {
           ++cA;
-          if (wid == 0) {
+          if (wid == kTauWave) {
             const double own = tau_own();
             publish_a(own);
             bool ok = true;
@@ -1128,10 +1162,35 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
       mv0 = mv1 = mv2 = mv3 = 0.0;
       ++cA;
       ++cB;
+      // the tau columns' update: wave 0 collects the sharers' partials and updates the columns it holds.  The partials
+      // go out at the start of the primal half-step; the collection waits in the dual half-step, beside the boundary
+      // hop's, so the two exchanges' latencies overlap (one extra LDS barrier makes the columns' x-bar visible before
+      // the DCM rows use them).  In the primal half-step instead, the tau exchange stood in front of the boundary hop:
+      // 5.3 us per config-3 DCM iteration, of which 2.5 us the tau exchange (profiles/r04b_chain_anatomy.log).
+      auto tau_step = [&](double own) {
+        bool ok = true;
+        const double kt = collect_a(own, ok);
+        if (!ok && lane == 0) misc[0] = 1;
+        if (tlane) {
+          const double xo = sp[0], xan = sp[1];
+          const double p1 = vmin(vmax(fma(-tau, sp[2] - kt, xo), sp[3]), sp[4]);
+          const double xbt = fma(2.0, p1, -xo);
+          XT[lane] = xbt;
+          sp[0] = fma(ca, xbt, cb * xan);
+          if (CHECK) {
+            if (town) {
+              const double d = xo - p1, da = p1 - xan;
+              mv0 += d * d;
+              mv1 += da * da;
+            }
+            sp[5] = p1;
+          }
+        }
+      };
+      double own = 0.0;
       // ---------------- primal half-step (reflected Halpern, rho = 1)
       {
-        double own = 0.0;
-        if (wid == 0) {
+        if (wid == kTauWave) {
           own = tau_own();
           publish_a(own);
         }
@@ -1153,31 +1212,20 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
         XE[tid] = xb[2];
         publish_b(xb);
         kown(xb, kx);
-        if (wid == 0) {  // tau columns: the sharers' partials arrived while the wave did its own columns
-          bool ok = true;
-          const double kt = collect_a(own, ok);
-          if (!ok && lane == 0) misc[0] = 1;
-          if (tlane) {
-            const double xo = sp[0], xan = sp[1];
-            const double p1 = vmin(vmax(fma(-tau, sp[2] - kt, xo), sp[3]), sp[4]);
-            const double xbt = fma(2.0, p1, -xo);
-            XT[lane] = xbt;
-            sp[0] = fma(ca, xbt, cb * xan);
-            if (CHECK) {
-              if (town) {
-                const double d = xo - p1, da = p1 - xan;
-                mv0 += d * d;
-                mv1 += da * da;
-              }
-              sp[5] = p1;
-            }
-          }
-        }
+#ifdef DVH_CHAIN_TAU_IN_PRIMAL  // A/B: the round-3 placement
+        if (wid == kTauWave) tau_step(own);
+#endif
       }
       lds_barrier();
       // ---------------- dual half-step
       {
         poll_b();
+#ifndef DVH_CHAIN_TAU_IN_PRIMAL
+        if (nsl > 0) {  // uniform over the workgroup: the segment holds tau columns
+          if (wid == kTauWave) tau_step(own);
+          lds_barrier();
+        }
+#endif
         kfin(kx, XE[tid + 1]);
 #pragma unroll
         for (int r = 0; r < NR; ++r) {  // row 0 (SOE) is an equality; the DCM row is >=: its dual stays >= 0
@@ -1363,6 +1411,10 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
     }
     if (tlane && town) xo_g[3 * T + jg0] = sp[5] * dcv[3 * T + jg0];
     if (ilane) yo_g[0] = sp[2] * drv[0];
+#ifdef DVH_CHAIN_PROBE_TIMING
+    if (tid == kTauWave * kWave) abort_word[16 + 8 * (int)blockIdx.x + 6] = (int)t_probe[0];
+    if (tid == 0) abort_word[16 + 8 * (int)blockIdx.x + 7] = (int)t_probe[1];
+#endif
     if (first && tid == 0) {
       b.istats[2 * k] = status;
       b.istats[2 * k + 1] = it;
