@@ -45,6 +45,12 @@ constexpr int kNeedsEll = -2;
 // instead of XP / YP (read back by the same lane at the check).  Layout after TP: [XP YP] (no kLfImages) [XA YA]
 // (kLfAnchors) [RO] (ICE) [CQ] (kLfCosts).
 constexpr int kLfAnchors = 1, kLfCosts = 2, kLfImages = 4;
+#ifndef DVH_BAND_TAU_WAVESUMS
+#define DVH_BAND_TAU_WAVESUMS 0
+#endif
+// tau_parts (below): per-wave sums of one tau column.  Off: the same-box bench A/B found no difference (227.5k vs
+// 227.7k windows/s, profiles/r04g_ab_band_tau_wavesums.log); the round-3 arithmetic (certified) is kept.
+constexpr bool kTauWaveSums = DVH_BAND_TAU_WAVESUMS != 0;
 __host__ __device__ inline size_t band_lds_doubles(int B, int S, bool ice, int LF) {
   const int NW = B / kWave, NC = ice ? 5 : 3, NR = ice ? 4 : 2;
   const size_t SB = (size_t)S * B;
@@ -648,13 +654,20 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
       os[3] = fma(kb[s][1], v[4], fma(kb[s][0], v[3], -rhs(s, 3)));
     }
   };
-  // per-lane partial K'y of the tau columns from the DCM rows' values vd[s] (steps summed in order)
+  // per-lane partial K'y of the tau columns from the DCM rows' values vd[s] (steps summed in order).  One column
+  // (J = 1, kTauWaveSums): every wave reduces its lanes' partials itself (one DPP tree, lane 0's sum) into TP[wid],
+  // so the tau update on wave 0 adds NW values instead of reducing B partials on the iteration's critical path.
   auto tau_parts = [&](const double (&vd)[S]) {
     if (J == 1) {
       double a = kd[0][2] * vd[0];
 #pragma unroll
       for (int s = 1; s < S; ++s) a = fma(kd[s][2], vd[s], a);
-      TP[tid] = a;
+      if constexpr (kTauWaveSums) {
+        a = wave_sum_dpp(a);
+        if (lane == 0) TP[wid] = a;
+      } else {
+        TP[tid] = a;
+      }
     } else {
       for (int j = 0; j < J; ++j) {
         double a = (jt[0] == j ? kd[0][2] : 0.0) * vd[0];
@@ -670,9 +683,17 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
     for (int s = 0; s < S; ++s) vd[s] = vr[s][1];
     tau_parts(vd);
   };
+  // the wave sums of a single tau column, in wave order (every lane reads the same slots: a broadcast)
+  auto tau_waves = [&]() {
+    double a = TP[0];
+#pragma unroll
+    for (int r = 1; r < NW; ++r) a += TP[r];
+    return a;
+  };
   // wave 0: lane j < J gets the sum over all lanes of TP[j][.] (fixed order; uniform per column)
   auto tau_kt = [&]() {
     double res = 0.0;
+    if (kTauWaveSums && J == 1) return lane == 0 ? tau_waves() : 0.0;
     for (int j = 0; j < J; ++j) {
       double a = 0.0;
 #pragma unroll
@@ -846,7 +867,9 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
     double kx[S][NR];  // own-lane part of K x-bar for the dual half-step
     {
       double ta0 = 0.0, ta1 = 0.0;
-      if constexpr (W0) {  // (0 + a == a: the first partials start the two chains)
+      if constexpr (W0 && kTauWaveSums) {
+        ta0 = tau_waves();
+      } else if constexpr (W0) {  // (0 + a == a: the first partials start the two chains)
         ta0 = TP[lane];
         if (NW > 1) ta1 = TP[kWave + lane];
 #pragma unroll
@@ -885,7 +908,9 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
         kown_q(s, xb[s], kx[s]);
         if (s < S - 1) kfin_next(s, kx[s], xb[s < S - 1 ? s + 1 : s][2]);  // the next step is the lane's own
       }
-      if constexpr (W0) {
+      if constexpr (W0 && kTauWaveSums) {
+        tau_update(ta0, ca, cb, chk_tag);
+      } else if constexpr (W0) {
         tau_update(uniform(wave_sum_dpp(ta0 + ta1)), ca, cb, chk_tag);
       } else {
         if (wid == 0 && J > 1) tau_update(tau_kt(), ca, cb, chk_tag);
@@ -901,33 +926,39 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
 #pragma unroll
       for (int s = 0; s < S; ++s) xtv[s] = lds_ld(xta[s]);
       kfin_next(S - 1, kx[S - 1], xen);
+      auto row_step = [&](int s, int r) __attribute__((always_inline)) {
+        // row 0 (SOE) is an equality; DCM / ICE rows are >=: duals stay >= 0
+        if (!CHECK && r == 0) {  // equality row, no image needed: 2 (y - sigma Kx) - y = y - 2 sigma Kx
+          y[s][0] = fma(ca, fma(sigma2n, kx[s][0], y[s][0]), cb * ayv(s, 0));
+          return;
+        }
+        double p1 = fma(-sigma, kx[s][r], y[s][r]);
+        if (r > 0) p1 = vmax(p1, 0.0);
+        if (CHECK) {
+          const double d = y[s][r] - p1, da = p1 - ayv(s, r);
+          mv2 += d * d;
+          mv3 += da * da;
+          if constexpr (LI) {
+            const int i = row_of(s, r);
+            if (i >= 0) yim[opaque(i)] = p1;
+          } else {
+            YP[(r * S + s) * B + tid] = p1;
+          }
+        }
+        y[s][r] = fma(ca, fma(2.0, p1, -y[s][r]), cb * ayv(s, r));
+      };
+      // the >= rows first: their duals feed the tau partials, whose wave reduction then has the SOE rows' work
+      // beside it
 #pragma unroll
       for (int s = 0; s < S; ++s) {
         kx[s][1] = fma(kd[s][2], xtv[s], kx[s][1]);  // kfin_tau
 #pragma unroll
-        for (int r = 0; r < NR; ++r) {  // row 0 (SOE) is an equality; DCM / ICE rows are >=: duals stay >= 0
-          if (!CHECK && r == 0) {  // equality row, no image needed: 2 (y - sigma Kx) - y = y - 2 sigma Kx
-            y[s][0] = fma(ca, fma(sigma2n, kx[s][0], y[s][0]), cb * ayv(s, 0));
-            continue;
-          }
-          double p1 = fma(-sigma, kx[s][r], y[s][r]);
-          if (r > 0) p1 = vmax(p1, 0.0);
-          if (CHECK) {
-            const double d = y[s][r] - p1, da = p1 - ayv(s, r);
-            mv2 += d * d;
-            mv3 += da * da;
-            if constexpr (LI) {
-              const int i = row_of(s, r);
-              if (i >= 0) yim[opaque(i)] = p1;
-            } else {
-              YP[(r * S + s) * B + tid] = p1;
-            }
-          }
-          y[s][r] = fma(ca, fma(2.0, p1, -y[s][r]), cb * ayv(s, r));
-        }
+        for (int r = 1; r < NR; ++r) row_step(s, r);
       }
-      YS[tid + 1] = y[S - 1][0];
       if (J > 0) tau_parts_of(y);
+#pragma unroll
+      for (int s = 0; s < S; ++s) row_step(s, 0);
+      YS[tid + 1] = y[S - 1][0];
       if (W0 || wid == 0) {  // init row (lane kInitLane): ene_0 = target
         if (ilane) {
           const double y0 = sp[0], ya0 = sp[1];
