@@ -294,6 +294,10 @@ def main():
                     help="seeded: every seed-stride-th scenario (battery-energy order) solved cold, the rest warm "
                          "from their nearest seed (dervet_hip/sweep.py); cold: every window from zero")
     ap.add_argument("--seed-stride", type=int, default=32)
+    ap.add_argument("--blend", type=int, default=4,
+                    help="seeded schedule: every warm window starts from the inverse-distance-weighted blend of its "
+                         "BLEND nearest seeds' transferred solutions (1: the nearest seed alone)")
+    ap.add_argument("--blend-power", type=float, default=1.0, help="blend weights 1 / distance^POWER")
     ap.add_argument("--no-cold-ref", action="store_true", help="skip the untimed all-cold reference solve")
     ap.add_argument("--kkt-predict", type=int, default=4,
                     help="dvh_options.kkt_predict for cold solves (--schedule cold and the cold reference; the seeded "
@@ -361,7 +365,8 @@ def main():
         make = functools.partial(scenarios.config4, spec=args.build == "device")
     if args.schedule == "seeded":
         P = series.parameters() if series is not None else scenarios.sweep_parameters(scen)
-        sweep = SeededSweep(make, scen, P["E"], stride=args.seed_stride, features=scenarios.sweep_features(P))
+        sweep = SeededSweep(make, scen, P["E"], stride=args.seed_stride, features=scenarios.sweep_features(P),
+                            blend=args.blend, blend_power=args.blend_power)
         t1 = time.time()
         dev = sweep.to_device(solver, f"cuda:{local}")
         desc = sweep.desc
@@ -494,7 +499,7 @@ def main():
     schedule = {"kind": args.schedule}
     if sweep is not None:
         ns = sweep.n_seed
-        schedule.update(seed_stride=args.seed_stride, seed_windows=ns, iters_mean_seed=round(float(iters[:ns].mean()), 1),
+        schedule.update(seed_stride=args.seed_stride, blend=sweep.blend, seed_windows=ns, iters_mean_seed=round(float(iters[:ns].mean()), 1),
                         iters_mean_warm=round(float(iters[ns:].mean()), 1) if count > ns else None,
                         pdhg_launches_per_step=2 if count > ns else 1)
     if sweep is not None and not args.no_cold_ref:
@@ -582,8 +587,9 @@ def main():
         "config": {"workload": f"config4 sweep: {S:,} scenarios x 12 monthly windows per GPU (battery + PV + "
                                "DCM + retailETS, T=672-744 h)",
                    "scenarios_per_gpu": S, "windows_per_gpu": count, "eps_rel_kkt": 1e-6, **opts,
-                   "schedule": (f"seeded (1 in {args.seed_stride} scenarios cold, the rest warm from the nearest "
-                                f"seed in (log E/load, duration, PV/load); warm phase {WARM_OPTIONS})" if sweep is not None else "cold"),
+                   "schedule": (f"seeded (1 in {args.seed_stride} scenarios cold, the rest warm from the "
+                                f"inverse-distance-weighted blend of the {sweep.blend} nearest seeds in (log E/load, "
+                                f"duration, PV/load); warm phase {WARM_OPTIONS})" if sweep is not None else "cold"),
                    "parallelism": f"dp{world} (independent windows, 1 RCCL all-gather of results)"},
         "scenario_years_per_s": round(value / 12.0, 2),
         "iters_mean": round(float(iters.mean()), 1),

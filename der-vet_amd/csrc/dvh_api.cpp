@@ -67,7 +67,7 @@ struct dvh_handle {
                                                   // ran grid-wide); dvh_last_chain_aborts
   std::string warn;                               // diagnostics of the last solve's fallbacks (dvh_last_warning)
   DevBuf o_data, o_cases, o_len, o_hist, o_soe;  // reliability sweep
-  DevBuf s_pairs, s_bad;                          // seeded-sweep warm transfer (dvh_sweep.hip)
+  DevBuf s_pairs, s_wts, s_bad;                   // seeded-sweep warm transfer (dvh_sweep.hip)
   DevBuf g_seeds, g_word;                         // scenario series generator (dvh_series.hip)
   DevBuf d_route;                                 // cascade lists' counts / ELL widths (dvh_route.hip)
   int32_t* route_host = nullptr;                  // their pinned host mirror (one small read-back per tier)
@@ -238,7 +238,7 @@ int dvh_destroy(dvh_handle* h) {
                     &h->w_qs, &h->w_vbuf, &h->w_wbuf, &h->w_tmpc, &h->w_tmpr, &h->w_longk, &h->w_longt, &h->w_scal,
                     &h->w_fc, &h->w_fr,
                     &h->m_list, &h->m_plan, &h->m_pos, &h->m_xbuf, &h->m_abort, &h->o_data, &h->o_cases, &h->o_len, &h->o_hist, &h->o_soe,
-                    &h->s_pairs, &h->s_bad, &h->g_seeds, &h->g_word, &h->d_route};
+                    &h->s_pairs, &h->s_wts, &h->s_bad, &h->g_seeds, &h->g_word, &h->d_route};
   for (DevBuf* b : bufs) b->release();
   if (h->route_host) hipHostFree(h->route_host);
   for (auto& e : h->ev)
@@ -256,37 +256,57 @@ int dvh_destroy(dvh_handle* h) {
 const char* dvh_last_error(const dvh_handle* h) { return h ? h->err.c_str() : "null handle"; }
 const char* dvh_last_warning(const dvh_handle* h) { return h ? h->warn.c_str() : "null handle"; }
 
-int dvh_warm_transfer(dvh_handle* h, const dvh_packed* b, const int32_t* pairs, int32_t count) {
+int dvh_warm_transfer_blend(dvh_handle* h, const dvh_packed* b, const int32_t* rows, const double* weights,
+                            int32_t count, int32_t q) {
   if (!h) return DVH_ERR_ARG;
-  if (count < 0 || (count > 0 && (!b || !pairs))) return fail(h, DVH_ERR_ARG, "warm transfer: bad arguments");
+  if (q < 1 || q > dvh::kMaxBlend) return fail(h, DVH_ERR_ARG, "warm transfer: partners per window must be 1..8");
+  if (count < 0 || (count > 0 && (!b || !rows || !weights))) return fail(h, DVH_ERR_ARG, "warm transfer: bad arguments");
   if (count == 0) return DVH_OK;
   if (!b->desc || !b->c || !b->u || !b->x || !b->y) return fail(h, DVH_ERR_ARG, "null device array in packed batch");
-  // every window written once, and no partner written (a workgroup would read it while another writes it)
+  const size_t R = (size_t)q + 2;
+  // every window written once, no partner written (a workgroup would read it while another writes it), finite weights
   std::vector<char> target((size_t)std::max(b->count, 0), 0);
   for (int32_t i = 0; i < count; ++i) {
-    const int32_t w = pairs[3 * (size_t)i], p = pairs[3 * (size_t)i + 1];
-    if (w < 0 || w >= b->count || p < 0 || p >= b->count || w == p)
-      return fail(h, DVH_ERR_ARG, "warm transfer: pair " + std::to_string(i) + " names no window / itself");
+    const int32_t w = rows[R * i];
+    if (w < 0 || w >= b->count)
+      return fail(h, DVH_ERR_ARG, "warm transfer: row " + std::to_string(i) + " names no window");
+    for (int32_t k = 0; k < q; ++k) {
+      const int32_t p = rows[R * i + 1 + k];
+      if (p < 0 || p >= b->count || w == p)
+        return fail(h, DVH_ERR_ARG, "warm transfer: pair " + std::to_string(i) + " names no window / itself");
+      if (!std::isfinite(weights[(size_t)q * i + k]))
+        return fail(h, DVH_ERR_ARG, "warm transfer: weight of row " + std::to_string(i) + " is not finite");
+    }
     if (target[w]) return fail(h, DVH_ERR_ARG, "warm transfer: window " + std::to_string(w) + " listed twice");
     target[w] = 1;
   }
   for (int32_t i = 0; i < count; ++i)
-    if (target[pairs[3 * (size_t)i + 1]])
-      return fail(h, DVH_ERR_ARG, "warm transfer: partner of pair " + std::to_string(i) + " is itself a listed window");
+    for (int32_t k = 0; k < q; ++k)
+      if (target[rows[R * i + 1 + k]])
+        return fail(h, DVH_ERR_ARG, "warm transfer: partner of pair " + std::to_string(i) + " is itself a listed window");
   DVH_HIP(h, hipSetDevice(h->device));
   hipStream_t s = h->stream;
-  DVH_HIP(h, h->s_pairs.ensure(sizeof(int32_t) * 3 * (size_t)count));
+  DVH_HIP(h, h->s_pairs.ensure(sizeof(int32_t) * R * (size_t)count));
+  DVH_HIP(h, h->s_wts.ensure(sizeof(double) * (size_t)q * (size_t)count));
   DVH_HIP(h, h->s_bad.ensure(sizeof(int32_t)));
-  DVH_HIP(h, hipMemcpyAsync(h->s_pairs.p, pairs, sizeof(int32_t) * 3 * (size_t)count, hipMemcpyHostToDevice, s));
+  DVH_HIP(h, hipMemcpyAsync(h->s_pairs.p, rows, sizeof(int32_t) * R * (size_t)count, hipMemcpyHostToDevice, s));
+  DVH_HIP(h, hipMemcpyAsync(h->s_wts.p, weights, sizeof(double) * (size_t)q * (size_t)count, hipMemcpyHostToDevice, s));
   DVH_HIP(h, hipMemsetAsync(h->s_bad.p, 0, sizeof(int32_t), s));
-  hipError_t e = dvh::launch_warm_transfer(b->desc, b->c, b->u, b->x, b->y, h->s_pairs.as<int32_t>(), count,
-                                           h->s_bad.as<int32_t>(), s);
+  hipError_t e = dvh::launch_warm_transfer(b->desc, b->c, b->u, b->x, b->y, h->s_pairs.as<int32_t>(),
+                                           h->s_wts.as<double>(), q, count, h->s_bad.as<int32_t>(), s);
   if (e != hipSuccess) return hip_fail(h, e, "launch_warm_transfer");
   int32_t bad = 0;
   DVH_HIP(h, hipMemcpyAsync(&bad, h->s_bad.p, sizeof(int32_t), hipMemcpyDeviceToHost, s));
   DVH_HIP(h, hipStreamSynchronize(s));
   if (bad) return fail(h, DVH_ERR_ARG, "warm transfer: " + std::to_string(bad) + " pair(s) of different LP shape");
   return DVH_OK;
+}
+
+int dvh_warm_transfer(dvh_handle* h, const dvh_packed* b, const int32_t* pairs, int32_t count) {
+  if (!h) return DVH_ERR_ARG;
+  if (count < 0 || (count > 0 && (!b || !pairs))) return fail(h, DVH_ERR_ARG, "warm transfer: bad arguments");
+  const std::vector<double> ones((size_t)std::max(count, 0), 1.0);  // one partner, weight 1: the plain transfer
+  return dvh_warm_transfer_blend(h, b, pairs, ones.data(), count, 1);
 }
 
 int dvh_series_draws(dvh_handle* h, const dvh_sweep_draws* d) {

@@ -149,10 +149,11 @@ int chain_team_count(int S, int PT);
 hipError_t launch_chain(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, const int32_t* pos, int npos,
                         const int32_t* plan, int PT, int S, void* xbuf, int32_t* abort_word, long long spin_ticks,
                         hipStream_t s);
-// Seeded-sweep warm starts (dvh_sweep.hip): pairs[count][3] = {window, partner window, T (> 0: battery + DCM dual
-// scaling) }; bad counts pairs whose windows differ in shape (skipped).
+// Seeded-sweep warm starts (dvh_sweep.hip): rows[count][q + 2] = {window, partner windows (q), T (> 0: battery + DCM
+// dual scaling)}, wts[count][q] the partners' weights; bad counts rows whose windows differ in shape (skipped).
+constexpr int kMaxBlend = 8;  // partners per window
 hipError_t launch_warm_transfer(const int64_t* desc, const double* c, const double* u, double* x, double* y,
-                                const int32_t* pairs, int count, int32_t* bad, hipStream_t s);
+                                const int32_t* rows, const double* wts, int q, int count, int32_t* bad, hipStream_t s);
 // Synthetic scenario series (dvh_series.hip): numpy-identical draws, one thread per scenario (ambiguous counts
 // scenarios with a wedge test too close to call), and the device builder's inputs of G windows (bad counts rows out of
 // range).

@@ -104,6 +104,8 @@ SYMBOLS = {
     "dvh_solve_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(LP), ctypes.c_int32, ctypes.POINTER(Result)]),
     "dvh_solve_packed_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Packed), ctypes.c_void_p]),
     "dvh_warm_transfer": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Packed), ctypes.c_void_p, ctypes.c_int32]),
+    "dvh_warm_transfer_blend": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Packed), ctypes.c_void_p,
+                                               ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]),
     "dvh_build_battery_group": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(BatteryGroup), ctypes.POINTER(Packed),
                                                ctypes.c_int32]),
     "dvh_synchronize": (ctypes.c_int, [ctypes.c_void_p]),

@@ -48,8 +48,7 @@ def seed_split(keys, stride, features=None, cover=False):
     pick = np.where(np.abs(seed_pos[left] - rest_pos) <= np.abs(seed_pos[near] - rest_pos), left, near)
     seeds, rest = order[seed_pos], order[rest_pos]
     if features is not None:
-        f = np.asarray(features, np.float64).reshape(S, -1)
-        f = (f - f.mean(0)) / np.where(f.std(0) > 0, f.std(0), 1.0)
+        f = standardise(features, S)
         if cover:  # greedy farthest-point seeds in feature space (same count), starting at the key-order seed
             ns = len(seeds)
             sel = [int(seeds[0])]
@@ -64,6 +63,42 @@ def seed_split(keys, stride, features=None, cover=False):
             rest = np.nonzero(mask)[0]
         pick = _nearest(f[rest], f[seeds])
     return seeds, rest, pick
+
+
+def standardise(features, S=None):
+    """Features [S, d] scaled to zero mean and unit variance per column (constant columns left unscaled)."""
+    f = np.asarray(features, np.float64)
+    f = f.reshape(S if S is not None else f.shape[0], -1)
+    return (f - f.mean(0)) / np.where(f.std(0) > 0, f.std(0), 1.0)
+
+
+def seed_partners(fr, fs, q, first=None, power=1.0):
+    """The q nearest seeds of every row of fr among the rows of fs (exact squared distances, nearest first; `first`:
+    the nearest already known, e.g. from ``_nearest``) and inverse-distance weights 1 / d^power summing to 1 (a seed at
+    distance 0 takes the whole weight).  Returns (idx [R, q] int64, w [R, q] float64)."""
+    fr = np.ascontiguousarray(fr, np.float64)
+    fs = np.ascontiguousarray(fs, np.float64)
+    q = max(1, min(int(q), len(fs)))
+    R = len(fr)
+    idx = np.zeros((R, q), np.int64)
+    w = np.zeros((R, q), np.float64)
+    for a in range(0, R, 2048):
+        d = ((fr[a:a + 2048, None, :] - fs[None, :, :]) ** 2).sum(-1)
+        part = np.argsort(d, axis=1, kind="stable")[:, :q]
+        if first is not None:  # keep the exact argmin of _nearest first (ties broken the same way)
+            f0 = np.asarray(first[a:a + 2048], np.int64)
+            rest = np.where(part == f0[:, None], -1, part)
+            rows = []
+            for i in range(len(part)):
+                o = [int(f0[i])] + [int(v) for v in rest[i] if v >= 0]
+                rows.append(o[:q])
+            part = np.array(rows, np.int64)
+        dd = np.sqrt(np.take_along_axis(d, part, 1))
+        inv = np.where(dd > 0, 1.0 / np.where(dd > 0, dd, 1.0) ** power, np.inf)
+        ww = np.where(np.isinf(inv).any(1, keepdims=True), np.isinf(inv).astype(np.float64), inv)
+        w[a:a + 2048] = ww / ww.sum(1, keepdims=True)
+        idx[a:a + 2048] = part
+    return idx, w
 
 
 def _nearest(fr, fs):
@@ -112,11 +147,12 @@ class _Transfer:
     m: int
     g_rest: int
     g_seed: int
-    local: object        # [g_rest] index into the seed group
+    local: object        # [g_rest] index into the seed group, or [g_rest, q] for a blend of q partners
     battery_dcm: bool    # x = [ch, dis, ene, tau (1)]: scale the duals too
     T: int
     w_rest: int = 0      # window index of the rest group's first window (packing order)
     w_seed: int = 0      # and of the seed group's
+    weights: object = None  # [g_rest, q] the partners' weights (blend), None: one partner
 
 
 def _scenarios_of(g):
@@ -141,11 +177,12 @@ def _same_pattern(a, b):
     return a.T == b.T and np.array_equal(a.dcm_t, b.dcm_t) and np.array_equal(a.dcm_j, b.dcm_j)
 
 
-def plan(seed_groups, rest_groups, partner_of):
+def plan(seed_groups, rest_groups, partner_of, blend=None):
     """Transfers from the packed seed windows (packed first) to the rest windows (packed after them).
 
-    partner_of: dict rest scenario id -> seed scenario id.  Groups are matched by window id (tag[1]) and must
-    share the CSR pattern."""
+    partner_of: dict rest scenario id -> seed scenario id (the nearest).  blend (optional): dict rest scenario id ->
+    (seed scenario ids [q], weights [q]) -- the window starts from the weighted blend of those partners.  Groups are
+    matched by window id (tag[1]) and must share the CSR pattern."""
     out = []
     on = om = wk = 0
     seed_at = {}
@@ -182,12 +219,41 @@ def plan(seed_groups, rest_groups, partner_of):
         if len(want) and (len(ss) == 0 or not np.array_equal(ss[j], want)):
             raise KeyError(f"a partner seed is not in the seed group of window {wid!r}")
         local = so[j].astype(np.int64)
+        weights = None
+        if blend is not None:  # every partner of the blend, looked up in the seed group as the nearest one is
+            bq = [blend[int(r)] for r in rs]
+            want_q = np.array([b[0] for b in bq], np.int64).reshape(len(rs), -1)
+            jq = np.minimum(np.searchsorted(ss, want_q), max(len(ss) - 1, 0))
+            if want_q.size and (len(ss) == 0 or not np.array_equal(ss[jq], want_q)):
+                raise KeyError(f"a blend partner is not in the seed group of window {wid!r}")
+            local = so[jq].astype(np.int64)
+            weights = np.array([b[1] for b in bq], np.float64).reshape(len(rs), -1)
         out.append(_Transfer(on, om, son, som, g.n, g.m, g.G, sg.G, local,
-                             g.n == 3 * g.T + 1 and g.J == 1, g.T, wk, swk))
+                             g.n == 3 * g.T + 1 and g.J == 1, g.T, wk, swk, weights))
         on += g.G * g.n
         om += g.G * g.m
         wk += g.G
     return out
+
+
+def transfer_rows(tr_list):
+    """(int32 [windows][q + 2] {window, partner windows (q), T}, float64 [windows][q] weights) of blended transfers,
+    for ``dvh_warm_transfer_blend``."""
+    rows, wts = [], []
+    for t in tr_list:
+        loc = np.asarray(t.local, np.int64).reshape(t.g_rest, -1)
+        q = loc.shape[1]
+        r = np.empty((t.g_rest, q + 2), np.int32)
+        r[:, 0] = t.w_rest + np.arange(t.g_rest)
+        r[:, 1:q + 1] = t.w_seed + loc
+        r[:, q + 1] = t.T if t.battery_dcm else 0
+        rows.append(r)
+        wts.append(np.ones((t.g_rest, 1)) if t.weights is None else np.asarray(t.weights, np.float64))
+    if not rows:
+        return np.zeros((0, 3), np.int32), np.zeros((0, 1))
+    if len({r.shape[1] for r in rows}) != 1:
+        raise ValueError("transfers with different partner counts")
+    return np.ascontiguousarray(np.concatenate(rows)), np.ascontiguousarray(np.concatenate(wts))
 
 
 def transfer_pairs(tr_list):
@@ -195,6 +261,8 @@ def transfer_pairs(tr_list):
     ``dvh_warm_transfer`` (the same warm starts as ``transfer``, in one launch on the solver's stream)."""
     parts = []
     for t in tr_list:
+        if t.weights is not None:
+            raise ValueError("blended transfers: use transfer_rows / dvh_warm_transfer_blend")
         p = np.empty((t.g_rest, 3), np.int32)
         p[:, 0] = t.w_rest + np.arange(t.g_rest)
         p[:, 1] = t.w_seed + np.asarray(t.local, np.int64)
@@ -207,6 +275,13 @@ def transfer_device(solver, tr_list, pb, pairs=None):
     """``transfer`` for a device-resident batch through the library (``dvh_warm_transfer``): one launch on the
     solver's stream, ordered after the seed solve and before the warm one; no host-side tensor work."""
     import ctypes
+    if pairs is None and any(t.weights is not None for t in tr_list):  # blends of several partners
+        rows, wts = transfer_rows(tr_list)
+        p = pb.as_ctypes()
+        solver._check(solver._lib.dvh_warm_transfer_blend(
+            solver._h, ctypes.byref(p), rows.ctypes.data_as(ctypes.c_void_p), wts.ctypes.data_as(ctypes.c_void_p),
+            len(rows), rows.shape[1] - 2), "dvh_warm_transfer_blend")
+        return
     pairs = transfer_pairs(tr_list) if pairs is None else np.ascontiguousarray(pairs, np.int32)
     if pairs.ndim != 2 or pairs.shape[1] != 3:
         raise ValueError(f"pairs must be [count, 3] {{window, partner, T}}, got shape {pairs.shape}")
@@ -220,22 +295,33 @@ def transfer(tr_list, x, y, c, u):
     solutions already in x / y.  c, u: the packed objective and upper bounds."""
     import torch
     for t in tr_list:
-        loc = torch.as_tensor(t.local, device=x.device)
-        Xs = x[t.on_seed:t.on_seed + t.g_seed * t.n].view(t.g_seed, t.n)[loc]
-        Us = u[t.on_seed:t.on_seed + t.g_seed * t.n].view(t.g_seed, t.n)[loc]
+        locs = np.asarray(t.local, np.int64).reshape(t.g_rest, -1)
+        wts = None if t.weights is None else torch.as_tensor(np.asarray(t.weights, np.float64), device=x.device)
         Ur = u[t.on_rest:t.on_rest + t.g_rest * t.n].view(t.g_rest, t.n)
-        ok = torch.isfinite(Ur) & torch.isfinite(Us) & (Us > 0)
-        ratio = torch.where(ok, Ur / torch.where(ok, Us, torch.ones_like(Us)), torch.ones_like(Us))
-        x[t.on_rest:t.on_rest + t.g_rest * t.n].view(t.g_rest, t.n).copy_(Xs * ratio)
-        Ys = y[t.om_seed:t.om_seed + t.g_seed * t.m].view(t.g_seed, t.m)[loc]
-        if t.battery_dcm:
-            T = t.T
-            Cs = c[t.on_seed:t.on_seed + t.g_seed * t.n].view(t.g_seed, t.n)[loc]
-            Cr = c[t.on_rest:t.on_rest + t.g_rest * t.n].view(t.g_rest, t.n)
-            cd = Cr[:, 3 * T:3 * T + 1] / Cs[:, 3 * T:3 * T + 1].clamp(min=1e-12)
-            cp = Cr[:, :T].abs().mean(1, keepdim=True) / Cs[:, :T].abs().mean(1, keepdim=True).clamp(min=1e-12)
-            Ys = torch.cat([Ys[:, :T + 1] * cp, Ys[:, T + 1:] * cd], dim=1)
-        y[t.om_rest:t.om_rest + t.g_rest * t.m].view(t.g_rest, t.m).copy_(Ys)
+        Xb = Yb = None
+        for k in range(locs.shape[1]):  # partners in row order (one: the plain transfer)
+            loc = torch.as_tensor(locs[:, k], device=x.device)
+            Xs = x[t.on_seed:t.on_seed + t.g_seed * t.n].view(t.g_seed, t.n)[loc]
+            Us = u[t.on_seed:t.on_seed + t.g_seed * t.n].view(t.g_seed, t.n)[loc]
+            ok = torch.isfinite(Ur) & torch.isfinite(Us) & (Us > 0)
+            ratio = torch.where(ok, Ur / torch.where(ok, Us, torch.ones_like(Us)), torch.ones_like(Us))
+            Xk = Xs * ratio
+            Ys = y[t.om_seed:t.om_seed + t.g_seed * t.m].view(t.g_seed, t.m)[loc]
+            if t.battery_dcm:
+                T = t.T
+                Cs = c[t.on_seed:t.on_seed + t.g_seed * t.n].view(t.g_seed, t.n)[loc]
+                Cr = c[t.on_rest:t.on_rest + t.g_rest * t.n].view(t.g_rest, t.n)
+                cd = Cr[:, 3 * T:3 * T + 1] / Cs[:, 3 * T:3 * T + 1].clamp(min=1e-12)
+                cp = Cr[:, :T].abs().mean(1, keepdim=True) / Cs[:, :T].abs().mean(1, keepdim=True).clamp(min=1e-12)
+                Ys = torch.cat([Ys[:, :T + 1] * cp, Ys[:, T + 1:] * cd], dim=1)
+            if wts is None:
+                Xb, Yb = Xk, Ys
+            else:
+                wk = wts[:, k:k + 1]
+                Xb = wk * Xk if Xb is None else Xb + wk * Xk
+                Yb = wk * Ys if Yb is None else Yb + wk * Ys
+        x[t.on_rest:t.on_rest + t.g_rest * t.n].view(t.g_rest, t.n).copy_(Xb)
+        y[t.om_rest:t.om_rest + t.g_rest * t.m].view(t.g_rest, t.m).copy_(Yb)
 
 
 def sub_batch(pb, a, b):
@@ -253,16 +339,26 @@ class SeededSweep:
     (``functools.partial(scenarios.config4, spec=True)``: then ``packed`` is None and ``to_device`` expands the
     windows on the GPU, lp/gpu_builder.py); keys: similarity key per scenario (same order as `scenario_ids`)."""
 
-    def __init__(self, make_groups, scenario_ids, keys, stride=8, features=None, cover=False):
+    def __init__(self, make_groups, scenario_ids, keys, stride=8, features=None, cover=False, blend=1,
+                 blend_power=1.0):
         from .lp import builder
         ids = np.asarray(list(scenario_ids), np.int64)
         seed_i, rest_i, pick = seed_split(keys, stride, features, cover)
         self.seed_ids, self.rest_ids = ids[seed_i], ids[rest_i]
         partner_of = {int(r): int(self.seed_ids[p]) for r, p in zip(self.rest_ids, pick)}
+        # blend > 1 (with features): every rest window starts from the inverse-distance-weighted blend of its `blend`
+        # nearest seeds' transferred solutions (algorithm lab, 2,048 scenarios: warm iterations 2,063 -> 1,978 with 3)
+        bl = None
+        self.blend = 1
+        if blend > 1 and features is not None and len(seed_i) > 1 and len(rest_i):
+            f = standardise(features, len(ids))
+            idx, w = seed_partners(f[rest_i], f[seed_i], blend, first=pick, power=blend_power)
+            self.blend = idx.shape[1]
+            bl = {int(r): (self.seed_ids[idx[i]], w[i]) for i, r in enumerate(self.rest_ids)}
         sg = make_groups(self.seed_ids)
         rg = make_groups(self.rest_ids) if len(self.rest_ids) else []
-        self.transfers = plan(sg, rg, partner_of)
-        self.pairs = transfer_pairs(self.transfers)
+        self.transfers = plan(sg, rg, partner_of, bl)
+        self.pairs = transfer_pairs(self.transfers) if bl is None else None
         self.n_seed = sum(g.G for g in sg)
         self.tags = [t for g in sg + rg for t in g.tags]
         self.specs = None

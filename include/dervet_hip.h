@@ -261,6 +261,12 @@ int dvh_series_windows(dvh_handle* h, const dvh_window_series* w);
  * naming no window, a window listed twice, a partner that is itself listed (checked before the launch), or windows
  * of different shape (those pairs are skipped, the others applied). */
 int dvh_warm_transfer(dvh_handle* h, const dvh_packed* batch, const int32_t* pairs, int32_t count);
+/* The same from a weighted blend of q partners (1 <= q <= 8): rows[count][q + 2] = {window, partner_1 .. partner_q, T},
+ * weights[count][q] (host; normally summing to 1): x = sum_k w_k x_k', y = sum_k w_k y_k' with x_k', y_k' partner k's
+ * solution transferred as dvh_warm_transfer does (summed in row order).  q = 1 with weight 1 is dvh_warm_transfer bit
+ * for bit.  DVH_ERR_ARG as dvh_warm_transfer, and for q out of range or a weight that is not finite. */
+int dvh_warm_transfer_blend(dvh_handle* h, const dvh_packed* batch, const int32_t* rows, const double* weights,
+                            int32_t count, int32_t q);
 
 /* Timing of the most recent solve on the handle's stream (HIP events, milliseconds):
  * [0] whole solve, [1] setup kernel (transpose + scaling + power iteration), [2] PDHG kernel. */

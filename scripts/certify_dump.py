@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--opt", action="append", default=[], help="dvh_options field=value (repeatable)")
     ap.add_argument("--no-cold", action="store_true")
     ap.add_argument("--lib", default=None, help="alternative libdervet_hip.so (A/B builds)")
+    ap.add_argument("--blend", type=int, default=1, help="warm starts blended from this many nearest seeds")
     args = ap.parse_args()
     if args.lib:
         from dervet_hip import _lib
@@ -38,7 +39,8 @@ def main():
     scen = range(args.scenarios)
     t0 = time.time()
     P = scenarios.sweep_parameters(scen)
-    sweep = SeededSweep(scenarios.config4, scen, P["E"], stride=32, features=scenarios.sweep_features(P))
+    sweep = SeededSweep(scenarios.config4, scen, P["E"], stride=32, features=scenarios.sweep_features(P),
+                        blend=args.blend)
     dev = sweep.packed.to_torch("cuda:0").alloc_outputs()
     print(f"built {dev.count} windows in {time.time() - t0:.1f} s", flush=True)
     solver = BatchSolver(0)

@@ -105,7 +105,19 @@ def main():
     groups = scenarios.config4(range(S))
     wins = [[lp for lp in builder.group_window_lps(g)] for g in groups]  # [window id][scenario]
     P = scenarios.sweep_parameters(range(S))
-    seeds, rest, pick = seed_split(P["E"], 32, scenarios.sweep_features(P))
+    stride = int(os.environ.get("LAB_STRIDE", "32"))
+    seeds, rest, pick = seed_split(P["E"], stride, scenarios.sweep_features(P))
+    warm_mode = os.environ.get("LAB_WARM", "nearest")
+    if warm_mode.startswith("avg") or warm_mode.startswith("idw"):  # the q nearest seeds in standardised features
+        q = int(warm_mode[3:].split("p")[0])
+        pw_ = float(warm_mode.split("p")[1]) if "p" in warm_mode[3:] else 1.0
+        f = scenarios.sweep_features(P)
+        f = (f - f.mean(0)) / np.where(f.std(0) > 0, f.std(0), 1.0)
+        d = ((f[rest][:, None, :] - f[seeds][None, :, :]) ** 2).sum(-1)
+        pick2 = np.argsort(d, axis=1)[:, :q]
+        dd = np.sqrt(np.take_along_axis(d, pick2, 1))
+        wgt = np.full(dd.shape, 1.0 / q) if warm_mode.startswith("avg") else \
+            (1.0 / np.maximum(dd, 1e-9) ** pw_) / (1.0 / np.maximum(dd, 1e-9) ** pw_).sum(1, keepdims=True)
     lab = Lab()
     ref = None
     for v in variants:
@@ -132,7 +144,13 @@ def main():
                 for i, s in enumerate(rest):
                     k = wi * ns + pick[i]
                     lps.append(w[s])
-                    starts.append(transfer(w[s], seed_lps[k], rs["x"][k], rs["y"][k]))
+                    if warm_mode != "nearest":
+                        a = [transfer(w[s], seed_lps[wi * ns + p], rs["x"][wi * ns + p], rs["y"][wi * ns + p])
+                             for p in pick2[i]]
+                        starts.append((sum(wq * aa[0] for wq, aa in zip(wgt[i], a)),
+                                       sum(wq * aa[1] for wq, aa in zip(wgt[i], a))))
+                    else:
+                        starts.append(transfer(w[s], seed_lps[k], rs["x"][k], rs["y"][k]))
             r = lab.solve(lps, starts, check_every=64, kkt_every=1, warm_start=1, **wo)
             summary("warm " + tag, r)
 

@@ -453,6 +453,9 @@ int dvh_last_timing(const dvh_handle* h, double* ms3) {
 // device-only entry points of the header: not part of the CPU restatement
 int dvh_solve_packed_device(dvh_handle*, const dvh_packed*, void*) { return DVH_ERR_UNSUPPORTED; }
 int dvh_warm_transfer(dvh_handle*, const dvh_packed*, const int32_t*, int32_t) { return DVH_ERR_UNSUPPORTED; }
+int dvh_warm_transfer_blend(dvh_handle*, const dvh_packed*, const int32_t*, const double*, int32_t, int32_t) {
+  return DVH_ERR_UNSUPPORTED;
+}
 int dvh_synchronize(dvh_handle*) { return DVH_OK; }
 int dvh_last_stats(const dvh_handle*, int32_t* out4) {
   if (out4) std::memset(out4, 0, 4 * sizeof(int32_t));

@@ -208,3 +208,101 @@ def test_nearest_seed_search_equals_the_exact_argmin_with_ties():
     ref = ((fr[:, None, :] - fs[None, :, :]) ** 2).sum(-1).argmin(1)
     assert np.array_equal(_nearest(fr, fs), ref)
     assert np.array_equal(_nearest(fr[:3], fs[:2]), ((fr[:3, None] - fs[None, :2]) ** 2).sum(-1).argmin(1))
+
+
+def test_seed_partners_nearest_first_and_inverse_distance_weights():
+    from dervet_hip.sweep import _nearest, seed_partners
+    rng = np.random.default_rng(7)
+    fs = rng.normal(0, 1, (40, 3))
+    fr = np.concatenate([rng.normal(0, 1, (500, 3)), fs[5:6]])  # the last row sits on seed 5
+    first = _nearest(fr, fs)
+    idx, w = seed_partners(fr, fs, 3, first=first)
+    assert idx.shape == (501, 3) and np.array_equal(idx[:, 0], first)
+    d = np.sqrt(((fr[:, None, :] - fs[None, :, :]) ** 2).sum(-1))
+    for i in range(500):
+        assert set(idx[i]) == set(np.argsort(d[i], kind="stable")[:3])
+        inv = 1.0 / d[i, idx[i]]
+        np.testing.assert_allclose(w[i], inv / inv.sum(), rtol=1e-14)
+    assert w[500, 0] == 1.0 and (w[500, 1:] == 0.0).all()  # a seed at distance 0 takes the whole weight
+
+
+def test_blended_transfer_on_host_is_the_weighted_sum_of_partner_transfers():
+    """SeededSweep(blend=3): every rest window starts from the weighted sum of its three nearest seeds' transferred
+    solutions (the single-partner transfer of each, weights summing to 1); transfer_rows names them for the device."""
+    from dervet_hip.sweep import transfer_rows
+    ids = np.arange(24)
+    P = scenarios.sweep_parameters(ids)
+    sw = SeededSweep(scenarios.config4, ids, P["E"], stride=4, features=scenarios.sweep_features(P), blend=3)
+    assert sw.blend == 3 and sw.pairs is None
+    pb = sw.packed.to_torch("cpu").alloc_outputs()
+    g = torch.Generator().manual_seed(2)
+    pb.x.copy_(torch.randn(pb.x.shape, generator=g, dtype=torch.float64))
+    pb.y.copy_(torch.randn(pb.y.shape, generator=g, dtype=torch.float64))
+    x0, y0 = pb.x.clone(), pb.y.clone()
+    transfer(sw.transfers, pb.x, pb.y, pb.c, pb.u)
+    rows, wts = transfer_rows(sw.transfers)
+    assert rows.shape == (sw.packed.count - sw.n_seed, 5) and wts.shape == (rows.shape[0], 3)
+    np.testing.assert_allclose(wts.sum(1), 1.0, rtol=1e-14)
+    desc = np.asarray(sw.packed.desc)
+    u, c = sw.packed.u, sw.packed.c
+    for r in rows[::7]:
+        w, T = int(r[0]), int(r[4])
+        on_r, om_r, n, m = int(desc[w, 6]), int(desc[w, 7]), int(desc[w, 0]), int(desc[w, 1])
+        wx, wy = np.zeros(n), np.zeros(m)
+        for k, p in enumerate(r[1:4]):
+            on_s, om_s = int(desc[p, 6]), int(desc[p, 7])
+            ok = np.isfinite(u[on_r:on_r + n]) & np.isfinite(u[on_s:on_s + n]) & (u[on_s:on_s + n] > 0)
+            ratio = np.where(ok, u[on_r:on_r + n] / np.where(ok, u[on_s:on_s + n], 1.0), 1.0)
+            cd = c[on_r + 3 * T] / max(c[on_s + 3 * T], 1e-12)
+            cp = np.abs(c[on_r:on_r + T]).mean() / max(np.abs(c[on_s:on_s + T]).mean(), 1e-12)
+            ys = y0[om_s:om_s + m].numpy()
+            wk = wts[list(rows[:, 0]).index(w), k]
+            wx += wk * (x0[on_s:on_s + n].numpy() * ratio)
+            wy += wk * np.concatenate([ys[:T + 1] * cp, ys[T + 1:] * cd])
+        np.testing.assert_allclose(pb.x[on_r:on_r + n].numpy(), wx, rtol=1e-13, atol=1e-13)
+        np.testing.assert_allclose(pb.y[om_r:om_r + m].numpy(), wy, rtol=1e-13, atol=1e-13)
+    with pytest.raises(ValueError):
+        transfer_pairs(sw.transfers)
+
+
+@pytest.mark.gpu
+def test_device_blend_transfer_equals_host_blend_transfer():
+    """dvh_warm_transfer_blend (one launch) gives the torch blend's warm starts to rounding, and q = 1 with weight 1
+    is dvh_warm_transfer bit for bit."""
+    from dervet_hip import BatchSolver
+    from dervet_hip.sweep import transfer_device, transfer_rows
+    ids = np.arange(48)
+    P = scenarios.sweep_parameters(ids)
+    sw = SeededSweep(scenarios.config4, ids, P["E"], stride=8, features=scenarios.sweep_features(P), blend=3)
+    host = sw.packed.to_torch("cpu").alloc_outputs()
+    g = torch.Generator().manual_seed(4)
+    host.x.copy_(torch.randn(host.x.shape, generator=g, dtype=torch.float64))
+    host.y.copy_(torch.randn(host.y.shape, generator=g, dtype=torch.float64))
+    dev = sw.packed.to_torch("cuda:0").alloc_outputs()
+    dev.x.copy_(host.x)
+    dev.y.copy_(host.y)
+    x0, y0 = host.x.clone(), host.y.clone()
+    transfer(sw.transfers, host.x, host.y, host.c, host.u)
+    with BatchSolver(0) as s:
+        transfer_device(s, sw.transfers, dev)
+        np.testing.assert_allclose(dev.x.cpu().numpy(), host.x.numpy(), rtol=1e-13, atol=1e-13)
+        np.testing.assert_allclose(dev.y.cpu().numpy(), host.y.numpy(), rtol=1e-13, atol=1e-13)
+        # one partner, weight 1, through the blend entry == the plain transfer
+        import ctypes
+        sw1 = SeededSweep(scenarios.config4, ids, P["E"], stride=8, features=scenarios.sweep_features(P))
+        d1 = sw1.packed.to_torch("cuda:0").alloc_outputs()
+        d2 = sw1.packed.to_torch("cuda:0").alloc_outputs()
+        for d in (d1, d2):
+            d.x.copy_(x0.to("cuda:0"))
+            d.y.copy_(y0.to("cuda:0"))
+        transfer_device(s, sw1.transfers, d1)
+        rows, wts = transfer_rows(sw1.transfers)
+        p = d2.as_ctypes()
+        s._check(s._lib.dvh_warm_transfer_blend(s._h, ctypes.byref(p), rows.ctypes.data_as(ctypes.c_void_p),
+                                                wts.ctypes.data_as(ctypes.c_void_p), len(rows), 1), "blend")
+        assert torch.equal(d1.x, d2.x) and torch.equal(d1.y, d2.y)
+        bad = np.array([[5, 1, 2, 3, 0]], np.int32)
+        with pytest.raises(Exception):  # a non-finite weight
+            w_bad = np.array([[0.5, np.nan, 0.5]])
+            s._check(s._lib.dvh_warm_transfer_blend(s._h, ctypes.byref(p), bad.ctypes.data_as(ctypes.c_void_p),
+                                                    w_bad.ctypes.data_as(ctypes.c_void_p), 1, 3), "blend")
