@@ -132,6 +132,7 @@ def main():
     ap.add_argument("--med-scenarios", type=int, default=1000)
     ap.add_argument("--deg-scenarios", type=int, default=1000)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--blend", type=int, default=4, help="seeded schedules: warm starts blended from this many seeds")
     ap.add_argument("--sample", type=int, default=48)
     ap.add_argument("--procs", type=int, default=16)
     args = ap.parse_args()
@@ -182,7 +183,8 @@ def main():
         run("config4-slice", f"{args.c4_scenarios} scenarios x 12 monthly windows (bench.py runs 10,000)",
             P(scenarios.config4(ids)), s, args.reps, args.sample, args.procs)
         P4 = scenarios.sweep_parameters(ids)
-        sw = SeededSweep(scenarios.config4, ids, P4["E"], stride=32, features=scenarios.sweep_features(P4))
+        sw = SeededSweep(scenarios.config4, ids, P4["E"], stride=32, features=scenarios.sweep_features(P4),
+                         blend=args.blend)
         run("config4-slice", f"{args.c4_scenarios} scenarios x 12 monthly windows, seeded schedule",
             sw.packed, s, args.reps, args.sample, args.procs, sweep=sw)
     if 6 in only:
@@ -351,7 +353,7 @@ def config5_horizon(s, ids, years, args):
             mk = lambda v, y=y: scenarios.config5(v, years=min(yb, years - y), start_year=2017 + y,  # noqa: E731
                                                   min_soe=ms[np.searchsorted(ids, np.asarray(list(v)))],
                                                   cap_min_soe=True)
-        sw = SeededSweep(mk, ids, P5["E"], stride=32, features=feats)
+        sw = SeededSweep(mk, ids, P5["E"], stride=32, features=feats, blend=args.blend)
         dev = sw.to_device(s, "cuda:0")
         build_s += time.perf_counter() - t
         if y == 0:

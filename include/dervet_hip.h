@@ -269,7 +269,10 @@ int dvh_warm_transfer_blend(dvh_handle* h, const dvh_packed* batch, const int32_
                             int32_t count, int32_t q);
 
 /* Timing of the most recent solve on the handle's stream (HIP events, milliseconds):
- * [0] whole solve, [1] setup kernel (transpose + scaling + power iteration), [2] PDHG kernel. */
+ * [0] whole solve, [1] setup kernel (transpose + scaling + power iteration), [2] PDHG kernels.  On the default
+ * cascade the band kernels scale the windows they take themselves, inside the PDHG launch, and the setup kernel runs
+ * only for what they refuse, between the cascade's PDHG launches: there [1] is ~0 and [2] holds all of it (setup
+ * included); the A/B paths (dvh_set_kernel_path 1 / 2) run setup_kernel first and split the two as written. */
 int dvh_last_timing(const dvh_handle* h, double* ms3);
 
 /* Host waits on the stream during the most recent solve (dvh_solve_batch / dvh_solve_packed_device): the

@@ -79,6 +79,10 @@ def transfer(lp_r, lp_s, xs, ys):
     x = xs * ratio
     y = ys.copy()
     T = lp_r.m_eq - 1
+    if lp_r.n == 3 * T + 1 and os.environ.get("LAB_TAU_SCALE"):  # the demand column by the ratio of peak net loads
+        qr, qs = np.abs(lp_r.q[T + 1:]).max(), np.abs(lp_s.q[T + 1:]).max()
+        if qs > 0:
+            x[3 * T] = xs[3 * T] * qr / qs
     if lp_r.n == 3 * T + 1:
         cd = lp_r.c[3 * T] / max(lp_s.c[3 * T], 1e-12)
         cp = np.abs(lp_r.c[:T]).mean() / max(np.abs(lp_s.c[:T]).mean(), 1e-12)
@@ -106,12 +110,22 @@ def main():
     wins = [[lp for lp in builder.group_window_lps(g)] for g in groups]  # [window id][scenario]
     P = scenarios.sweep_parameters(range(S))
     stride = int(os.environ.get("LAB_STRIDE", "32"))
-    seeds, rest, pick = seed_split(P["E"], stride, scenarios.sweep_features(P))
+    feats = scenarios.sweep_features(P)
+    extra = os.environ.get("LAB_FEAT", "")
+    cols = {"price": P["price_scale"], "demand": P["demand"], "rte": P["rte"], "load": np.log(P["load_scale"]),
+            "E": np.log(P["E"])}
+    for name in [e for e in extra.split(",") if e]:
+        wgt = 1.0
+        if ":" in name:
+            name, wgt = name.split(":")[0], float(name.split(":")[1])
+        col = cols[name]
+        feats = np.concatenate([feats, (wgt * (col - col.mean()) / col.std())[:, None]], axis=1)
+    seeds, rest, pick = seed_split(P["E"], stride, feats)
     warm_mode = os.environ.get("LAB_WARM", "nearest")
     if warm_mode.startswith("avg") or warm_mode.startswith("idw"):  # the q nearest seeds in standardised features
         q = int(warm_mode[3:].split("p")[0])
         pw_ = float(warm_mode.split("p")[1]) if "p" in warm_mode[3:] else 1.0
-        f = scenarios.sweep_features(P)
+        f = feats
         f = (f - f.mean(0)) / np.where(f.std(0) > 0, f.std(0), 1.0)
         d = ((f[rest][:, None, :] - f[seeds][None, :, :]) ** 2).sum(-1)
         pick2 = np.argsort(d, axis=1)[:, :q]
