@@ -82,17 +82,26 @@ def seed_partners(fr, fs, q, first=None, power=1.0):
     R = len(fr)
     idx = np.zeros((R, q), np.int64)
     w = np.zeros((R, q), np.float64)
+    bb = (fs * fs).sum(1)
     for a in range(0, R, 2048):
-        d = ((fr[a:a + 2048, None, :] - fs[None, :, :]) ** 2).sum(-1)
-        part = np.argsort(d, axis=1, kind="stable")[:, :q]
+        # candidates by the expanded form (one GEMM), q + 2 of them to absorb its rounding, then exact distances
+        fa = fr[a:a + 2048]
+        g = fa @ fs.T
+        g *= -2.0
+        g += bb[None, :]
+        qc = min(q + 2, len(fs))
+        cand = np.argpartition(g, qc - 1, axis=1)[:, :qc] if qc < len(fs) else np.tile(np.arange(len(fs)), (len(fa), 1))
+        cand.sort(axis=1)  # index order, so that equal distances keep the lower seed first
+        dc = ((fa[:, None, :] - fs[cand]) ** 2).sum(-1)
+        o = np.argsort(dc, axis=1, kind="stable")[:, :q]
+        part = np.take_along_axis(cand, o, 1)
+        d = np.zeros((len(fa), len(fs)))
+        np.put_along_axis(d, part, np.take_along_axis(dc, o, 1), 1)
         if first is not None:  # keep the exact argmin of _nearest first (ties broken the same way)
             f0 = np.asarray(first[a:a + 2048], np.int64)
-            rest = np.where(part == f0[:, None], -1, part)
-            rows = []
-            for i in range(len(part)):
-                o = [int(f0[i])] + [int(v) for v in rest[i] if v >= 0]
-                rows.append(o[:q])
-            part = np.array(rows, np.int64)
+            has = (part == f0[:, None]).any(1)
+            part[~has, -1] = f0[~has]  # (a tie at the boundary: the known nearest replaces the last one)
+            part = np.take_along_axis(part, np.argsort(part != f0[:, None], axis=1, kind="stable"), 1)
         dd = np.sqrt(np.take_along_axis(d, part, 1))
         inv = np.where(dd > 0, 1.0 / np.where(dd > 0, dd, 1.0) ** power, np.inf)
         ww = np.where(np.isinf(inv).any(1, keepdims=True), np.isinf(inv).astype(np.float64), inv)
@@ -180,9 +189,9 @@ def _same_pattern(a, b):
 def plan(seed_groups, rest_groups, partner_of, blend=None):
     """Transfers from the packed seed windows (packed first) to the rest windows (packed after them).
 
-    partner_of: dict rest scenario id -> seed scenario id (the nearest).  blend (optional): dict rest scenario id ->
-    (seed scenario ids [q], weights [q]) -- the window starts from the weighted blend of those partners.  Groups are
-    matched by window id (tag[1]) and must share the CSR pattern."""
+    partner_of: dict rest scenario id -> seed scenario id (the nearest).  blend (optional): (rest scenario ids [R],
+    their partners' seed scenario ids [R, q], weights [R, q]) -- the window starts from the weighted blend of those
+    partners.  Groups are matched by window id (tag[1]) and must share the CSR pattern."""
     out = []
     on = om = wk = 0
     seed_at = {}
@@ -197,6 +206,12 @@ def plan(seed_groups, rest_groups, partner_of, blend=None):
     po = np.argsort(pk, kind="stable")
     pk, pv = pk[po], pv[po]
     cols = {}
+    if blend is not None:
+        b_ids = np.asarray(blend[0], np.int64)
+        b_ord = np.argsort(b_ids, kind="stable")
+        b_ids = b_ids[b_ord]
+        b_seed = np.asarray(blend[1], np.int64)[b_ord]
+        b_w = np.asarray(blend[2], np.float64)[b_ord]
     for g in rest_groups:
         wid = _window_id(g.tags[0])
         if wid not in seed_at:
@@ -221,13 +236,15 @@ def plan(seed_groups, rest_groups, partner_of, blend=None):
         local = so[j].astype(np.int64)
         weights = None
         if blend is not None:  # every partner of the blend, looked up in the seed group as the nearest one is
-            bq = [blend[int(r)] for r in rs]
-            want_q = np.array([b[0] for b in bq], np.int64).reshape(len(rs), -1)
+            ib = np.minimum(np.searchsorted(b_ids, rs), max(len(b_ids) - 1, 0))
+            if len(rs) and (len(b_ids) == 0 or not np.array_equal(b_ids[ib], rs)):
+                raise KeyError("a rest scenario has no blend partners")
+            want_q = b_seed[ib]
             jq = np.minimum(np.searchsorted(ss, want_q), max(len(ss) - 1, 0))
             if want_q.size and (len(ss) == 0 or not np.array_equal(ss[jq], want_q)):
                 raise KeyError(f"a blend partner is not in the seed group of window {wid!r}")
             local = so[jq].astype(np.int64)
-            weights = np.array([b[1] for b in bq], np.float64).reshape(len(rs), -1)
+            weights = b_w[ib]
         out.append(_Transfer(on, om, son, som, g.n, g.m, g.G, sg.G, local,
                              g.n == 3 * g.T + 1 and g.J == 1, g.T, wk, swk, weights))
         on += g.G * g.n
@@ -354,7 +371,7 @@ class SeededSweep:
             f = standardise(features, len(ids))
             idx, w = seed_partners(f[rest_i], f[seed_i], blend, first=pick, power=blend_power)
             self.blend = idx.shape[1]
-            bl = {int(r): (self.seed_ids[idx[i]], w[i]) for i, r in enumerate(self.rest_ids)}
+            bl = (self.rest_ids, self.seed_ids[idx], w)
         sg = make_groups(self.seed_ids)
         rg = make_groups(self.rest_ids) if len(self.rest_ids) else []
         self.transfers = plan(sg, rg, partner_of, bl)
