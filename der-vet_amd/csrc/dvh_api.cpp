@@ -816,14 +816,22 @@ static int device_cascade(dvh_handle* h, const dvh::Batch& b, const dvh::Work& w
     return e != hipSuccess ? e : sync_stream(h, s);
   };
   int variant = -1, bvar = -1;
-  DVH_HIP(h, dvh::launch_pdhg_band(b, w, ch, o, s, false, form_for(ch.count), nullptr, 0, &bvar));
+  // the battery forms iterate on [0, 1]-normalised boxes (dvh_band.hip BOX; DVH_BAND_BOX=0 turns it off for A/B);
+  // the few windows with an unbounded ch / dis / ene column (status -3) are re-run by the plain form, which takes
+  // every one of them (same structure and scaling checks), in the same read-back
+  const char* box_env = getenv("DVH_BAND_BOX");
+  const bool box = !(box_env && atoi(box_env) == 0);
+  DVH_HIP(h, dvh::launch_pdhg_band(b, w, ch, o, s, false, form_for(ch.count), box, nullptr, 0, &bvar));
   DVH_HIP(h, route(0, nullptr, ch.count, -2, 0, 0));
-  DVH_HIP(h, readback(0, 1));
+  if (box) DVH_HIP(h, route(1, nullptr, ch.count, -3, 0, 1));
+  DVH_HIP(h, readback(0, box ? 2 : 1));
+  if (box && rh[8] > 0)
+    DVH_HIP(h, dvh::launch_pdhg_band(b, w, ch, o, s, false, form_for(rh[8]), false, L[1], rh[8], nullptr));
   int cur = rh[0];
   h->n_band += nsmall - cur;
   if (nsmall - cur > 0) variant = bvar;
   if (cur > 0) {  // pass 2: the band kernel's ICE form over pass 1's refusals
-    DVH_HIP(h, dvh::launch_pdhg_band(b, w, ch, o, s, true, form_for(cur), L[0], cur, &bvar));
+    DVH_HIP(h, dvh::launch_pdhg_band(b, w, ch, o, s, true, form_for(cur), false, L[0], cur, &bvar));
     DVH_HIP(h, route(1, L[0], cur, -2, 0, 4));
     DVH_HIP(h, readback(1, 1));
     const int left = rh[8];

@@ -97,9 +97,27 @@ __device__ __noinline__ RowKkt row_kkt_fn(double kv, double qi, double yi, float
 // GATE: the predicted KKT gate (dvh_options.kkt_predict > 0) is compiled in only where the host asks for it -- its
 // state and extra reduction raised the register allocation of the check path by 30-40 spilled VGPRs in every form
 // (profiles/r02zzk_ab_configs12_spills.log), which runs with the default options paid for nothing.
-template <int B, int S, bool ICE, int LF, int WPS, bool GATE>
+//
+// BOX (box form, the default for the battery windows): every ch / dis / ene column has a finite box [lo, hi] in the
+// scaled space, so the kernel iterates on x' = (x - lo) / w, w = hi - lo, whose box is [0, 1]: the projection is the
+// FMA's own clamp modifier (one v_fma_f64 ... clamp instead of v_fma + v_max + v_min per column and iteration).  The
+// change of variables is exact: K' = K diag(w) (both SpMV directions), c' = c w, q' = q - K lo, and a per-column
+// primal step tau / w^2 gives x' + (tau / w^2)(w g) = (x + tau g - lo) / w, i.e. the same PDHG iterates.  The
+// movement norms that drive restarts and the primal weight are taken in x units (w d'), the KKT check runs on the
+// primed LP, whose objectives, row residuals and (zero, for a two-sided box) column residuals equal the original's
+// once the constant c lo is added.  A window with an unbounded ch / dis / ene column is returned with status
+// kNeedsPlain and re-run by the plain form (dvh_api.cpp device_cascade).
+constexpr int kNeedsPlain = -3;
+__device__ __forceinline__ double fma_clamp01(double a, double b, double c) {
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3 clamp" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+template <int B, int S, bool ICE, int LF, int WPS, bool GATE, bool BOX>
 __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const Work w, const Chunk ch, const Opts o,
                                                         const int32_t* list) {
+  static_assert(!BOX || (!ICE && !(LF & kLfImages)), "the box form covers the battery forms with images in LDS");
   constexpr int NW = B / kWave;
   constexpr int SB = S * B;        // step capacity
   constexpr int NC = ICE ? 5 : 3;  // columns per step: ch, dis, ene (, elec, on)
@@ -172,9 +190,9 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
     ice_b[u] = -1;
     ice_n[u] = 0;
   }
-  if (tid == 0) flag[0] = flag[1] = 0;
+  if (tid == 0) flag[0] = flag[1] = flag[2] = 0;
   __syncthreads();
-  int bad = 0, crossed = 0;
+  int bad = 0, crossed = 0, unboxed = 0;
   for (int j = tid; j < J; j += B) crossed |= lraw[3 * T + j] > uraw[3 * T + j];
   for (int r = tid; r <= T; r += B) {
     const int p0 = gkp[r], len = gkp[r + 1] - p0;
@@ -197,6 +215,7 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
     // the kernel keeps no lower bound for ch / dis (/ elec / on); crossed bounds: infeasible as given
     bad |= lraw[t] != 0.0 || lraw[T + t] != 0.0;
     crossed |= lraw[t] > uraw[t] || lraw[T + t] > uraw[T + t] || lraw[2 * T + t] > uraw[2 * T + t];
+    if (BOX) unboxed |= !(isfinite(uraw[t]) && isfinite(uraw[T + t]) && isfinite(lraw[2 * T + t]) && isfinite(uraw[2 * T + t]));
     if (ICE) {
       bad |= lraw[CE + t] != 0.0 || lraw[CO + t] != 0.0;
       crossed |= lraw[CE + t] > uraw[CE + t] || lraw[CO + t] > uraw[CO + t];
@@ -251,6 +270,7 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
   }
   if (bad) flag[0] = 1;
   if (crossed) flag[1] = 1;
+  if (unboxed) flag[2] = 1;
   __syncthreads();
   if (ICE)
     for (int u = tid; u < T; u += B)
@@ -268,6 +288,16 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
   }
   if (flag[0] != 0) {
     bail();
+    return;
+  }
+  auto bail_plain = [&]() {
+    if (tid == 0) {
+      b.istats[2 * k] = kNeedsPlain;
+      b.istats[2 * k + 1] = 0;
+    }
+  };
+  if (BOX && flag[2] != 0) {
+    bail_plain();
     return;
   }
 
@@ -792,7 +822,78 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
     }
   }
   double pw = uniform(pwi);
-  const double cnorm = uniform(sqrt(nrm[2])), qnorm = uniform(sqrt(nrm[3])), c0 = uniform(b.c0[k]);
+  // ---- box form: x' = (x - lo) / w on the ch / dis / ene columns (after the scaling, the power iteration and the
+  //      warm start's weight, which all see the original variables)
+  double tj[S][3];                      // per-column primal steps tau / w^2
+  double* wbox = w.vbuf + W.wn;         // the columns' widths w (window workspace: read at checks, restarts, the end)
+  double cbox = 0.0;                    // c lo, the objective's constant under the change of variables
+  auto wcol = [&](int s, int v) { return val[s] ? wbox[opaque(col(s, v))] : 0.0; };
+  if constexpr (BOX) {
+    double wb[S][3];
+    bool unb = false;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+#pragma unroll
+      for (int v = 0; v < 3; ++v) {
+        double wv = hi[s][v] - (v == 2 ? loe[s] : 0.0);  // padding steps: 0
+        unb |= !isfinite(wv);
+        if (!(wv >= 0x1p-500)) wv = 0.0;  // a (numerically) fixed column: x' = 0, x = lo
+        wb[s][v] = wv;
+      }
+    }
+    if (__syncthreads_or(unb)) {
+      bail_plain();
+      return;
+    }
+    // the next lane's first ene (width, lower bound) for the lane's last SOE row; step 0's for the init row
+    XP[tid] = wb[0][2];
+    XP[B + 1 + tid] = loe[0];
+    if (tid == 0) XP[B] = XP[2 * B + 1] = 0.0;
+    __syncthreads();
+    const double wnx = XP[tid + 1], lnx = XP[B + 2 + tid], we0 = XP[0], le0 = XP[B + 1];
+    __syncthreads();  // (XP is rewritten with the images below)
+    double cl[1] = {0.0};
+    kp0 *= wb[0][2];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const double wn1 = s < S - 1 ? wb[s < S - 1 ? s + 1 : s][2] : wnx;
+      const double ln1 = s < S - 1 ? loe[s < S - 1 ? s + 1 : s] : lnx;
+      if (val[s]) {  // q' = q - K lo over the SOE row: its ene_t and ene_{t+1} terms (ch / dis have lo = 0)
+        const double qs = fma(-ks[s][3], ln1, fma(-ks[s][2], loe[s], qv(s, 0)));
+        if (LC)
+          cqa(3, s) = qs;
+        else
+          q[s][0] = qs;
+        cl[0] = fma(cof(s, 2), loe[s], cl[0]);
+      }
+      ks[s][0] *= wb[s][0];
+      ks[s][1] *= wb[s][1];
+      ks[s][2] *= wb[s][2];
+      ks[s][3] *= wn1;
+      kd[s][0] *= wb[s][0];
+      kd[s][1] *= wb[s][1];
+#pragma unroll
+      for (int v = 0; v < 3; ++v) {
+        const double lo = v == 2 ? loe[s] : 0.0, wv = wb[s][v], cs = cof(s, v) * wv;
+        if (LC)
+          cqa(v, s) = cs;
+        else
+          cc[s][v] = cs;
+        const double xv = wv > 0.0 ? fmin(fmax((x[s][v] - lo) / wv, 0.0), 1.0) : 0.0;
+        x[s][v] = xa[s][v] = xv;
+        if constexpr (LA) XA[(v * S + s) * B + tid] = xv;
+        XP[(v * S + s) * B + tid] = xv;
+        if (val[s]) wbox[col(s, v)] = wv;
+      }
+    }
+    if (ilane) {
+      sp[3] = fma(-sp[4], le0, sp[3]);
+      sp[4] *= we0;
+    }
+    block_sum<B, 1>(cl, red);
+    cbox = cl[0];
+  }
+  const double cnorm = uniform(sqrt(nrm[2])), qnorm = uniform(sqrt(nrm[3])), c0 = uniform(b.c0[k] + cbox);
   int it = 0, kin = 0, status = kIterLimit;
   double r0 = -1.0, rprev = -1.0;
   double* fin = red + kNRed * NW;
@@ -801,6 +902,18 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
   const int chk = o.check_every > 0 ? o.check_every : 64;
   double tau = uniform(eta / pw), sigma = uniform(eta * pw);
   double sigma2n = uniform(-2.0 * sigma);  // the equality rows' fused dual step (non-check iterations)
+  auto box_steps = [&]() {
+    if constexpr (BOX) {
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+#pragma unroll
+        for (int v = 0; v < 3; ++v) {
+          const double wv = wcol(s, v);
+          tj[s][v] = wv > 0.0 ? tau / (wv * wv) : 0.0;
+        }
+    }
+  };
+  box_steps();
   const int kkt_every = o.kkt_every > 0 ? o.kkt_every : 1;
   int ck = chk, kk_ = kkt_every;
   KktGate gate;  // dvh_options.kkt_predict (dvh_device.h)
@@ -886,11 +999,21 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
       for (int s = 0; s < S; ++s) {
 #pragma unroll
         for (int v = 0; v < NC; ++v) {  // branch-free: padding steps have c = lo = hi = 0 and stay at 0
-          const double lo = v == 2 ? loe[s] : 0.0;
-          const double p1 = vmin(vmax(fma(tau, kty[s][v], x[s][v]), lo), hib(s, v));
+          double p1;
+          if constexpr (BOX) {
+            p1 = fma_clamp01(tj[s][v < 3 ? v : 0], kty[s][v], x[s][v]);
+          } else {
+            const double lo = v == 2 ? loe[s] : 0.0;
+            p1 = vmin(vmax(fma(tau, kty[s][v], x[s][v]), lo), hib(s, v));
+          }
           xb[s][v] = fma(2.0, p1, -x[s][v]);
           if (CHECK) {
-            const double d = x[s][v] - p1, da = p1 - axv(s, v);
+            double d = x[s][v] - p1, da = p1 - axv(s, v);
+            if constexpr (BOX) {  // movements in x units
+              const double wv = wcol(s, v < 3 ? v : 0);
+              d *= wv;
+              da *= wv;
+            }
             mv0 += d * d;
             mv1 += da * da;
             if constexpr (LI) {
@@ -1052,8 +1175,12 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
         ktr(s, yp[s], s == 0 ? ysp : yp[s > 0 ? s - 1 : 0][0], kt);
         if (val[s]) {
 #pragma unroll
-          for (int v = 0; v < NC; ++v)
-            col_kkt(col(s, v), kt[v], cof(s, v), v == 2 ? loe[s] : 0.0, hib(s, v), xp[s][v]);
+          for (int v = 0; v < NC; ++v) {
+            if constexpr (BOX)  // the primed LP: box [0, 1]
+              col_kkt(col(s, v), kt[v], cof(s, v), 0.0, 1.0, xp[s][v]);
+            else
+              col_kkt(col(s, v), kt[v], cof(s, v), v == 2 ? loe[s] : 0.0, hib(s, v), xp[s][v]);
+          }
         }
       }
       if (wid == 0 && J > 0) {
@@ -1138,6 +1265,7 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
       tau = uniform(eta / pw);
       sigma = uniform(eta * pw);
       sigma2n = uniform(-2.0 * sigma);
+      box_steps();
       double xp[S][NC], yp[S][NR];
       load_images(xp, yp);
 #pragma unroll
@@ -1182,7 +1310,15 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
     if (LI || !val[s]) continue;
     const int t = t0 + s;
 #pragma unroll
-    for (int v = 0; v < NC; ++v) xo_g[col(s, v)] = XP[(v * S + s) * B + tid] * dcv[col(s, v)];
+    for (int v = 0; v < NC; ++v) {
+      const int j = col(s, v);
+      if constexpr (BOX) {  // x = lo + w x' (clipped to the box against the rounding), then unscaled
+        const double d = dcv[j], lo = lraw[j] / d, hv = uraw[j] / d;
+        xo_g[j] = fmin(fmax(fma(wbox[j], XP[(v * S + s) * B + tid], lo), lo), hv) * d;
+      } else {
+        xo_g[j] = XP[(v * S + s) * B + tid] * dcv[j];
+      }
+    }
     yo_g[t + 1] = YP[s * B + tid] * drv[t + 1];
     if (drow[s] >= 0) yo_g[drow[s]] = YP[(S + s) * B + tid] * drv[drow[s]];
     if (ICE) {
@@ -1199,12 +1335,12 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
   }
 }
 
-template <int B, int S, bool ICE, int LF, int WPS, bool GATE>
+template <int B, int S, bool ICE, int LF, int WPS, bool GATE, bool BOX>
 hipError_t launch_band_one_g(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, hipStream_t s,
                            const int32_t* list, int nlist, int* variant_out) {
   static_assert(B * S == kBandSteps, "every form covers T <= kBandSteps");
   const size_t lds = band_lds_bytes(B, S, ICE, LF);
-  auto kern = pdhg_band_kernel<B, S, ICE, LF, WPS, GATE>;
+  auto kern = pdhg_band_kernel<B, S, ICE, LF, WPS, GATE, BOX>;
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   if (getenv("DVH_BAND_OCC")) {  // residency diagnostics (A/B helper)
@@ -1215,18 +1351,19 @@ hipError_t launch_band_one_g(const Batch& b, const Work& w, const Chunk& ch, con
     hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kern, B, lds);
     hipFuncAttributes fa;
     hipFuncGetAttributes(&fa, (const void*)kern);
-    fprintf(stderr, "band<%d,%d,%d,%d,gate %d>: lds %zu B, blocks/CU %d, lds/CU %zu, regs %d, local %zu\n", B, S, (int)ICE, LF,
-            (int)GATE, lds, nb, (size_t)pr.maxSharedMemoryPerMultiProcessor, fa.numRegs, (size_t)fa.localSizeBytes);
+    fprintf(stderr, "band<%d,%d,%d,%d,gate %d,box %d>: lds %zu B, blocks/CU %d, lds/CU %zu, regs %d, local %zu\n", B, S,
+            (int)ICE, LF, (int)GATE, (int)BOX, lds, nb, (size_t)pr.maxSharedMemoryPerMultiProcessor, fa.numRegs, (size_t)fa.localSizeBytes);
   }
   hipLaunchKernelGGL(kern, dim3(list ? nlist : ch.count), dim3(B), lds, s, b, w, ch, o, list);
   if (variant_out) *variant_out = 9000000 + 1000 * (S - 1) + (ICE ? 100 : 0) + B / kWave;
   return hipGetLastError();
 }
-template <int B, int S, bool ICE, int LF, int WPS>
+template <int B, int S, bool ICE, int LF, int WPS, bool BOX = false>
 hipError_t launch_band_one(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, hipStream_t s,
                            const int32_t* list, int nlist, int* variant_out) {
-  if (o.kkt_predict > 0) return launch_band_one_g<B, S, ICE, LF, WPS, true>(b, w, ch, o, s, list, nlist, variant_out);
-  return launch_band_one_g<B, S, ICE, LF, WPS, false>(b, w, ch, o, s, list, nlist, variant_out);
+  if (o.kkt_predict > 0)
+    return launch_band_one_g<B, S, ICE, LF, WPS, true, BOX>(b, w, ch, o, s, list, nlist, variant_out);
+  return launch_band_one_g<B, S, ICE, LF, WPS, false, BOX>(b, w, ch, o, s, list, nlist, variant_out);
 }
 
 }  // namespace
@@ -1247,9 +1384,13 @@ hipError_t launch_band_one(const Batch& b, const Work& w, const Chunk& ch, const
 #define DVH_BAND3_LF kLfCosts
 #endif
 hipError_t launch_pdhg_band(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, hipStream_t s, bool ice,
-                            int form, const int32_t* list, int nlist, int* variant_out) {
+                            int form, bool box, const int32_t* list, int nlist, int* variant_out) {
   if (ice) return launch_band_one<kBandSteps, 1, true, DVH_BANDI_LF, 3>(b, w, ch, o, s, list, nlist, variant_out);
-  if (form == 1) return launch_band_one<kBandSteps, 1, false, 0, 3>(b, w, ch, o, s, list, nlist, variant_out);
+  if (form == 1) {
+    if (box) return launch_band_one<kBandSteps, 1, false, 0, 3, true>(b, w, ch, o, s, list, nlist, variant_out);
+    return launch_band_one<kBandSteps, 1, false, 0, 3>(b, w, ch, o, s, list, nlist, variant_out);
+  }
+  if (box) return launch_band_one<kBandSteps / 3, 3, false, DVH_BAND3_LF, 2, true>(b, w, ch, o, s, list, nlist, variant_out);
   return launch_band_one<kBandSteps / 3, 3, false, DVH_BAND3_LF, 2>(b, w, ch, o, s, list, nlist, variant_out);
 }
 

@@ -119,8 +119,10 @@ hipError_t launch_pdhg_ell(const Batch& b, const Work& w, const Chunk& ch, const
 // ice: the variant with LP-relaxed ICE columns (elec, on) and rows; list (nlist entries): global window indices,
 // or null for the whole chunk; form: steps per lane of the battery kernel (3 default, 1 = the 768-thread form);
 // variant_out: 9000000 + 1000 (steps per lane - 1) + 100 ice + waves per window.
+// box (battery forms): iterate on the columns' [0, 1]-normalised boxes (dvh_band.hip, BOX); windows with an unbounded
+// ch / dis / ene column come back with status -3 (kNeedsPlain) and must be re-run with box = false.
 hipError_t launch_pdhg_band(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, hipStream_t s, bool ice,
-                            int form, const int32_t* list, int nlist, int* variant_out);
+                            int form, bool box, const int32_t* list, int nlist, int* variant_out);
 size_t setup_lds_bytes(int max_n, int max_m);
 // Setup (scaling, transpose) of the listed medium windows (scaling vectors kept in the global workspace).
 hipError_t launch_setup_medium(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n,

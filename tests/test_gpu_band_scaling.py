@@ -83,3 +83,50 @@ def test_factors_outside_single_precision_range_leave_the_band_kernel(gpu_solver
     assert ks["band_windows"] == 2 and ks["ell_windows"] + ks["generic_windows"] == 1, ks
     o, h = _highs(lp)
     assert res[1].status == 0 and abs(res[1].obj - h["obj"]) <= 1e-5 * abs(h["obj"]), (res[1].obj, h["obj"])
+
+
+def test_box_form_matches_the_plain_form(gpu_solver, monkeypatch):
+    """The battery forms iterate on [0, 1]-normalised column boxes (csrc/dvh_band.hip BOX: the projection is the FMA's
+    clamp).  The change of variables is exact, so the box form reaches the plain form's optimum on the same windows --
+    the bench shape and the badly scaled copies -- in about as many iterations."""
+    base = [lp for g in scenarios.config4(range(3)) for lp in builder.group_window_lps(g)]
+    lps = base + [_badly_scaled(lp) for lp in base[::3]]
+    box = gpu_solver.solve(lps)
+    assert gpu_solver.kernel_stats()["band_windows"] == len(lps)
+    monkeypatch.setenv("DVH_BAND_BOX", "0")
+    plain = gpu_solver.solve(lps)
+    monkeypatch.delenv("DVH_BAND_BOX")
+    it_box = it_plain = 0
+    for i, (lp, a, b) in enumerate(zip(lps, box, plain)):
+        assert a.status == 0 and b.status == 0, (i, a.status_name, b.status_name)
+        assert abs(a.obj - b.obj) <= 2e-6 * abs(b.obj), (i, a.obj, b.obj)
+        assert np.all(a.x >= lp.l - 1e-9 * (1 + np.abs(lp.l))) and np.all(a.x <= lp.u + 1e-9 * (1 + np.abs(lp.u)))
+        it_box += a.iters
+        it_plain += b.iters
+    assert it_box <= 1.1 * it_plain, (it_box, it_plain)
+    for i in (0, 5, len(base)):
+        o, h = _highs(lps[i])
+        assert abs(box[i].obj - h["obj"]) <= 1e-5 * abs(h["obj"]), (i, box[i].obj, h["obj"])
+        assert window_lp.primal_residual_rel(o, box[i].x)[0] <= 1e-6
+
+
+def test_unbounded_column_goes_to_the_plain_form(gpu_solver):
+    """A window whose charge column has no upper bound has no box: the box form returns it (status -3) and the plain
+    band form solves it in the same cascade pass (still counted as a band window) to HiGHS's optimum; a fixed column
+    (lo == hi) stays in the box form with width 0."""
+    lps = [lp for g in scenarios.config4([1]) for lp in builder.group_window_lps(g)][:4]
+    u = lps[1].u.copy()
+    u[3] = np.inf  # ch_3 unbounded
+    lps[1] = dataclasses.replace(lps[1], u=u)
+    T2 = lps[2].m_eq - 1
+    l2, u2 = lps[2].l.copy(), lps[2].u.copy()
+    l2[2 * T2 + 5] = u2[2 * T2 + 5] = 0.5 * (l2[2 * T2 + 5] + u2[2 * T2 + 5])  # ene_5 fixed mid-box
+    lps[2] = dataclasses.replace(lps[2], l=l2, u=u2)
+    res = gpu_solver.solve(lps)
+    ks = gpu_solver.kernel_stats()
+    assert ks["band_windows"] == len(lps) and ks["ell_windows"] == 0 and ks["generic_windows"] == 0, ks
+    for i in (1, 2):
+        o, h = _highs(lps[i])
+        assert h["status"] == 0 and res[i].status == 0, (i, res[i].status_name)
+        assert abs(res[i].obj - h["obj"]) <= 1e-5 * abs(h["obj"]), (i, res[i].obj, h["obj"])
+    assert abs(res[2].x[2 * T2 + 5] - l2[2 * T2 + 5]) <= 1e-9 * abs(l2[2 * T2 + 5]), res[2].x[2 * T2 + 5]
