@@ -57,6 +57,7 @@ struct dvh_handle {
   // packed inputs / outputs for the host API
   DevBuf d_desc, d_indptr, d_indices, d_data, d_c, d_c0, d_q, d_l, d_u, d_x, d_y, d_stats, d_istats;
   // workspace
+  DevBuf w_queue;  // the band kernels' work-queue counter
   DevBuf w_tptr, w_tind, w_tval, w_kval, w_rowof, w_perm, w_dr, w_dc, w_cs, w_ls, w_us, w_qs, w_vbuf, w_wbuf,
       w_tmpc, w_tmpr, w_longk, w_longt, w_scal, w_fc, w_fr;
   DevBuf d_list, d_hinv;
@@ -84,6 +85,9 @@ struct dvh_handle {
   int kernel_path = 0;  // 0 band -> ELL -> generic, 1 generic only, 2 ELL -> generic (no band kernel), 3 / 4 as 0
                         // with the battery band kernel's one-step / three-step form forced (0 picks by batch size)
   int cus = 0;          // compute units of the device (band kernel form choice)
+  std::vector<int32_t> order;  // dvh_set_launch_order: the next solve's band-pass window order (empty: packing order)
+  std::vector<int32_t> order_used;  // (the copy a solve consumed: kept until the next one, the H2D copy reads it)
+  DevBuf d_order;
   dvh::LargeSolver* large = nullptr;  // grid-wide path for windows above dvh::kSmallMax (created on first use)
   float large_ms[2] = {0, 0};         // setup, PDHG time of the large windows of the last solve
   // Further devices of this handle (device_mask bits after the first, or dvh_create_devices): same options; a
@@ -238,7 +242,7 @@ int dvh_destroy(dvh_handle* h) {
                     &h->w_qs, &h->w_vbuf, &h->w_wbuf, &h->w_tmpc, &h->w_tmpr, &h->w_longk, &h->w_longt, &h->w_scal,
                     &h->w_fc, &h->w_fr,
                     &h->m_list, &h->m_plan, &h->m_pos, &h->m_xbuf, &h->m_abort, &h->o_data, &h->o_cases, &h->o_len, &h->o_hist, &h->o_soe,
-                    &h->s_pairs, &h->s_wts, &h->s_bad, &h->g_seeds, &h->g_word, &h->d_route};
+                    &h->s_pairs, &h->s_wts, &h->s_bad, &h->g_seeds, &h->g_word, &h->d_route, &h->d_order, &h->w_queue};
   for (DevBuf* b : bufs) b->release();
   if (h->route_host) hipHostFree(h->route_host);
   for (auto& e : h->ev)
@@ -409,6 +413,20 @@ int dvh_last_path_counts4(const dvh_handle* h, int32_t* out4) {
   out4[1] = h->n_generic;
   out4[2] = h->n_large;
   out4[3] = h->n_band;
+  return DVH_OK;
+}
+
+int dvh_set_launch_order(dvh_handle* h, const int32_t* order, int32_t count) {
+  if (!h || count < 0 || (count > 0 && !order)) return DVH_ERR_ARG;
+  h->order.clear();
+  if (count == 0) return DVH_OK;
+  std::vector<char> seen(count, 0);  // a permutation of 0 .. count - 1 (the kernels index windows with it)
+  for (int32_t i = 0; i < count; ++i) {
+    const int32_t k = order[i];
+    if (k < 0 || k >= count || seen[k]) return fail(h, DVH_ERR_ARG, "launch order is not a permutation of 0 .. count - 1");
+    seen[k] = 1;
+  }
+  h->order.assign(order, order + count);
   return DVH_OK;
 }
 
@@ -794,7 +812,8 @@ static int chain_pass(dvh_handle* h, const dvh::Batch& b, const dvh::Work& w, co
 // the ICE form when it refuses windows: their count, then their size classes once they are set up); a batch the band
 // kernel takes whole waits once.
 static int device_cascade(dvh_handle* h, const dvh::Batch& b, const dvh::Work& w, const dvh::Chunk& ch,
-                          const dvh::Opts& o, int nsmall, int wc, int mn, int mm, hipStream_t s) {
+                          const dvh::Opts& o, int nsmall, int wc, int mn, int mm, hipStream_t s,
+                          const int32_t* order = nullptr) {
   const size_t I = sizeof(int32_t);
   int32_t* L[5];
   for (int r = 0; r < 5; ++r) L[r] = h->d_list.as<int32_t>() + (size_t)r * wc;
@@ -816,12 +835,16 @@ static int device_cascade(dvh_handle* h, const dvh::Batch& b, const dvh::Work& w
     return e != hipSuccess ? e : sync_stream(h, s);
   };
   int variant = -1, bvar = -1;
-  // the battery forms iterate on [0, 1]-normalised boxes (dvh_band.hip BOX; DVH_BAND_BOX=0 turns it off for A/B);
-  // the few windows with an unbounded ch / dis / ene column (status -3) are re-run by the plain form, which takes
-  // every one of them (same structure and scaling checks), in the same read-back
+  // the battery forms iterate on [0, 1]-normalised boxes (dvh_band.hip BOX; bench 246.4k vs 239.7k windows/s,
+  // profiles/r04m_ab_band_box.log); the few windows with an unbounded ch / dis / ene column (status -3) are re-run by
+  // the plain form, which takes every one of them (same structure and scaling checks), after the same read-back.
+  // The ICE form's box (elec / on too) is opt-in: it spills as much as the plain ICE form and ran 0.8 % slower on
+  // config 5 (profiles/r04n_ab_ice_box.log).  DVH_BAND_BOX: 0 none, 1 (default) battery forms, 2 battery + ICE.
   const char* box_env = getenv("DVH_BAND_BOX");
-  const bool box = !(box_env && atoi(box_env) == 0);
-  DVH_HIP(h, dvh::launch_pdhg_band(b, w, ch, o, s, false, form_for(ch.count), box, nullptr, 0, &bvar));
+  const int box_mode = box_env ? atoi(box_env) : 1;
+  const bool box = box_mode >= 1, box_ice = box_mode >= 2;
+  // (order: the chunk's windows in the caller's launch order, dvh_set_launch_order; the results do not depend on it)
+  DVH_HIP(h, dvh::launch_pdhg_band(b, w, ch, o, s, false, form_for(ch.count), box, order, order ? ch.count : 0, &bvar));
   DVH_HIP(h, route(0, nullptr, ch.count, -2, 0, 0));
   if (box) DVH_HIP(h, route(1, nullptr, ch.count, -3, 0, 1));
   DVH_HIP(h, readback(0, box ? 2 : 1));
@@ -831,9 +854,12 @@ static int device_cascade(dvh_handle* h, const dvh::Batch& b, const dvh::Work& w
   h->n_band += nsmall - cur;
   if (nsmall - cur > 0) variant = bvar;
   if (cur > 0) {  // pass 2: the band kernel's ICE form over pass 1's refusals
-    DVH_HIP(h, dvh::launch_pdhg_band(b, w, ch, o, s, true, form_for(cur), false, L[0], cur, &bvar));
+    DVH_HIP(h, dvh::launch_pdhg_band(b, w, ch, o, s, true, form_for(cur), box_ice, L[0], cur, &bvar));
     DVH_HIP(h, route(1, L[0], cur, -2, 0, 4));
-    DVH_HIP(h, readback(1, 1));
+    if (box_ice) DVH_HIP(h, route(2, L[0], cur, -3, 0, 1));
+    DVH_HIP(h, readback(1, box_ice ? 2 : 1));
+    if (box_ice && rh[16] > 0)  // the plain ICE form over the ICE windows without a box
+      DVH_HIP(h, dvh::launch_pdhg_band(b, w, ch, o, s, true, form_for(rh[16]), false, L[1], rh[16], nullptr));
     const int left = rh[8];
     h->n_band += cur - left;
     if (cur - left > 0 && variant < 0) variant = bvar;
@@ -1007,12 +1033,13 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
   DVH_HIP(h, h->w_scal.ensure(D * (size_t)wc * dvh::kScal));
   DVH_HIP(h, h->w_fc.ensure(sizeof(float) * wn));
   DVH_HIP(h, h->w_fr.ensure(sizeof(float) * wm));
+  DVH_HIP(h, h->w_queue.ensure(sizeof(int32_t)));
   dvh::Work w{h->w_tptr.as<int32_t>(), h->w_tind.as<int32_t>(), h->w_tval.as<double>(), h->w_kval.as<double>(),
               h->w_rowof.as<int32_t>(), h->w_perm.as<int32_t>(), h->w_dr.as<double>(), h->w_dc.as<double>(),
               h->w_cs.as<double>(), h->w_ls.as<double>(), h->w_us.as<double>(), h->w_qs.as<double>(),
               h->w_vbuf.as<double>(), h->w_wbuf.as<double>(), h->w_tmpc.as<double>(), h->w_tmpr.as<double>(),
               h->w_longk.as<int32_t>(), h->w_longt.as<int32_t>(), h->d_hinv.as<double>(), h->w_scal.as<double>(),
-              h->w_fc.as<float>(), h->w_fr.as<float>()};
+              h->w_fc.as<float>(), h->w_fr.as<float>(), h->w_queue.as<int32_t>()};
   DVH_HIP(h, h->d_list.ensure(I * 5 * (size_t)wc));  // the cascade's five device lists (dvh_route.hip)
   DVH_HIP(h, h->d_route.ensure(I * 8 * 5));
   if (!h->route_host) DVH_HIP(h, hipHostMalloc((void**)&h->route_host, I * 8 * 5, hipHostMallocDefault));
@@ -1024,6 +1051,15 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
   DVH_HIP(h, hipEventRecord(h->ev[0], s));
   std::vector<double> scal;
   std::vector<int32_t> ist;
+  // dvh_set_launch_order: consumed by this solve; applied when it covers the batch, which is one chunk of small windows
+  const int32_t* order = nullptr;
+  h->order_used.swap(h->order);
+  h->order.clear();
+  if (!h->order_used.empty() && (int)h->order_used.size() == count && chunks.size() == 1 && chunks[0].nsmall == count) {
+    DVH_HIP(h, h->d_order.ensure(I * count));
+    DVH_HIP(h, hipMemcpyAsync(h->d_order.as<int32_t>(), h->order_used.data(), I * count, hipMemcpyHostToDevice, s));
+    order = h->d_order.as<int32_t>();
+  }
   for (const C& c : chunks) {
     if (c.nsmall == 0 && c.med.empty()) continue;
     if (h->chunk_used == h->chunk_events.size()) {
@@ -1053,7 +1089,7 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
       continue;
     }
     if (cascade) {
-      if (int rc = device_cascade(h, b, w, c.ch, o, c.nsmall, wc, c.mn, c.mm, s)) return rc;
+      if (int rc = device_cascade(h, b, w, c.ch, o, c.nsmall, wc, c.mn, c.mm, s, order)) return rc;
       if (int rc = chain_pass(h, b, w, c.ch, o, c.med, c.med_T, desc, med_done, s)) return rc;
       DVH_HIP(h, hipEventRecord(e2, s));
       continue;

@@ -24,6 +24,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "dvh_device.h"
@@ -76,6 +77,9 @@ __host__ __device__ inline size_t band_lds_bytes(int B, int S, bool ice, int LF)
 struct ColKkt {
   double rd2, cx, bt;
 };
+struct ColKktX : ColKkt {
+  double rdx;  // |r_d| |x| of the column, unscaled (the battery forms' objective gate)
+};
 __device__ __noinline__ ColKkt col_kkt_fn(double kt, double cj, double loj, double hij, double xj, float fd) {
   const double id = (double)__builtin_amdgcn_rcpf(fd);
   const double rs = cj - kt;  // scaled reduced cost
@@ -83,6 +87,19 @@ __device__ __noinline__ ColKkt col_kkt_fn(double kt, double cj, double loj, doub
   const double lam = (fl && fh) ? rs : (fl ? fmax(rs, 0.0) : (fh ? fmin(rs, 0.0) : 0.0));
   const double rd = (rs - lam) * id;
   return {rd * rd, cj * xj, (fl ? loj * fmax(lam, 0.0) : 0.0) + (fh ? hij * fmin(lam, 0.0) : 0.0)};
+}
+__device__ __noinline__ ColKktX col_kkt_fn_x(double kt, double cj, double loj, double hij, double xj, float fd) {
+  const double id = (double)__builtin_amdgcn_rcpf(fd);
+  const double rs = cj - kt;  // scaled reduced cost
+  const bool fl = isfinite(loj), fh = isfinite(hij);
+  const double lam = (fl && fh) ? rs : (fl ? fmax(rs, 0.0) : (fh ? fmin(rs, 0.0) : 0.0));
+  const double rd = (rs - lam) * id;
+  ColKktX r;
+  r.rd2 = rd * rd;
+  r.cx = cj * xj;
+  r.bt = (fl ? loj * fmax(lam, 0.0) : 0.0) + (fh ? hij * fmin(lam, 0.0) : 0.0);
+  r.rdx = fabs(rd) * fabs(xj * (double)fd);
+  return r;
 }
 struct RowKkt {
   double rp2, y2;
@@ -98,15 +115,15 @@ __device__ __noinline__ RowKkt row_kkt_fn(double kv, double qi, double yi, float
 // state and extra reduction raised the register allocation of the check path by 30-40 spilled VGPRs in every form
 // (profiles/r02zzk_ab_configs12_spills.log), which runs with the default options paid for nothing.
 //
-// BOX (box form, the default for the battery windows): every ch / dis / ene column has a finite box [lo, hi] in the
+// BOX (box form, the default): every ch / dis / ene (/ elec / on) column has a finite box [lo, hi] in the
 // scaled space, so the kernel iterates on x' = (x - lo) / w, w = hi - lo, whose box is [0, 1]: the projection is the
 // FMA's own clamp modifier (one v_fma_f64 ... clamp instead of v_fma + v_max + v_min per column and iteration).  The
 // change of variables is exact: K' = K diag(w) (both SpMV directions), c' = c w, q' = q - K lo, and a per-column
 // primal step tau / w^2 gives x' + (tau / w^2)(w g) = (x + tau g - lo) / w, i.e. the same PDHG iterates.  The
 // movement norms that drive restarts and the primal weight are taken in x units (w d'), the KKT check runs on the
 // primed LP, whose objectives, row residuals and (zero, for a two-sided box) column residuals equal the original's
-// once the constant c lo is added.  A window with an unbounded ch / dis / ene column is returned with status
-// kNeedsPlain and re-run by the plain form (dvh_api.cpp device_cascade).
+// once the constant c lo is added.  A window with an unbounded ch / dis / ene (/ elec / on) column is returned with
+// status kNeedsPlain and re-run by the plain form (dvh_api.cpp device_cascade).
 constexpr int kNeedsPlain = -3;
 __device__ __forceinline__ double fma_clamp01(double a, double b, double c) {
   double r;
@@ -115,15 +132,13 @@ __device__ __forceinline__ double fma_clamp01(double a, double b, double c) {
 }
 
 template <int B, int S, bool ICE, int LF, int WPS, bool GATE, bool BOX>
-__global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const Work w, const Chunk ch, const Opts o,
-                                                        const int32_t* list) {
-  static_assert(!BOX || (!ICE && !(LF & kLfImages)), "the box form covers the battery forms with images in LDS");
+__device__ __forceinline__ void band_window(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, const int k) {
+  static_assert(!BOX || !(LF & kLfImages), "the box form keeps the check images in LDS");
   constexpr int NW = B / kWave;
   constexpr int SB = S * B;        // step capacity
   constexpr int NC = ICE ? 5 : 3;  // columns per step: ch, dis, ene (, elec, on)
   constexpr int NR = ICE ? 4 : 2;  // rows per step: SOE, DCM (, ICE rated, ICE minimum)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int k = list ? list[blockIdx.x] : ch.first + (int)blockIdx.x;
   const int kl = k - ch.first;
   const WinOff W = win_offsets(b, ch, k);
   const int n = W.n, m = W.m, meq = W.meq;
@@ -217,6 +232,7 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
     crossed |= lraw[t] > uraw[t] || lraw[T + t] > uraw[T + t] || lraw[2 * T + t] > uraw[2 * T + t];
     if (BOX) unboxed |= !(isfinite(uraw[t]) && isfinite(uraw[T + t]) && isfinite(lraw[2 * T + t]) && isfinite(uraw[2 * T + t]));
     if (ICE) {
+      if (BOX) unboxed |= !(isfinite(uraw[CE + t]) && isfinite(uraw[CO + t]));
       bad |= lraw[CE + t] != 0.0 || lraw[CO + t] != 0.0;
       crossed |= lraw[CE + t] > uraw[CE + t] || lraw[CO + t] > uraw[CO + t];
     }
@@ -824,18 +840,18 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
   double pw = uniform(pwi);
   // ---- box form: x' = (x - lo) / w on the ch / dis / ene columns (after the scaling, the power iteration and the
   //      warm start's weight, which all see the original variables)
-  double tj[S][3];                      // per-column primal steps tau / w^2
+  double tj[S][3];  // per-column primal steps tau / w^2 of ch / dis / ene (elec / on: in RO, over their upper bounds)
   double* wbox = w.vbuf + W.wn;         // the columns' widths w (window workspace: read at checks, restarts, the end)
   double cbox = 0.0;                    // c lo, the objective's constant under the change of variables
   auto wcol = [&](int s, int v) { return val[s] ? wbox[opaque(col(s, v))] : 0.0; };
   if constexpr (BOX) {
-    double wb[S][3];
+    double wb[S][NC];
     bool unb = false;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
 #pragma unroll
-      for (int v = 0; v < 3; ++v) {
-        double wv = hi[s][v] - (v == 2 ? loe[s] : 0.0);  // padding steps: 0
+      for (int v = 0; v < NC; ++v) {
+        double wv = hib(s, v) - (v == 2 ? loe[s] : 0.0);  // padding steps: 0
         unb |= !isfinite(wv);
         if (!(wv >= 0x1p-500)) wv = 0.0;  // a (numerically) fixed column: x' = 0, x = lo
         wb[s][v] = wv;
@@ -872,10 +888,20 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
       ks[s][3] *= wn1;
       kd[s][0] *= wb[s][0];
       kd[s][1] *= wb[s][1];
+      if constexpr (ICE) {  // elec / on: the DCM row's elec term, the two ICE rows (their q: lo = 0, unchanged)
+        const double we = wb[s][NC > 3 ? 3 : 0], wo = wb[s][NC > 4 ? 4 : 0];
+        kd[s][3] *= we;
+        ka[s][0] *= we;
+        ka[s][1] *= wo;
+        kb[s][0] *= we;
+        kb[s][1] *= wo;
+      }
 #pragma unroll
-      for (int v = 0; v < 3; ++v) {
+      for (int v = 0; v < NC; ++v) {
         const double lo = v == 2 ? loe[s] : 0.0, wv = wb[s][v], cs = cof(s, v) * wv;
-        if (LC)
+        if (v >= 3)
+          ro(v - 3, s) = cs;
+        else if (LC)
           cqa(v, s) = cs;
         else
           cc[s][v] = cs;
@@ -907,9 +933,12 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
 #pragma unroll
       for (int s = 0; s < S; ++s)
 #pragma unroll
-        for (int v = 0; v < 3; ++v) {
-          const double wv = wcol(s, v);
-          tj[s][v] = wv > 0.0 ? tau / (wv * wv) : 0.0;
+        for (int v = 0; v < NC; ++v) {
+          const double wv = wcol(s, v), st = wv > 0.0 ? tau / (wv * wv) : 0.0;
+          if (v < 3)
+            tj[s][v < 3 ? v : 0] = st;
+          else
+            ro(v - 1, s) = st;
         }
     }
   };
@@ -1001,7 +1030,7 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
         for (int v = 0; v < NC; ++v) {  // branch-free: padding steps have c = lo = hi = 0 and stay at 0
           double p1;
           if constexpr (BOX) {
-            p1 = fma_clamp01(tj[s][v < 3 ? v : 0], kty[s][v], x[s][v]);
+            p1 = fma_clamp01(v < 3 ? tj[s][v < 3 ? v : 0] : ro(v - 1, s), kty[s][v], x[s][v]);
           } else {
             const double lo = v == 2 ? loe[s] : 0.0;
             p1 = vmin(vmax(fma(tau, kty[s][v], x[s][v]), lo), hib(s, v));
@@ -1010,7 +1039,7 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
           if (CHECK) {
             double d = x[s][v] - p1, da = p1 - axv(s, v);
             if constexpr (BOX) {  // movements in x units
-              const double wv = wcol(s, v < 3 ? v : 0);
+              const double wv = wcol(s, v);
               d *= wv;
               da *= wv;
             }
@@ -1123,13 +1152,16 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
     const bool last = it + chk > o.max_iters;
     bool kkt = (--kk_ == 0) || last;
     if (kkt) kk_ = kkt_every;
-    double acc[kNRed];
+    // the ICE form reduces the round-3 set (no dual-residual term in its objective gate): the extra value cost it 6 %
+    // on config 5 at unchanged iterations (register pressure of its check path; profiles/r04ab_ab_kkt_rdx.log)
+    constexpr int NRED = (ICE && DVH_KKT_RDX) ? kNRed - 1 : kNRed;
+    double acc[NRED];
     acc[0] = mv0;
     acc[1] = mv1;
     acc[2] = mv2;
     acc[3] = mv3;
 #pragma unroll
-    for (int u = 4; u < kNRed; ++u) acc[u] = 0.0;
+    for (int u = 4; u < NRED; ++u) acc[u] = 0.0;
     double r = 0.0;
     if constexpr (GATE) {
       // predicted KKT gate: the restart sums first; a due check runs only if the last check's worst ratio to eps,
@@ -1156,10 +1188,18 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
       lds_barrier();
       auto col_kkt = [&](int j, double kt, double cj, double loj, double hij, double xj) {
         const int jj = opaque(j);
-        const ColKkt r = col_kkt_fn(kt, cj, loj, hij, xj, w.fc[W.wn + jj]);
-        acc[5] += r.rd2;
-        acc[6] += r.cx;
-        acc[8] += r.bt;
+        if constexpr (NRED > kRdx && DVH_KKT_RDX) {
+          const ColKktX r = col_kkt_fn_x(kt, cj, loj, hij, xj, w.fc[W.wn + jj]);
+          acc[5] += r.rd2;
+          acc[6] += r.cx;
+          acc[8] += r.bt;
+          acc[kRdx] += r.rdx;
+        } else {
+          const ColKkt r = col_kkt_fn(kt, cj, loj, hij, xj, w.fc[W.wn + jj]);
+          acc[5] += r.rd2;
+          acc[6] += r.cx;
+          acc[8] += r.bt;
+        }
       };
       auto row_kkt = [&](int i, double kv, double qi, double yi, bool ge) {
         const int ii = opaque(i);
@@ -1220,15 +1260,15 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
     }
     if constexpr (GATE) {
       if (kkt) {  // the KKT sums in the slots after the restart sums' (red is not reused before a barrier)
-        double acc6[kNRed - 4];
+        double acc6[NRED - 4];
 #pragma unroll
-        for (int u = 4; u < kNRed; ++u) acc6[u - 4] = acc[u];
-        block_sum1<B, kNRed - 4, true>(acc6, red + 4 * NW);
+        for (int u = 4; u < NRED; ++u) acc6[u - 4] = acc[u];
+        block_sum1<B, NRED - 4, true>(acc6, red + 4 * NW);
 #pragma unroll
-        for (int u = 4; u < kNRed; ++u) acc[u] = acc6[u - 4];
+        for (int u = 4; u < NRED; ++u) acc[u] = acc6[u - 4];
       }
     } else if (kkt) {
-      block_sum1<B, kNRed, true>(acc, red);
+      block_sum1<B, NRED, true>(acc, red);
     } else {
       double acc4[4] = {acc[0], acc[1], acc[2], acc[3]};
       block_sum1<B, 4, true>(acc4, red);
@@ -1246,7 +1286,7 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
         fin[2] = dres;
         fin[3] = gap;
       }
-      if (kkt_done(o, pres, dres, gap, pobj, dobj, acc[4], acc[9])) {
+      if (kkt_done(o, pres, dres, gap, pobj, dobj, acc[4], acc[9], (NRED > kRdx && DVH_KKT_RDX) ? acc[kRdx] : 0.0)) {
         status = kOptimal;
         break;
       }
@@ -1335,12 +1375,57 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const Batch b, const 
   }
 }
 
-template <int B, int S, bool ICE, int LF, int WPS, bool GATE, bool BOX>
-hipError_t launch_band_one_g(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, hipStream_t s,
-                           const int32_t* list, int nlist, int* variant_out) {
+// Persistent form (PERSIST; the three-step battery form): the grid is the device's resident workgroup slots (two per CU),
+// and each workgroup takes the next window from an atomic counter until the list is exhausted, so a slot freed by a
+// short window takes the next one at once.  One workgroup per window left the slots to the hardware dispatcher,
+// which deals workgroups in order round-robin over the XCDs: with durations that vary window to window (warm
+// iterations 200 .. 10,000) the in-order dispatch leaves slots idle.  Measured: the bench's windows ran 7-8 % faster
+// when launched sorted by their own iteration counts (either direction, profiles/r04r_ab_launch_order.log), a
+// synthetic kernel of random durations lost 20 % to the sorted order (scripts/probe_dispatch.hip,
+// profiles/r04t_probe_dispatch.log: 33.5 vs 28.2 ms, persistent 29.9), and the persistent band kernel runs the
+// bench's PDHG in 467 vs 478 ms (profiles/r04u_ab_band_queue.log).  Its loop costs registers (64-68 spilled VGPRs in the
+// setup and check paths; the iteration's two paths keep none), which the ICE form cannot afford (config 5: 61k vs
+// 91k windows/s): the ICE and one-step forms stay one workgroup per window.  Every workgroup leaves once the counter
+// passes the list (the counter zeroed on the stream before the launch).
+struct BandArgs {
+  Batch b;
+  Work w;
+  Chunk ch;
+  Opts o;
+  const int32_t* list;  // global window indices, or null: the chunk
+  int count;            // windows to solve (list entries, or the chunk's)
+  int32_t* queue;       // work-queue counter (PERSIST), zeroed before the launch
+};
+template <int B, int S, bool ICE, int LF, int WPS, bool GATE, bool BOX, bool PERSIST>
+__global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const BandArgs args) {
+  if constexpr (!PERSIST) {
+    const int i = blockIdx.x;
+    band_window<B, S, ICE, LF, WPS, GATE, BOX>(args.b, args.w, args.ch, args.o,
+                                               args.list ? args.list[i] : args.ch.first + i);
+  } else {
+    __shared__ int32_t next;
+    for (;;) {
+      // wave 0 takes the next window in a wave-uniform branch, the whole wave in the atomic (lane 0 adds 1, the others
+      // 0): a lane-0-only atomic inside the loop is structurized into an inner loop whose barriers the waves do not
+      // reach in step (the workgroups hang: scripts/probe_dispatch.hip)
+      if (__builtin_amdgcn_readfirstlane(threadIdx.x) < kWave)
+        next = __builtin_amdgcn_readfirstlane(atomicAdd(args.queue, (threadIdx.x & (kWave - 1)) == 0 ? 1 : 0));
+      __syncthreads();
+      const int i = __builtin_amdgcn_readfirstlane(next);  // uniform: the loop's exit is a scalar branch
+      __syncthreads();  // (every wave has read it before wave 0 takes the next one)
+      if (i >= args.count) return;
+      band_window<B, S, ICE, LF, WPS, GATE, BOX>(args.b, args.w, args.ch, args.o,
+                                                 args.list ? args.list[i] : args.ch.first + i);
+    }
+  }
+}
+
+template <int B, int S, bool ICE, int LF, int WPS, bool GATE, bool BOX, bool PERSIST>
+hipError_t launch_band_one_q(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, hipStream_t s,
+                             const int32_t* list, int nlist, int* variant_out) {
   static_assert(B * S == kBandSteps, "every form covers T <= kBandSteps");
   const size_t lds = band_lds_bytes(B, S, ICE, LF);
-  auto kern = pdhg_band_kernel<B, S, ICE, LF, WPS, GATE, BOX>;
+  auto kern = pdhg_band_kernel<B, S, ICE, LF, WPS, GATE, BOX, PERSIST>;
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   if (getenv("DVH_BAND_OCC")) {  // residency diagnostics (A/B helper)
@@ -1351,12 +1436,41 @@ hipError_t launch_band_one_g(const Batch& b, const Work& w, const Chunk& ch, con
     hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kern, B, lds);
     hipFuncAttributes fa;
     hipFuncGetAttributes(&fa, (const void*)kern);
-    fprintf(stderr, "band<%d,%d,%d,%d,gate %d,box %d>: lds %zu B, blocks/CU %d, lds/CU %zu, regs %d, local %zu\n", B, S,
-            (int)ICE, LF, (int)GATE, (int)BOX, lds, nb, (size_t)pr.maxSharedMemoryPerMultiProcessor, fa.numRegs, (size_t)fa.localSizeBytes);
+    fprintf(stderr, "band<%d,%d,%d,%d,gate %d,box %d,persist %d>: lds %zu B, blocks/CU %d, lds/CU %zu, regs %d, local %zu\n",
+            B, S, (int)ICE, LF, (int)GATE, (int)BOX, (int)PERSIST, lds, nb, (size_t)pr.maxSharedMemoryPerMultiProcessor,
+            fa.numRegs, (size_t)fa.localSizeBytes);
   }
-  hipLaunchKernelGGL(kern, dim3(list ? nlist : ch.count), dim3(B), lds, s, b, w, ch, o, list);
+  const int count = list ? nlist : ch.count;
+  if (count <= 0) return hipSuccess;
+  int grid = count;
+  if (PERSIST) {  // every resident slot (workgroups per CU at this form x CUs), or fewer
+    static int slots_dev = -1, slots = 0;  // (per instantiation; recomputed when the current device changes)
+    int dev = 0;
+    if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+    if (dev != slots_dev) {
+      int nb = 0, cus = 0;
+      if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kern, B, lds)) != hipSuccess) return e;
+      if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
+      slots = std::max(1, nb) * std::max(1, cus);
+      slots_dev = dev;
+    }
+    grid = std::min(count, slots);
+    if ((e = hipMemsetAsync(w.queue, 0, sizeof(int32_t), s)) != hipSuccess) return e;
+  }
+  const BandArgs args{b, w, ch, o, list, count, w.queue};
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(B), lds, s, args);
   if (variant_out) *variant_out = 9000000 + 1000 * (S - 1) + (ICE ? 100 : 0) + B / kWave;
   return hipGetLastError();
+}
+template <int B, int S, bool ICE, int LF, int WPS, bool GATE, bool BOX>
+hipError_t launch_band_one_g(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, hipStream_t s,
+                             const int32_t* list, int nlist, int* variant_out) {
+  if constexpr (S == 3 && !ICE) {  // the persistent form (DVH_BAND_QUEUE=0: one workgroup per window, A/B)
+    const char* q = getenv("DVH_BAND_QUEUE");
+    if (!(q && atoi(q) == 0))
+      return launch_band_one_q<B, S, ICE, LF, WPS, GATE, BOX, true>(b, w, ch, o, s, list, nlist, variant_out);
+  }
+  return launch_band_one_q<B, S, ICE, LF, WPS, GATE, BOX, false>(b, w, ch, o, s, list, nlist, variant_out);
 }
 template <int B, int S, bool ICE, int LF, int WPS, bool BOX = false>
 hipError_t launch_band_one(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, hipStream_t s,
@@ -1385,7 +1499,10 @@ hipError_t launch_band_one(const Batch& b, const Work& w, const Chunk& ch, const
 #endif
 hipError_t launch_pdhg_band(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, hipStream_t s, bool ice,
                             int form, bool box, const int32_t* list, int nlist, int* variant_out) {
-  if (ice) return launch_band_one<kBandSteps, 1, true, DVH_BANDI_LF, 3>(b, w, ch, o, s, list, nlist, variant_out);
+  if (ice) {
+    if (box) return launch_band_one<kBandSteps, 1, true, DVH_BANDI_LF, 3, true>(b, w, ch, o, s, list, nlist, variant_out);
+    return launch_band_one<kBandSteps, 1, true, DVH_BANDI_LF, 3>(b, w, ch, o, s, list, nlist, variant_out);
+  }
   if (form == 1) {
     if (box) return launch_band_one<kBandSteps, 1, false, 0, 3, true>(b, w, ch, o, s, list, nlist, variant_out);
     return launch_band_one<kBandSteps, 1, false, 0, 3>(b, w, ch, o, s, list, nlist, variant_out);

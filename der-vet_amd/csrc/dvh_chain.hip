@@ -50,16 +50,17 @@ constexpr int kCB = kChainB;  // threads (and maximum steps) per segment
 constexpr int kTauWave = DVH_CHAIN_TAU_WAVE;  // the wave holding the tau slots (wave 0 holds the init / ghost row)
 static_assert(kTauWave >= 0 && kTauWave < kCB / kWave, "the tau wave exists");
 constexpr int kJSeg = kChainJSeg;  // tau columns per segment
-constexpr int kXSeg = 140;    // granules per segment in the exchange buffer
 // granule offsets inside a segment's area (p = round parity)
+constexpr int kCW = 2 * kNRed;  // granules per parity of the check sums (two per value)
 constexpr int kOffD = 0;      // + 2p: reflected first ene (down, to s-1)
 constexpr int kOffU = 4;      // + 6p: reflected ch, dis, ene of the last step (up, to s+1)
 constexpr int kOffA2 = 16;    // + 8p + 2u: partial K'y of tau slot u
 constexpr int kOffK = 32;     // + 12p: KKT images {first ene, 4 tau partials}
-constexpr int kOffC = 56;     // + 20p + 2v: check partial sums
-constexpr int kOffW = 96;     // + p: the team's next window (segment 0's area)
-constexpr int kOffAck = 98;   // + p: this segment has read it
-constexpr int kOffT = 100;    // + 20p + 2v: check sums over all segments (segment 0's area: the leader's)
+constexpr int kOffC = 56;     // + kCW p + 2v: check partial sums
+constexpr int kOffW = kOffC + 2 * kCW;  // + p: the team's next window (segment 0's area)
+constexpr int kOffAck = kOffW + 2;      // + p: this segment has read it
+constexpr int kOffT = kOffAck + 2;      // + kCW p + 2v: check sums over all segments (segment 0's area: the leader's)
+constexpr int kXSeg = kOffT + 2 * kCW;  // granules per segment in the exchange buffer
 // poll-list entries per segment: A [0, 256), K [256, 512), C [512, 1016), up [1016, 1022), down [1022, 1024)
 constexpr int kPollMax = 1024;
 constexpr int kPollK = 256, kPollC = 512, kPollU = 1016, kPollD = 1022;
@@ -71,14 +72,15 @@ typedef __attribute__((address_space(1))) int gi32;
 // KKT pieces of one column / one row (out of line, as in dvh_band.hip: the check runs every kkt_every * check_every
 // iterations and inlined it would raise the kernel's register allocation)
 struct ColKktC {
-  double rd2, cx, bt;
+  double rd2, cx, bt, rdx;
 };
 __device__ __noinline__ ColKktC col_kkt_c(double kt, double cj, double loj, double hij, double xj, double d) {
   const double rc = (cj - kt) / d;
   const bool fl = isfinite(loj), fh = isfinite(hij);
   const double lam = (fl && fh) ? rc : (fl ? fmax(rc, 0.0) : (fh ? fmin(rc, 0.0) : 0.0));
   const double rd = rc - lam;
-  return {rd * rd, cj * xj, (fl ? loj * d * fmax(lam, 0.0) : 0.0) + (fh ? hij * d * fmin(lam, 0.0) : 0.0)};
+  return {rd * rd, cj * xj, (fl ? loj * d * fmax(lam, 0.0) : 0.0) + (fh ? hij * d * fmin(lam, 0.0) : 0.0),
+          fabs(rd) * fabs(xj * d)};
 }
 struct RowKktC {
   double rp2, y2;
@@ -1003,7 +1005,7 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
           const int i = base + tid;
           const bool act = i < cnt;
           const int r = act ? 1 + i / nv : 0, v = act ? i % nv : 0;
-          gu64* g = tb + (int64_t)r * kXSeg + kOffC + 20 * par + 2 * v;
+          gu64* g = tb + (int64_t)r * kXSeg + kOffC + kCW * par + 2 * v;
           bool ok = !act;
           unsigned hi = 0, lo = 0, spins = 0;
           while (!__all(ok)) {
@@ -1037,12 +1039,12 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
         if (wid == 0 && lane < nv && !misc[0]) {
           double s = 0.0;
           for (int r = 0; r < P; ++r) s += CR[r * kNRed + lane];
-          put_f64(tb + kOffT + 20 * par + 2 * lane, tag, s);
+          put_f64(tb + kOffT + kCW * par + 2 * lane, tag, s);
           CR[lane] = s;
         }
       } else if (wid == 0) {
-        if (lane < nv) put_f64(mine + kOffC + 20 * par + 2 * lane, tag, mv);
-        if (lane < 2 * nv) poff[kPollC + lane] = (kOffT + lane) | (20 << 16);
+        if (lane < nv) put_f64(mine + kOffC + kCW * par + 2 * lane, tag, mv);
+        if (lane < 2 * nv) poff[kPollC + lane] = (kOffT + lane) | (kCW << 16);
         __builtin_amdgcn_wave_barrier();
         if (!poll(kPollC, 2 * nv, cC)) {
           if (lane == 0) misc[0] = 1;
@@ -1323,6 +1325,7 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
           acc[5] += r.rd2;
           acc[6] += r.cx;
           acc[8] += r.bt;
+          if (DVH_KKT_RDX) acc[kRdx] += r.rdx;
         };
         auto row_kkt = [&](int i, double kv, double qi, double yi, bool ge) {
           const RowKktC r = row_kkt_c(kv, qi, yi, drv[opaque(i)], ge);
@@ -1362,7 +1365,7 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
         fin[1] = pres;
         fin[2] = dres;
         fin[3] = gap;
-        if (kkt_done(o, pres, dres, gap, pobj, dobj, acc[4], acc[9])) {
+        if (kkt_done(o, pres, dres, gap, pobj, dobj, acc[4], acc[9], DVH_KKT_RDX ? acc[kRdx] : 0.0)) {
           status = kOptimal;
           break;
         }

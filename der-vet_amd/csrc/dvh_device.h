@@ -9,7 +9,11 @@
 namespace dvh {
 namespace {
 
-constexpr int kNRed = 10;  // values reduced by a termination (KKT) check
+#ifndef DVH_KKT_RDX
+#define DVH_KKT_RDX 1  // the objective gate's dual-residual term (kkt_done); 0: the round-3 gate (A/B builds)
+#endif
+constexpr int kNRed = 10 + DVH_KKT_RDX;  // values reduced by a termination (KKT) check ([10]: sum_j |r_d,j| |x_j|)
+constexpr int kRdx = DVH_KKT_RDX ? 10 : 0;  // its slot (an unused 0 slot without it)
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
 constexpr int kOptimal = 0, kIterLimit = 3, kNumerical = 4;
@@ -150,10 +154,14 @@ __device__ __forceinline__ void block_sum1(double (&v)[NV], double* red) {
 // and, with eps_obj > 0, the objective-error estimate |pobj - dobj| + ||y||_2 ||r_p||_2 <= eps_obj (1 + |pobj|)
 // (the gap plus the dual-weighted primal residual: what an infeasible candidate can gain on the optimum; it keeps
 // every window's objective within 1e-5 of HiGHS where the KKT test alone let 1.08e-5 through).
+// rdx: sum_j |r_d,j| |x_j|, what the dual objective can overstate the optimum by (p* >= dobj - sum_j
+// |r_d,j| |x*_j|, with x in place of x*): a window whose dual residual sits on a large column (the demand charge's tau)
+// otherwise stopped with its objective 1.6e-6 off (profiles/r04y_certify.json).  Every kernel and both restatements
+// (oracle/pdlp_ref.py, oracle/cpu_pdhg.cpp) apply it.
 __device__ __forceinline__ bool kkt_done(const Opts& o, double pres, double dres, double gap, double pobj,
-                                         double dobj, double rp2, double y2) {
+                                         double dobj, double rp2, double y2, double rdx = 0.0) {
   if (!(pres <= o.eps && dres <= o.eps && gap <= o.eps)) return false;
-  return !(o.eps_obj > 0.0) || fabs(pobj - dobj) + sqrt(rp2 * y2) <= o.eps_obj * (1.0 + fabs(pobj));
+  return !(o.eps_obj > 0.0) || fabs(pobj - dobj) + sqrt(rp2 * y2) + rdx <= o.eps_obj * (1.0 + fabs(pobj));
 }
 
 // Predicted KKT gate (dvh_options.kkt_predict = P > 0): a due KKT check is skipped while the last check's worst

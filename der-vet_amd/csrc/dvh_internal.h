@@ -90,6 +90,7 @@ struct Work {
   float* fc;        // [sum n]  Dc rounded to single precision (the band kernel's KKT checks; written by the band
                     //          kernels, whose factors stay within [2^-100, 2^100])
   float* fr;        // [sum m]  Dr rounded to single precision
+  int32_t* queue;   // [1] the band kernels' work-queue counter (zeroed before each launch)
 };
 
 struct Chunk {

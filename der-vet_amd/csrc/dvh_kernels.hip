@@ -706,6 +706,7 @@ __global__ __launch_bounds__(B) void pdhg_kernel(const Batch b, const Work w, co
       acc[5] += rd * rd;
       acc[6] += cj * xj;
       acc[8] += (fl ? loj * d * fmax(lam, 0.0) : 0.0) + (fh ? hij * d * fmin(lam, 0.0) : 0.0);
+      if (DVH_KKT_RDX) acc[kRdx] += fabs(rd) * fabs(xj * d);
     };
     auto row_kkt = [&](int i, double kx, double qi, double yi) {
       const double d = drv[i];
@@ -755,7 +756,7 @@ __global__ __launch_bounds__(B) void pdhg_kernel(const Batch b, const Work w, co
       fin[1] = pres;
       fin[2] = dres;
       fin[3] = gap;
-      if (kkt_done(o, pres, dres, gap, pobj, dobj, acc[4], acc[9])) {
+      if (kkt_done(o, pres, dres, gap, pobj, dobj, acc[4], acc[9], DVH_KKT_RDX ? acc[kRdx] : 0.0)) {
         status = kOptimal;
         break;
       }
@@ -1492,6 +1493,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(WPE))) void p
         acc[5] += rd * rd;
         acc[6] += cj * xj;
         acc[8] += (fl ? loj * d * fmax(lam, 0.0) : 0.0) + (fh ? hij * d * fmin(lam, 0.0) : 0.0);
+        if (DVH_KKT_RDX) acc[kRdx] += fabs(rd) * fabs(xj * d);
       };
       auto row_kkt = [&](int i, double kv, double qi, double yi2) {
         const double d = drv[opaque(i)];
@@ -1553,7 +1555,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(WPE))) void p
         fin[2] = dres;
         fin[3] = gap;
       }
-      if (kkt_done(o, pres, dres, gap, pobj, dobj, acc[4], acc[9])) {
+      if (kkt_done(o, pres, dres, gap, pobj, dobj, acc[4], acc[9], DVH_KKT_RDX ? acc[kRdx] : 0.0)) {
         status = kOptimal;
         break;
       }

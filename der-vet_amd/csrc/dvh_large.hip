@@ -458,11 +458,12 @@ __global__ __launch_bounds__(LB) void lg_kkt_rows(LgArgs a) {
   }
 }
 
-// KKT columns: reduced-cost residual |rc - lambda|^2, c'x, bound part of the dual objective.
+// KKT columns: reduced-cost residual |rc - lambda|^2, c'x, bound part of the dual objective, sum |r_d| |x| (the objective
+// gate's dual-residual term, csrc/dvh_device.h kkt_done).
 __global__ __launch_bounds__(LB) void lg_kkt_cols(LgArgs a) {
   const LgState* st = a.st;
   if (st->status >= 0 || !is_kkt_check(a, st)) return;
-  double v[3] = {0.0, 0.0, 0.0};
+  double v[4] = {0.0, 0.0, 0.0, 0.0};
   auto acc = [&](int j, double ktys) {
     const double rc = a.c[j] - ktys / a.dc[j];
     const double lo = a.l[j], hi = a.u[j];
@@ -472,6 +473,7 @@ __global__ __launch_bounds__(LB) void lg_kkt_cols(LgArgs a) {
     v[0] += rd * rd;
     v[1] += a.c[j] * (a.dc[j] * a.xo[j]);
     v[2] += (fl ? lo * fmax(lam, 0.0) : 0.0) + (fu ? hi * fmin(lam, 0.0) : 0.0);
+    v[3] += fabs(rd) * fabs(a.dc[j] * a.xo[j]);
   };
   if ((int)blockIdx.x < a.nbc) {
     const int j = blockIdx.x * LB + threadIdx.x;
@@ -480,7 +482,7 @@ __global__ __launch_bounds__(LB) void lg_kkt_cols(LgArgs a) {
       for (int e = 0; e < a.wc; ++e) kty += a.tv[(size_t)e * a.n + j] * a.yo[a.ti[(size_t)e * a.n + j]];
       acc(j, kty);
     }
-    lg_block_sum<3>(v);
+    lg_block_sum<4>(v);
   } else {
     const int L = blockIdx.x - a.nbc;
     double s[1] = {0.0};
@@ -492,6 +494,7 @@ __global__ __launch_bounds__(LB) void lg_kkt_cols(LgArgs a) {
     a.part[(size_t)blockIdx.x * kPart + 2] = v[0];
     a.part[(size_t)blockIdx.x * kPart + 3] = v[1];
     a.part[(size_t)blockIdx.x * kPart + 4] = v[2];
+    a.part[(size_t)blockIdx.x * kPart + 5] = v[3];
   }
 }
 
@@ -501,11 +504,11 @@ __global__ __launch_bounds__(1024) void lg_check(LgArgs a) {
   if (st->status >= 0) return;
   const int ncb = a.nbc + a.nlc, nrb = a.nbr + a.nlr;
   const bool kkt = is_kkt_check(a, st);
-  double cm[2], rm[2], ck[3] = {0.0, 0.0, 0.0}, rk[3] = {0.0, 0.0, 0.0};
+  double cm[2], rm[2], ck[4] = {0.0, 0.0, 0.0, 0.0}, rk[3] = {0.0, 0.0, 0.0};
   lg_reduce_parts<2>(a.part, 0, ncb, 0, cm);
   lg_reduce_parts<2>(a.part, ncb, nrb, 0, rm);
   if (kkt) {
-    lg_reduce_parts<3>(a.part, 0, ncb, 2, ck);
+    lg_reduce_parts<4>(a.part, 0, ncb, 2, ck);
     lg_reduce_parts<3>(a.part, ncb, nrb, 2, rk);
   }
   if (threadIdx.x != 0) return;
@@ -521,7 +524,8 @@ __global__ __launch_bounds__(1024) void lg_check(LgArgs a) {
     st->dres = sqrt(ck[0]) / (1.0 + st->nc);
     st->gap = fabs(pobj - dobj) / (1.0 + fabs(pobj) + fabs(dobj));
     st->pobj = pobj;
-    const bool obj_ok = !(a.eps_obj > 0.0) || fabs(pobj - dobj) + sqrt(rk[0] * rk[2]) <= a.eps_obj * (1.0 + fabs(pobj));
+    const bool obj_ok =
+        !(a.eps_obj > 0.0) || fabs(pobj - dobj) + sqrt(rk[0] * rk[2]) + ck[3] <= a.eps_obj * (1.0 + fabs(pobj));
     if (st->pres <= a.eps && st->dres <= a.eps && st->gap <= a.eps && obj_ok) {
       st->status = kOptimal;
       return;

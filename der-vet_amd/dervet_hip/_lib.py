@@ -120,6 +120,7 @@ SYMBOLS = {
     "dvh_last_chain_aborts": (ctypes.c_int, [ctypes.c_void_p, c_int32_p]),
     "dvh_last_warning": (ctypes.c_char_p, [ctypes.c_void_p]),
     "dvh_set_kernel_path": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "dvh_set_launch_order": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]),
     "dvh_outage_coverage": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(OutageCase), ctypes.c_int32, c_int32_p,
                                            c_double_p]),
     "dvh_outage_min_soe": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(OutageCase), ctypes.c_int32, c_int32_p,

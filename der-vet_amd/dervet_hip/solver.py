@@ -171,6 +171,13 @@ class BatchSolver:
         mode = (1 if path else 0) if isinstance(path, bool) else self._PATHS[path]
         self._check(self._lib.dvh_set_kernel_path(self._h, mode), "dvh_set_kernel_path")
 
+    def set_launch_order(self, order):
+        """The next solve launches its battery-band pass over the windows in this order (a permutation of the batch's
+        window indices; scheduling only, the results do not depend on it).  None / empty clears."""
+        o = np.ascontiguousarray(np.zeros(0, np.int32) if order is None else order, np.int32)
+        self._check(self._lib.dvh_set_launch_order(self._h, o.ctypes.data_as(ctypes.c_void_p), len(o)),
+                    "dvh_set_launch_order")
+
     def solve(self, lps, start=None):
         """Solve a list of WindowLP on the GPU; returns a list of WindowResult (same order).
 

@@ -288,12 +288,13 @@ def transfer_pairs(tr_list):
     return np.ascontiguousarray(np.concatenate(parts)) if parts else np.zeros((0, 3), np.int32)
 
 
-def transfer_device(solver, tr_list, pb, pairs=None):
+def transfer_device(solver, tr_list, pb, pairs=None, rows=None):
     """``transfer`` for a device-resident batch through the library (``dvh_warm_transfer``): one launch on the
-    solver's stream, ordered after the seed solve and before the warm one; no host-side tensor work."""
+    solver's stream, ordered after the seed solve and before the warm one; no host-side tensor work.
+    rows: ``transfer_rows(tr_list)`` when the caller keeps it (blends)."""
     import ctypes
     if pairs is None and any(t.weights is not None for t in tr_list):  # blends of several partners
-        rows, wts = transfer_rows(tr_list)
+        rows, wts = transfer_rows(tr_list) if rows is None else rows
         p = pb.as_ctypes()
         solver._check(solver._lib.dvh_warm_transfer_blend(
             solver._h, ctypes.byref(p), rows.ctypes.data_as(ctypes.c_void_p), wts.ctypes.data_as(ctypes.c_void_p),
@@ -376,6 +377,8 @@ class SeededSweep:
         rg = make_groups(self.rest_ids) if len(self.rest_ids) else []
         self.transfers = plan(sg, rg, partner_of, bl)
         self.pairs = transfer_pairs(self.transfers) if bl is None else None
+        self.rows = transfer_rows(self.transfers) if bl is not None else None
+        self._order_dev = None
         self.n_seed = sum(g.G for g in sg)
         self.tags = [t for g in sg + rg for t in g.tags]
         self.specs = None
@@ -393,6 +396,36 @@ class SeededSweep:
             from .lp import gpu_builder
             return gpu_builder.pack_specs_device(self.specs, solver, device)
         return self.packed.to_torch(device).alloc_outputs()
+
+    def _order_warm(self, solver, dev):
+        """Longest-expected-first launch order for the warm phase (dvh_set_launch_order): a rest window's expected
+        cost is its blend's weighted mean of the partner seeds' iteration counts, just solved (the only predictor
+        at hand: Spearman 0.18 with the warm count on the bench's 116,256 windows).  The band kernel's persistent
+        form takes windows in this order, so only the launch's tail depends on it: PDHG 467.4 -> 463.3 ms per
+        bench step (profiles/r04u_ab_band_queue.log; sorted by the windows' own counts, 441 ms, is the ceiling).  On
+        the device (torch) apart from the permutation's copy to the host, which the library validates.
+        DVH_SWEEP_ORDER=0: packing order (prev / prevasc / random: diagnostics of the r04r study)."""
+        if self.rows is None or os.environ.get("DVH_SWEEP_ORDER", "1") == "0":
+            return
+        import torch
+        rows, wts = self.rows
+        n_rest = dev.count - self.n_seed
+        if len(rows) != n_rest:
+            return
+        if self._order_dev is None or self._order_dev[0].device != dev.istats.device:
+            self._order_dev = (torch.as_tensor(rows[:, 1:-1].astype(np.int64), device=dev.istats.device),
+                               torch.as_tensor(wts, device=dev.istats.device),
+                               torch.as_tensor(rows[:, 0].astype(np.int64) - self.n_seed, device=dev.istats.device))
+        part, w, win = self._order_dev
+        iters = dev.istats.view(-1, 2)[:, 1].to(torch.float64)
+        if os.environ.get("DVH_SWEEP_ORDER") in ("prev", "prevasc"):  # diagnostic: the previous solve's own counts
+            pred = iters[win + self.n_seed] * (-1.0 if os.environ["DVH_SWEEP_ORDER"] == "prevasc" else 1.0)
+        elif os.environ.get("DVH_SWEEP_ORDER") == "random":  # diagnostic
+            pred = torch.rand(len(win), generator=torch.Generator().manual_seed(7), dtype=torch.float64).to(win.device)
+        else:
+            pred = (w * iters[part]).sum(1)
+        order = win[torch.argsort(pred, descending=True, stable=True)].to(torch.int32).cpu().numpy()
+        solver.set_launch_order(order)
 
     def solve(self, solver, dev, warm_options=None, seed_options=None):
         """dev: this sweep's packed batch on the device (``self.packed.to_torch(..).alloc_outputs()``).
@@ -425,7 +458,8 @@ class SeededSweep:
         if cnt > self.n_seed:
             if dev.x.is_cuda and not os.environ.get("DVH_SWEEP_TORCH_TRANSFER"):
                 # one launch on the library's stream (the seed solve has completed on it)
-                transfer_device(solver, self.transfers, dev, self.pairs)
+                transfer_device(solver, self.transfers, dev, self.pairs, self.rows)
+                self._order_warm(solver, dev)
             else:  # host tensors (tests), or the torch formulation for A/B timing
                 transfer(self.transfers, dev.x, dev.y, dev.c, dev.u)
                 if dev.x.is_cuda:

@@ -345,6 +345,14 @@ int dvh_last_outage_ms(const dvh_handle* h, double* ms);
  * per compute unit, else the three-step form. */
 int dvh_set_kernel_path(dvh_handle* h, int mode);
 
+/* Launch order of the next solve (scheduling only: the results do not depend on it).  order: host array, a
+ * permutation of 0 .. count - 1 (validated; DVH_ERR_ARG otherwise), copied.  The next dvh_solve_packed_device /
+ * dvh_solve_batch launches its battery-band pass over the windows in this order when count equals its window count
+ * and the batch is one chunk of on-chip windows (else the packing order); the order is consumed by that solve.
+ * Longest-expected-first orders shorten the launch's tail (dervet_hip/sweep.py orders a warm phase by its seeds'
+ * iteration counts).  count 0 clears. */
+int dvh_set_launch_order(dvh_handle* h, const int32_t* order, int32_t count);
+
 #ifdef __cplusplus
 }
 #endif

@@ -167,7 +167,7 @@ void solve_one(const dvh_lp& lp, const dvh_options& o, const double* x0, const d
     }
   };
   struct Kkt {
-    double pres, dres, gap, pobj, dobj, pabs, ynorm;
+    double pres, dres, gap, pobj, dobj, pabs, ynorm, rdx;
   };
   std::vector<double> xs(n), ys(m), res(m), rc(n);
   auto kkt = [&]() {
@@ -185,12 +185,13 @@ void solve_one(const dvh_lp& lp, const dvh_options& o, const double* x0, const d
     std::fill(rc.begin(), rc.end(), 0.0);
     for (int r = 0; r < m; ++r)
       for (int k = K.p[r]; k < K.p[r + 1]; ++k) rc[K.j[k]] += K.v[k] * ys[r];
-    double dr = 0, cx = 0, bt = 0;
+    double dr = 0, cx = 0, bt = 0, rdx = 0;
     for (int c = 0; c < n; ++c) {
       const double g = lp.c[c] - rc[c];
       const bool fl = std::isfinite(lp.l[c]), fh = std::isfinite(lp.u[c]);
       const double lam = (fl && fh) ? g : (fl ? std::max(g, 0.0) : (fh ? std::min(g, 0.0) : 0.0));
       dr += (g - lam) * (g - lam);
+      rdx += std::fabs(g - lam) * std::fabs(xs[c]);
       cx += lp.c[c] * xs[c];
       bt += (fl ? lp.l[c] * std::max(lam, 0.0) : 0.0) + (fh ? lp.u[c] * std::min(lam, 0.0) : 0.0);
     }
@@ -199,6 +200,7 @@ void solve_one(const dvh_lp& lp, const dvh_options& o, const double* x0, const d
     k.dobj = qy + bt + lp.c0;
     k.pabs = std::sqrt(pr);
     k.ynorm = std::sqrt(yn);
+    k.rdx = rdx;
     k.pres = k.pabs / (1.0 + qn);
     k.dres = std::sqrt(dr) / (1.0 + cn);
     k.gap = std::fabs(k.pobj - k.dobj) / (1.0 + std::fabs(k.pobj) + std::fabs(k.dobj));
@@ -222,8 +224,9 @@ void solve_one(const dvh_lp& lp, const dvh_options& o, const double* x0, const d
         have = true;
         lx = xp;
         ly = yp;
-        const bool obj_ok = !(o.eps_obj > 0.0) ||
-                            std::fabs(last.pobj - last.dobj) + last.ynorm * last.pabs <= o.eps_obj * (1.0 + std::fabs(last.pobj));
+        // objective gate (csrc/dvh_device.h kkt_done): gap + ||y|| ||r_p|| + sum_j |r_d,j| |x_j|
+        const bool obj_ok = !(o.eps_obj > 0.0) || std::fabs(last.pobj - last.dobj) + last.ynorm * last.pabs + last.rdx <=
+                                                       o.eps_obj * (1.0 + std::fabs(last.pobj));
         if (last.pres <= o.eps && last.dres <= o.eps && last.gap <= o.eps && obj_ok) {
           out.status = DVH_OPTIMAL;
           break;
@@ -413,6 +416,7 @@ int dvh_last_chain_aborts(const dvh_handle*, int32_t* out) {
 }
 const char* dvh_last_warning(const dvh_handle*) { return ""; }
 int dvh_set_kernel_path(dvh_handle*, int) { return DVH_OK; }
+int dvh_set_launch_order(dvh_handle*, const int32_t*, int32_t) { return DVH_OK; }
 int dvh_outage_coverage(dvh_handle*, const dvh_outage_case*, int32_t, int32_t*, double*) { return DVH_ERR_UNSUPPORTED; }
 int dvh_outage_min_soe(dvh_handle*, const dvh_outage_case*, int32_t, const int32_t*, double*) {
   return DVH_ERR_UNSUPPORTED;

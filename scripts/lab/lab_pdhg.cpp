@@ -488,6 +488,7 @@ int dvh_last_chain_aborts(const dvh_handle*, int32_t* out) {
 }
 const char* dvh_last_warning(const dvh_handle*) { return ""; }
 int dvh_set_kernel_path(dvh_handle*, int) { return DVH_OK; }
+int dvh_set_launch_order(dvh_handle*, const int32_t*, int32_t) { return DVH_OK; }
 void lab_set_traj(int* t) { g_traj = t; }
 int dvh_outage_coverage(dvh_handle*, const dvh_outage_case*, int32_t, int32_t*, double*) { return DVH_ERR_UNSUPPORTED; }
 int dvh_outage_min_soe(dvh_handle*, const dvh_outage_case*, int32_t, const int32_t*, double*) {

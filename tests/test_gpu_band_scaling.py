@@ -130,3 +130,45 @@ def test_unbounded_column_goes_to_the_plain_form(gpu_solver):
         assert h["status"] == 0 and res[i].status == 0, (i, res[i].status_name)
         assert abs(res[i].obj - h["obj"]) <= 1e-5 * abs(h["obj"]), (i, res[i].obj, h["obj"])
     assert abs(res[2].x[2 * T2 + 5] - l2[2 * T2 + 5]) <= 1e-9 * abs(l2[2 * T2 + 5]), res[2].x[2 * T2 + 5]
+
+
+@pytest.mark.parametrize("box", ["1", "2"])
+def test_ice_window_without_a_box_goes_to_the_plain_ice_form(gpu_solver, monkeypatch, box):
+    """The ICE form's box (opt-in, DVH_BAND_BOX=2) covers elec / on too: an ICE window whose elec_t has no upper bound
+    is returned by the box form and solved by the plain ICE form in the same pass, to HiGHS's optimum (and by the
+    plain ICE form directly by default)."""
+    monkeypatch.setenv("DVH_BAND_BOX", box)
+    lps = [lp for g in scenarios.config5([4], years=1) for lp in builder.group_window_lps(g)][:3]
+    lp = lps[1]
+    T = lp.m_eq - 1
+    J = lp.n - 5 * T
+    u = lp.u.copy()
+    u[3 * T + J + 10] = np.inf  # elec_10
+    lps[1] = dataclasses.replace(lp, u=u)
+    res = gpu_solver.solve(lps)
+    ks = gpu_solver.kernel_stats()
+    assert ks["band_windows"] == len(lps) and ks["ell_windows"] == 0 and ks["generic_windows"] == 0, ks
+    for i in (0, 1):
+        o, h = _highs(lps[i])
+        assert h["status"] == 0 and res[i].status == 0, (i, res[i].status_name)
+        assert abs(res[i].obj - h["obj"]) <= 1e-5 * abs(h["obj"]), (i, res[i].obj, h["obj"])
+
+
+def test_launch_order_changes_scheduling_only(gpu_solver):
+    """dvh_set_launch_order: the band pass launches its windows in the given order (the seeded sweep's warm phase
+    runs longest-expected-first); every window's result is bit-identical to the packing-order solve, the order is
+    consumed by one solve, and a non-permutation is refused."""
+    from dervet_hip.solver import SolverError
+    lps = [lp for g in scenarios.config4(range(2)) for lp in builder.group_window_lps(g)]
+    a = gpu_solver.solve(lps)
+    gpu_solver.set_launch_order(np.arange(len(lps))[::-1])
+    b = gpu_solver.solve(lps)
+    for ra, rb in zip(a, b):
+        assert ra.status == rb.status == 0 and ra.iters == rb.iters and ra.obj == rb.obj
+        assert np.array_equal(ra.x, rb.x) and np.array_equal(ra.y, rb.y)
+    for bad in ([0, 0, 1], [1, 2, 3], [-1]):
+        with pytest.raises(SolverError, match="permutation"):
+            gpu_solver.set_launch_order(np.array(bad))
+    gpu_solver.set_launch_order(np.arange(len(lps) + 1))  # a different count: ignored by the next solve
+    c = gpu_solver.solve(lps)
+    assert all(ra.obj == rc.obj for ra, rc in zip(a, c))
