@@ -61,8 +61,13 @@ def _parity(pb, st, xs, sample, procs):
             "highs_windows_per_s": round(len(idx) / wall, 2), "highs_procs": used}
 
 
-def run(name, note, pb, solver, reps, sample, procs, sweep=None):
+def run(name, note, pb, solver, reps, sample, procs, sweep=None, options=None):
     dev = pb.to_torch("cuda:0").alloc_outputs()
+    restore = None
+    if options:  # dvh_options of this workload (restored after it)
+        o0 = solver.options()
+        restore = {k: getattr(o0, k) for k in options}
+        solver.set_options(**options)
     best, tm, paths = None, None, None
     for r in range(reps + 1):
         torch.cuda.synchronize()
@@ -88,6 +93,9 @@ def run(name, note, pb, solver, reps, sample, procs, sweep=None):
             "optimal": int((ist[:, 0] == 0).sum()),
             "kernel_path": {k: v for k, v in paths.items() if k.endswith("_windows")},
             "parity": _parity(pb, st, xs, sample, procs) if sample > 0 else None}
+    if options:
+        line["options"] = dict(options)
+        solver.set_options(**restore)
     print(json.dumps(line), flush=True)
     del dev
     return line
@@ -195,9 +203,12 @@ def main():
             meta = _json.load(f)
         names = ("es", "es+pv", "es+pv+dg")
         sigs = {nm: {k.split("__", 1)[1]: v for k, v in arr.items() if k.startswith(nm + "__")} for nm in names}
-        run("market-uc3", "Usecase 3 daily DA + FR windows, 3 golden cases x 365 days (LP relaxation of binary = 1)",
-            P([scenarios.market_days(sigs[nm], meta[nm]["params"]) for nm in names]), s, args.reps, args.sample,
-            args.procs)
+        days = P([scenarios.market_days(sigs[nm], meta[nm]["params"]) for nm in names])
+        run("market-uc3", "Usecase 3 daily DA + FR windows, 3 golden cases x 365 days (LP relaxation of binary = 1), "
+            "market options (scenarios.MARKET_OPTIONS)", days, s, args.reps, args.sample, args.procs,
+            options=scenarios.MARKET_OPTIONS)
+        run("market-uc3-default-options", "the same days with the library's default options (theta = 1)", days, s,
+            args.reps, args.sample, args.procs)
         groups = []
         for nm in names:
             sg, pdis = sigs[nm], float(meta[nm]["params"]["Battery"]["dis_max_rated"])
@@ -210,8 +221,8 @@ def main():
                       up_max=np.full(N, 0.25 * pdis), up_min=np.zeros(N), down_max=np.full(N, 0.25 * pdis),
                       down_min=np.zeros(N), combined=False)
             groups.append(scenarios.market_days(sg, meta[nm]["params"], reserves=res, lf=lf))
-        run("market-uc3+lf+sr+nsr", "the same 3 x 365 days with load following + SR + NSR (synthetic prices)",
-            P(groups), s, args.reps, args.sample, args.procs)
+        run("market-uc3+lf+sr+nsr", "the same 3 x 365 days with load following + SR + NSR (synthetic prices), market "
+            "options", P(groups), s, args.reps, args.sample, args.procs, options=scenarios.MARKET_OPTIONS)
     if 5 in only:
         config5_horizon(s, range(args.c5_scenarios), args.c5_years, args)
     if 8 in only:

@@ -313,6 +313,15 @@ def config5(scenarios, years=20, start_year=2017, min_soe=None, cap_min_soe=Fals
     return groups
 
 
+# dvh_options for market-service day windows (Usecase 3 style): primal-weight smoothing theta = 0.5 (PDLP's omega
+# <- exp(theta log(dy/dx) + (1 - theta) log(omega)) at restarts).  On the 1,095 golden days (algorithm lab, host cores)
+# the slowest day takes 5,504 iterations instead of 7,424 and the mean 1,589 instead of 1,799, objectives within 3e-7
+# of the theta = 1 solve; a batch of days is latency-bound on its slowest window, so the wall time follows the max.
+# Not the library default: on the battery / DCM windows of config 4 theta = 0.5 costs 18 % cold and 6 % warm
+# iterations, and config 3's DCM + PV window takes 1.85x as many.
+MARKET_OPTIONS = {"primal_weight_theta": 0.5}
+
+
 def market_days(signals, params, relax=True, days=None, name="es", reserves=None, lf=None):
     """Daily DA + frequency-regulation windows (Usecase 3 style) as one
     market_group.  signals: dict of [N] arrays da_price, regu_price, regd_price, fr_price, agg_emin, agg_emax,

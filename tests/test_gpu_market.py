@@ -54,6 +54,25 @@ def test_market_days_match_highs_and_bound_golden(gpu_solver, name):
     print(f"{name}: {len(days)} days, worst objective rel err {worst:.2e}")
 
 
+def test_market_options_keep_the_golden_bars_and_cut_the_slowest_day():
+    """scenarios.MARKET_OPTIONS (primal-weight smoothing theta = 0.5) on all 1,095 golden days through the default
+    cascade (the small ELL kernels): every day optimal within 1e-5 of the theta = 1 solve (which the test above pins
+    to HiGHS on its days), and the slowest day needs fewer iterations -- what a latency-bound batch of days waits for."""
+    lps = []
+    for name in ("es", "es+pv", "es+pv+dg"):
+        sig, meta = _signals(name)
+        lps += builder.group_window_lps(scenarios.market_days(sig, meta["params"]))
+    with BatchSolver(0) as s:
+        base = s.solve(lps)
+        s.set_options(**scenarios.MARKET_OPTIONS)
+        mk = s.solve(lps)
+    assert all(r.status == 0 for r in base) and all(r.status == 0 for r in mk)
+    for a, b in zip(base, mk):
+        assert abs(a.obj - b.obj) <= OBJ_TOL * max(abs(a.obj), 1.0), (a.obj, b.obj)
+    it0, it1 = max(r.iters for r in base), max(r.iters for r in mk)
+    assert it1 < 0.85 * it0, (it0, it1)
+
+
 def test_market_days_without_relaxation_row(gpu_solver):
     """relax=False: the same daily windows without the relaxation row (the binary = 0 form of the market LP)."""
     sig, meta = _signals("es")
