@@ -132,7 +132,8 @@ __device__ __forceinline__ double fma_clamp01(double a, double b, double c) {
 }
 
 template <int B, int S, bool ICE, int LF, int WPS, bool GATE, bool BOX>
-__device__ __forceinline__ void band_window(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, const int k) {
+__device__ __forceinline__ void band_window(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, const int k,
+                                            const int tid) {
   static_assert(!BOX || !(LF & kLfImages), "the box form keeps the check images in LDS");
   constexpr int NW = B / kWave;
   constexpr int SB = S * B;        // step capacity
@@ -142,7 +143,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
   const int kl = k - ch.first;
   const WinOff W = win_offsets(b, ch, k);
   const int n = W.n, m = W.m, meq = W.meq;
-  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   double* scal = w.scal + (int64_t)kl * kScal;
   const int T = meq - 1, J = n - (ICE ? 5 : 3) * T, MI = m - meq;
   const int MD = ICE ? MI - 2 * T : MI;  // DCM rows
@@ -1383,10 +1384,13 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
 // when launched sorted by their own iteration counts (either direction, profiles/r04r_ab_launch_order.log), a
 // synthetic kernel of random durations lost 20 % to the sorted order (scripts/probe_dispatch.hip,
 // profiles/r04t_probe_dispatch.log: 33.5 vs 28.2 ms, persistent 29.9), and the persistent band kernel runs the
-// bench's PDHG in 467 vs 478 ms (profiles/r04u_ab_band_queue.log).  Its loop costs registers (64-68 spilled VGPRs in the
-// setup and check paths; the iteration's two paths keep none), which the ICE form cannot afford (config 5: 61k vs
-// 91k windows/s): the ICE and one-step forms stay one workgroup per window.  Every workgroup leaves once the counter
-// passes the list (the counter zeroed on the stream before the launch).
+// bench's PDHG in 467 vs 478 ms (profiles/r04u_ab_band_queue.log).  The persistent instantiations (the three-step
+// battery form and the ICE form) are compiled in dvh_band_persist.hip without machine-level loop-invariant code motion:
+// built with it, the window setup's invariants were hoisted out of the loop over windows and spilled (12.6 % slower per
+// iteration, and the ICE form 61k vs 91k windows/s on config 5).  Now the battery form's PDHG runs 441 vs 459 ms and
+// config 5 112.7k vs 95.6k windows/s (profiles/r04al_band_persist_nolicm.log, r04an_ab_ice_queue.log); the one-step
+// battery form stays one workgroup per window.  Every workgroup leaves once the counter passes the list (the counter
+// zeroed on the stream before the launch).
 struct BandArgs {
   Batch b;
   Work w;
@@ -1401,10 +1405,20 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const BandArgs args) 
   if constexpr (!PERSIST) {
     const int i = blockIdx.x;
     band_window<B, S, ICE, LF, WPS, GATE, BOX>(args.b, args.w, args.ch, args.o,
-                                               args.list ? args.list[i] : args.ch.first + i);
+                                               args.list ? args.list[i] : args.ch.first + i, threadIdx.x);
   } else {
     __shared__ int32_t next;
     for (;;) {
+#if defined(__HIP_DEVICE_COMPILE__)
+      // The arguments are read through a kernarg pointer the compiler cannot see through, once per window: read as
+      // `args`, their ~70 scalar loads were hoisted out of this loop and kept live across the window (SGPRs spilled
+      // to VGPR lanes, 56 dwords of VGPRs to scratch; 12.6 % slower per iteration than one workgroup per window at
+      // equal durations, profiles/r04ak_band_queue_iter.log).  Laundered, each window reloads what it uses.
+      using KArgs = const __attribute__((address_space(4))) BandArgs*;
+      KArgs kp = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
+      asm volatile("" : "+s"(kp));
+      const BandArgs& args = *(const BandArgs*)kp;
+#endif
       // wave 0 takes the next window in a wave-uniform branch, the whole wave in the atomic (lane 0 adds 1, the others
       // 0): a lane-0-only atomic inside the loop is structurized into an inner loop whose barriers the waves do not
       // reach in step (the workgroups hang: scripts/probe_dispatch.hip)
@@ -1414,12 +1428,22 @@ __global__ __launch_bounds__(B, WPS) void pdhg_band_kernel(const BandArgs args) 
       const int i = __builtin_amdgcn_readfirstlane(next);  // uniform: the loop's exit is a scalar branch
       __syncthreads();  // (every wave has read it before wave 0 takes the next one)
       if (i >= args.count) return;
+      int tid = threadIdx.x;
+#if defined(__HIP_DEVICE_COMPILE__)
+      asm volatile("" : "+v"(tid));  // (likewise what the window derives from its thread index)
+#endif
       band_window<B, S, ICE, LF, WPS, GATE, BOX>(args.b, args.w, args.ch, args.o,
-                                                 args.list ? args.list[i] : args.ch.first + i);
+                                                 args.list ? args.list[i] : args.ch.first + i, tid);
     }
   }
 }
 
+#ifndef DVH_BANDI_LF
+#define DVH_BANDI_LF 0
+#endif
+#ifndef DVH_BAND3_LF
+#define DVH_BAND3_LF kLfCosts
+#endif
 template <int B, int S, bool ICE, int LF, int WPS, bool GATE, bool BOX, bool PERSIST>
 hipError_t launch_band_one_q(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, hipStream_t s,
                              const int32_t* list, int nlist, int* variant_out) {
@@ -1466,9 +1490,16 @@ template <int B, int S, bool ICE, int LF, int WPS, bool GATE, bool BOX>
 hipError_t launch_band_one_g(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, hipStream_t s,
                              const int32_t* list, int nlist, int* variant_out) {
   if constexpr (S == 3 && !ICE) {  // the persistent form (DVH_BAND_QUEUE=0: one workgroup per window, A/B)
+    static_assert(B == kBandSteps / 3 && LF == DVH_BAND3_LF && WPS == 2, "dvh_band_persist.hip instantiates this form");
     const char* q = getenv("DVH_BAND_QUEUE");
-    if (!(q && atoi(q) == 0))
-      return launch_band_one_q<B, S, ICE, LF, WPS, GATE, BOX, true>(b, w, ch, o, s, list, nlist, variant_out);
+    if (!(q && atoi(q) == 0)) return launch_band_persist(GATE, BOX, b, w, ch, o, s, list, nlist, variant_out);
+  }
+  if constexpr (ICE) {  // the ICE form's persistent grid (DVH_BAND_QUEUE=0 or DVH_BAND_QUEUE_ICE=0: off, A/B)
+    static_assert(B == kBandSteps && S == 1 && LF == DVH_BANDI_LF && WPS == 3, "dvh_band_persist.hip instantiates this form");
+    const char* q = getenv("DVH_BAND_QUEUE");
+    const char* qi = getenv("DVH_BAND_QUEUE_ICE");
+    if (!(q && atoi(q) == 0) && !(qi && atoi(qi) == 0))
+      return launch_band_persist_ice(GATE, BOX, b, w, ch, o, s, list, nlist, variant_out);
   }
   return launch_band_one_q<B, S, ICE, LF, WPS, GATE, BOX, false>(b, w, ch, o, s, list, nlist, variant_out);
 }
@@ -1491,12 +1522,33 @@ hipError_t launch_band_one(const Batch& b, const Work& w, const Chunk& ch, const
 // workspace (kLfImages) 5 % slower and 10x the HBM writes, with the anchors in LDS too (kLfAnchors) 8 % slower.
 // form 1: 768 threads, one step per lane, 12 waves, one window per CU (A/B, dvh_set_kernel_path 3).  The LP-relaxed
 // ICE windows keep the one-step form (twice the per-step state).
-#ifndef DVH_BANDI_LF
-#define DVH_BANDI_LF 0
-#endif
-#ifndef DVH_BAND3_LF
-#define DVH_BAND3_LF kLfCosts
-#endif
+#if DVH_BAND_PERSIST_TU
+// The persistent forms (three-step battery, ICE), compiled in dvh_band_persist.hip (this file with DVH_BAND_PERSIST_TU) without
+// machine-level loop-invariant code motion: hoisted out of the persistent loop, the window setup's invariants stayed live
+// across every window's iterations (56 spilled dwords, 12.6 % slower per iteration than one workgroup per window at
+// equal durations; 1.6 % without the hoisting, profiles/r04al_band_persist_nolicm.log).  The one-workgroup forms keep
+// the hoisting (this build of them is 1.4 % slower per iteration).
+hipError_t launch_band_persist(bool gate, bool box, const Batch& b, const Work& w, const Chunk& ch, const Opts& o,
+                               hipStream_t s, const int32_t* list, int nlist, int* variant_out) {
+  constexpr int B = kBandSteps / 3;
+  if (gate) {
+    if (box) return launch_band_one_q<B, 3, false, DVH_BAND3_LF, 2, true, true, true>(b, w, ch, o, s, list, nlist, variant_out);
+    return launch_band_one_q<B, 3, false, DVH_BAND3_LF, 2, true, false, true>(b, w, ch, o, s, list, nlist, variant_out);
+  }
+  if (box) return launch_band_one_q<B, 3, false, DVH_BAND3_LF, 2, false, true, true>(b, w, ch, o, s, list, nlist, variant_out);
+  return launch_band_one_q<B, 3, false, DVH_BAND3_LF, 2, false, false, true>(b, w, ch, o, s, list, nlist, variant_out);
+}
+hipError_t launch_band_persist_ice(bool gate, bool box, const Batch& b, const Work& w, const Chunk& ch, const Opts& o,
+                                   hipStream_t s, const int32_t* list, int nlist, int* variant_out) {
+  constexpr int B = kBandSteps;
+  if (gate) {
+    if (box) return launch_band_one_q<B, 1, true, DVH_BANDI_LF, 3, true, true, true>(b, w, ch, o, s, list, nlist, variant_out);
+    return launch_band_one_q<B, 1, true, DVH_BANDI_LF, 3, true, false, true>(b, w, ch, o, s, list, nlist, variant_out);
+  }
+  if (box) return launch_band_one_q<B, 1, true, DVH_BANDI_LF, 3, false, true, true>(b, w, ch, o, s, list, nlist, variant_out);
+  return launch_band_one_q<B, 1, true, DVH_BANDI_LF, 3, false, false, true>(b, w, ch, o, s, list, nlist, variant_out);
+}
+#else
 hipError_t launch_pdhg_band(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, hipStream_t s, bool ice,
                             int form, bool box, const int32_t* list, int nlist, int* variant_out) {
   if (ice) {
@@ -1510,5 +1562,6 @@ hipError_t launch_pdhg_band(const Batch& b, const Work& w, const Chunk& ch, cons
   if (box) return launch_band_one<kBandSteps / 3, 3, false, DVH_BAND3_LF, 2, true>(b, w, ch, o, s, list, nlist, variant_out);
   return launch_band_one<kBandSteps / 3, 3, false, DVH_BAND3_LF, 2>(b, w, ch, o, s, list, nlist, variant_out);
 }
+#endif
 
 }  // namespace dvh

@@ -124,6 +124,12 @@ hipError_t launch_pdhg_ell(const Batch& b, const Work& w, const Chunk& ch, const
 // ch / dis / ene column come back with status -3 (kNeedsPlain) and must be re-run with box = false.
 hipError_t launch_pdhg_band(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, hipStream_t s, bool ice,
                             int form, bool box, const int32_t* list, int nlist, int* variant_out);
+// Its persistent forms (dvh_band_persist.hip), the default for the three-step battery form and the ICE form unless
+// DVH_BAND_QUEUE=0 (DVH_BAND_QUEUE_ICE=0: the ICE form only); gate: dvh_options.kkt_predict > 0.
+hipError_t launch_band_persist(bool gate, bool box, const Batch& b, const Work& w, const Chunk& ch, const Opts& o,
+                               hipStream_t s, const int32_t* list, int nlist, int* variant_out);
+hipError_t launch_band_persist_ice(bool gate, bool box, const Batch& b, const Work& w, const Chunk& ch, const Opts& o,
+                                   hipStream_t s, const int32_t* list, int nlist, int* variant_out);
 size_t setup_lds_bytes(int max_n, int max_m);
 // Setup (scaling, transpose) of the listed medium windows (scaling vectors kept in the global workspace).
 hipError_t launch_setup_medium(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n,

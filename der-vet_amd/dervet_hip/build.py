@@ -10,8 +10,12 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "..", "csrc")
 LIB = os.path.join(HERE, "libdervet_hip.so")
-SOURCES = ["dvh_kernels.hip", "dvh_band.hip", "dvh_chain.hip", "dvh_build.hip", "dvh_sweep.hip", "dvh_series.hip", "dvh_route.hip", "dvh_large.hip", "dvh_outage.hip",
+SOURCES = ["dvh_kernels.hip", "dvh_band.hip", "dvh_band_persist.hip", "dvh_chain.hip", "dvh_build.hip", "dvh_sweep.hip", "dvh_series.hip", "dvh_route.hip", "dvh_large.hip", "dvh_outage.hip",
            "dvh_api.cpp", "dvh_validate.cpp"]
+# per-source flags: the band kernel's persistent form without machine-level loop-invariant code motion (its loop
+# invariants, hoisted out of the loop over windows, spilled; csrc/dvh_band_persist.hip)
+EXTRA_FLAGS = {"dvh_band_persist.hip": ["-mllvm", "-disable-machine-licm"]}
+INCLUDES = {"dvh_band_persist.hip": "dvh_band.hip"}  # (a one-line source around another: its compile time)
 HEADERS = ["dvh_internal.h", "dvh_device.h", "dvh_validate.h", "dvh_rng.h", "dvh_ziggurat.h", os.path.join("..", "..", "include", "dervet_hip.h")]
 
 
@@ -33,11 +37,11 @@ def build(force=False, verbose=False):
     objdir = os.path.join(HERE, "build_obj")
     os.makedirs(objdir, exist_ok=True)
     # longest first, so the pool's tail is short
-    order = sorted(SOURCES, key=lambda f: -os.path.getsize(os.path.join(CSRC, f)))
+    order = sorted(SOURCES, key=lambda f: -os.path.getsize(os.path.join(CSRC, INCLUDES.get(f, f))))
     objs = {f: os.path.join(objdir, f + ".o") for f in SOURCES}
 
     def compile_one(f):
-        cmd = [hipcc, *flags, "-c", os.path.join(CSRC, f), "-o", objs[f]]
+        cmd = [hipcc, *flags, *EXTRA_FLAGS.get(f, []), "-c", os.path.join(CSRC, f), "-o", objs[f]]
         if verbose:
             print(" ".join(cmd), flush=True)
         return f, subprocess.run(cmd, capture_output=True, text=True)

@@ -10,7 +10,9 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "der-vet_amd", "csrc")
-DEFAULT = ["dvh_band.hip", "dvh_kernels.hip", "dvh_chain.hip", "dvh_large.hip", "dvh_build.hip", "dvh_sweep.hip",
+sys.path.insert(0, os.path.join(ROOT, "der-vet_amd"))
+from dervet_hip.build import EXTRA_FLAGS  # noqa: E402  (per-source flags of the library build)
+DEFAULT = ["dvh_band.hip", "dvh_band_persist.hip", "dvh_kernels.hip", "dvh_chain.hip", "dvh_large.hip", "dvh_build.hip", "dvh_sweep.hip",
            "dvh_outage.hip"]
 
 
@@ -48,7 +50,7 @@ def main(argv):
     files = argv or DEFAULT
     for f in files:
         p = f if os.path.exists(f) else os.path.join(CSRC, f)
-        for k in usage(p):
+        for k in usage(p, EXTRA_FLAGS.get(os.path.basename(p), ())):
             if "VGPRs" not in k:
                 continue
             print(f"{os.path.basename(p):16s} vgpr {k['VGPRs']:>4s} spill_v {k.get('VGPRs Spill', '?'):>3s} "
