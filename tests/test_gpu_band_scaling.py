@@ -172,3 +172,24 @@ def test_launch_order_changes_scheduling_only(gpu_solver):
     gpu_solver.set_launch_order(np.arange(len(lps) + 1))  # a different count: ignored by the next solve
     c = gpu_solver.solve(lps)
     assert all(ra.obj == rc.obj for ra, rc in zip(a, c))
+
+
+@pytest.mark.parametrize("form", ["battery", "ice"])
+def test_persistent_form_matches_one_workgroup_per_window(gpu_solver, monkeypatch, form):
+    """The persistent band forms (csrc/dvh_band_persist.hip: the grid is the resident slots, each workgroup takes the
+    next window from a counter; built without machine LICM) change scheduling only: with more windows than slots, so
+    that workgroups run several windows one after another, every window's result is bit-identical to the
+    one-workgroup-per-window launch (DVH_BAND_QUEUE=0)."""
+    if form == "battery":
+        lps = [lp for g in scenarios.config4(range(48)) for lp in builder.group_window_lps(g)]  # 576 > 512 slots
+    else:
+        lps = [lp for g in scenarios.config5(range(24), years=1) for lp in builder.group_window_lps(g)]  # 288 > 256
+    a = gpu_solver.solve(lps)
+    assert gpu_solver.kernel_stats()["band_windows"] == len(lps)
+    monkeypatch.setenv("DVH_BAND_QUEUE", "0")
+    b = gpu_solver.solve(lps)
+    monkeypatch.delenv("DVH_BAND_QUEUE")
+    assert gpu_solver.kernel_stats()["band_windows"] == len(lps)
+    for i, (ra, rb) in enumerate(zip(a, b)):
+        assert ra.status == rb.status == 0 and ra.iters == rb.iters and ra.obj == rb.obj, (i, ra.iters, rb.iters)
+        assert np.array_equal(ra.x, rb.x) and np.array_equal(ra.y, rb.y), i
