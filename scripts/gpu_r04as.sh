@@ -1,0 +1,10 @@
+#!/bin/bash
+# Sanity pass on the committed tree (rebuilt library): smoke, the band tests, a short bench.
+set -o pipefail
+O=gpurun_out/r04as; mkdir -p $O
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log | cut -c1-160
+timeout -k 10 300 python -u -m pytest tests/test_gpu_band_scaling.py tests/test_gpu_market.py -m gpu -x -q --timeout 200 --timeout-method thread > $O/tests.log 2>&1 || { echo "tests failed"; tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 > $O/bench.log 2>&1 || { echo "bench failed"; tail -30 $O/bench.log; exit 1; }
+grep '^{' $O/bench.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['roofline']['frac'], d['roofline']['source_key'], d['roofline']['traffic'])"
