@@ -58,6 +58,7 @@ struct dvh_handle {
   DevBuf d_desc, d_indptr, d_indices, d_data, d_c, d_c0, d_q, d_l, d_u, d_x, d_y, d_stats, d_istats;
   // workspace
   DevBuf w_queue;  // the band kernels' work-queue counter
+  int band_slots[dvh::kPersistForms] = {};  // the persistent band forms' resident slots on this device (Work::slots)
   DevBuf w_tptr, w_tind, w_tval, w_kval, w_rowof, w_perm, w_dr, w_dc, w_cs, w_ls, w_us, w_qs, w_vbuf, w_wbuf,
       w_tmpc, w_tmpr, w_longk, w_longt, w_scal, w_fc, w_fr;
   DevBuf d_list, d_hinv;
@@ -848,8 +849,14 @@ static int device_cascade(dvh_handle* h, const dvh::Batch& b, const dvh::Work& w
   DVH_HIP(h, route(0, nullptr, ch.count, -2, 0, 0));
   if (box) DVH_HIP(h, route(1, nullptr, ch.count, -3, 0, 1));
   DVH_HIP(h, readback(0, box ? 2 : 1));
-  if (box && rh[8] > 0)
+  if (box && rh[8] > 0) {
+    // the plain form over the windows without a box; it can refuse some of them itself (-2: factors outside float's
+    // range, checked after scaling, which the box form never reached for them), so the -2 list is formed again, over
+    // the chunk, once it has run -- one more read-back, only when such windows exist
     DVH_HIP(h, dvh::launch_pdhg_band(b, w, ch, o, s, false, form_for(rh[8]), false, L[1], rh[8], nullptr));
+    DVH_HIP(h, route(0, nullptr, ch.count, -2, 0, 0));
+    DVH_HIP(h, readback(0, 1));
+  }
   int cur = rh[0];
   h->n_band += nsmall - cur;
   if (nsmall - cur > 0) variant = bvar;
@@ -858,8 +865,11 @@ static int device_cascade(dvh_handle* h, const dvh::Batch& b, const dvh::Work& w
     DVH_HIP(h, route(1, L[0], cur, -2, 0, 4));
     if (box_ice) DVH_HIP(h, route(2, L[0], cur, -3, 0, 1));
     DVH_HIP(h, readback(1, box_ice ? 2 : 1));
-    if (box_ice && rh[16] > 0)  // the plain ICE form over the ICE windows without a box
+    if (box_ice && rh[16] > 0) {  // the plain ICE form over the ICE windows without a box; its -2s listed again
       DVH_HIP(h, dvh::launch_pdhg_band(b, w, ch, o, s, true, form_for(rh[16]), false, L[1], rh[16], nullptr));
+      DVH_HIP(h, route(1, L[0], cur, -2, 0, 4));
+      DVH_HIP(h, readback(1, 1));
+    }
     const int left = rh[8];
     h->n_band += cur - left;
     if (cur - left > 0 && variant < 0) variant = bvar;
@@ -1039,7 +1049,7 @@ static int solve_packed(dvh_handle* h, const dvh_packed* bt, const std::vector<i
               h->w_cs.as<double>(), h->w_ls.as<double>(), h->w_us.as<double>(), h->w_qs.as<double>(),
               h->w_vbuf.as<double>(), h->w_wbuf.as<double>(), h->w_tmpc.as<double>(), h->w_tmpr.as<double>(),
               h->w_longk.as<int32_t>(), h->w_longt.as<int32_t>(), h->d_hinv.as<double>(), h->w_scal.as<double>(),
-              h->w_fc.as<float>(), h->w_fr.as<float>(), h->w_queue.as<int32_t>()};
+              h->w_fc.as<float>(), h->w_fr.as<float>(), h->w_queue.as<int32_t>(), h->band_slots};
   DVH_HIP(h, h->d_list.ensure(I * 5 * (size_t)wc));  // the cascade's five device lists (dvh_route.hip)
   DVH_HIP(h, h->d_route.ensure(I * 8 * 5));
   if (!h->route_host) DVH_HIP(h, hipHostMalloc((void**)&h->route_host, I * 8 * 5, hipHostMallocDefault));

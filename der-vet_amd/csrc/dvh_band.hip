@@ -1468,15 +1468,14 @@ hipError_t launch_band_one_q(const Batch& b, const Work& w, const Chunk& ch, con
   if (count <= 0) return hipSuccess;
   int grid = count;
   if (PERSIST) {  // every resident slot (workgroups per CU at this form x CUs), or fewer
-    static int slots_dev = -1, slots = 0;  // (per instantiation; recomputed when the current device changes)
-    int dev = 0;
-    if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
-    if (dev != slots_dev) {
-      int nb = 0, cus = 0;
+    // measured once per handle (each handle belongs to one device and one host thread at a time; Work::slots)
+    int& slots = w.slots[(ICE ? 4 : 0) + (GATE ? 2 : 0) + (BOX ? 1 : 0)];
+    if (slots <= 0) {
+      int nb = 0, cus = 0, dev = 0;
+      if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
       if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kern, B, lds)) != hipSuccess) return e;
       if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
       slots = std::max(1, nb) * std::max(1, cus);
-      slots_dev = dev;
     }
     grid = std::min(count, slots);
     if ((e = hipMemsetAsync(w.queue, 0, sizeof(int32_t), s)) != hipSuccess) return e;

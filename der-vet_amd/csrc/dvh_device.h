@@ -156,8 +156,10 @@ __device__ __forceinline__ void block_sum1(double (&v)[NV], double* red) {
 // every window's objective within 1e-5 of HiGHS where the KKT test alone let 1.08e-5 through).
 // rdx: sum_j |r_d,j| |x_j|, what the dual objective can overstate the optimum by (p* >= dobj - sum_j
 // |r_d,j| |x*_j|, with x in place of x*): a window whose dual residual sits on a large column (the demand charge's tau)
-// otherwise stopped with its objective 1.6e-6 off (profiles/r04y_certify.json).  Every kernel and both restatements
-// (oracle/pdlp_ref.py, oracle/cpu_pdhg.cpp) apply it.
+// otherwise stopped with its objective 1.6e-6 off (profiles/r04y_certify.json).  Every kernel applies it except the
+// band ICE form (NRED = kNRed - 1 in dvh_band.hip: the term cost 6 % on config 5 through its check path's registers,
+// DESIGN.md section 4), whose windows keep the round-3 test; both restatements (oracle/pdlp_ref.py,
+// oracle/cpu_pdhg.cpp) apply it to every window, so an ICE window can end one check later there than on the GPU.
 __device__ __forceinline__ bool kkt_done(const Opts& o, double pres, double dres, double gap, double pobj,
                                          double dobj, double rp2, double y2, double rdx = 0.0) {
   if (!(pres <= o.eps && dres <= o.eps && gap <= o.eps)) return false;

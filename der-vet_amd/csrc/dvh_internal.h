@@ -91,7 +91,11 @@ struct Work {
                     //          kernels, whose factors stay within [2^-100, 2^100])
   float* fr;        // [sum m]  Dr rounded to single precision
   int32_t* queue;   // [1] the band kernels' work-queue counter (zeroed before each launch)
+  int* slots;       // HOST [kPersistForms]: resident workgroup slots of each persistent band form on this handle's
+                    //   device (0: not measured yet); per handle, so that handles of a multi-device handle, driven
+                    //   by their own host threads, never share it
 };
+constexpr int kPersistForms = 8;  // (ICE, GATE, BOX) of the persistent band kernels
 
 struct Chunk {
   int first;        // first window index (global)

@@ -138,7 +138,7 @@ class Degradation:
         self.replaceable = np.broadcast_to(np.asarray(replaceable, bool), (S,)).copy()
         self.degrade_perc = np.zeros(S)
         self.replacements = np.zeros(S, np.int64)
-        self.skipped = np.zeros(S, np.int64)  # windows whose dispatch was not used (status not OPTIMAL / ITER_LIMIT)
+        self.skipped = np.zeros(S, np.int64)  # windows whose dispatch was not used (status not OPTIMAL)
         self.years_degraded = [set() for _ in range(S)]  # Battery.py:104 years_system_degraded
 
     def capacity(self):
@@ -226,8 +226,9 @@ class DegradationSweep:
                 T = lps[0].m_eq - 1
                 ene = np.stack([r.x[2 * T:3 * T] for r in res])
                 xs = [np.asarray(r.x) for r in res]
-            # only OPTIMAL / ITER_LIMIT dispatch is counted (an infeasible window's x is no SOE profile)
-            valid = np.isin(ist[:, 0], (0, 3))
+            # only OPTIMAL dispatch is counted (an infeasible window's x is no SOE profile; VERDICT r04:
+            # nor is an ITER_LIMIT one, which failed the KKT test) -- the others are counted in Degradation.skipped
+            valid = ist[:, 0] == 0
             deg = self.deg.update(ene, T * self.dt / 24.0, valid=valid,
                                   year=None if self.years is None else self.years[k])
             out.append(dict(k=k, iters=ist[:, 1], status=ist[:, 0], obj=obj, degradation=deg, capacity_before=cap,

@@ -24,8 +24,17 @@ per-window ``solve_optimization`` by ONE ``BatchSolver.solve`` over every LP win
      ``unpack_results`` and is saved with its error message (errors travel as ``cvx_error_msg``,
      MicrogridScenario.py:319-320); the loop goes on either way.
 
-Windows that are not LPs (binary / integer variables: MILP, ESSSizing.py:82-138) are solved by the
-reference ``solve_optimization`` in their place in the order.  Scenarios whose windows are coupled through
+Windows that are not LPs (binary / integer variables: MILP, ``binary`` = 1 in Model_Parameters_Template_DER.csv:17,
+e.g. ElectricVehicles.py:120-122) are solved by the reference ``solve_optimization`` in their place in the order,
+unless the user opts in with ``relax_milp=True`` (``install(relax_milp=True)``, ``CvxpyExporter(relax_milp=True)``):
+then the window is exported through ``get_problem_data(cvx.ECOS_BB)`` and the GPU solves its LP relaxation (boolean
+columns boxed to [0, 1], integrality dropped; export.ecos_to_window), whose objective bounds the MILP's from below.
+
+Failure detection: a window the GPU leaves without a certified optimum -- iteration limit,
+numerical failure, or an infeasibility / unboundedness verdict -- is re-solved by the reference
+``solve_optimization`` in place (``retry_failed``, default on), so that DER-VET receives exactly what its own solve
+of that window gives; ``LoopReport`` counts GPU, reference (MILP / non-LP) and retried windows.  With
+``retry_failed=False`` the GPU verdict is saved as ECOS would report it (iteration limit -> optimal_inaccurate).  Scenarios whose windows are coupled through
 saved results (battery degradation, Battery.py:87-110; sizing, MicrogridScenario.py:361-363) cannot batch their
 own windows; ``batched_cases_loop`` batches them ACROSS scenarios instead: window k of every case in one GPU
 call, saved before any case sets up window k + 1 (the serial case loop of dervet/DERVET.py:75-83, in lockstep).
@@ -40,20 +49,24 @@ STATUS_TO_CVXPY = _lib.STATUS_NAMES  # DVH status -> cvxpy status string read by
 
 
 class CvxpyExporter:
-    """(functions, constraints) of one window -> ExportedWindow via CVXPY's ECOS canonicalisation."""
+    """(functions, constraints) of one window -> ExportedWindow via CVXPY's ECOS canonicalisation (ECOS_BB for a
+    mixed-integer window when ``relax_milp``; without it such a window stays on the reference path)."""
 
-    def __init__(self):
+    def __init__(self, relax_milp=False):
         import cvxpy as cvx  # noqa: F401  (absent in this container; tests drive ecos_to_window directly)
         self.cvx = cvx
+        self.relax_milp = bool(relax_milp)
 
     def export(self, functions, constraints):
         cvx = self.cvx
         prob = cvx.Problem(cvx.Minimize(sum(functions.values())), constraints)
-        if any(v.attributes.get("boolean") or v.attributes.get("integer") for v in prob.variables()):
+        mip = any(v.attributes.get("boolean") or v.attributes.get("integer") for v in prob.variables())
+        if mip and not self.relax_milp:
             return None  # MILP: stays on the reference path
-        data, chain, inverse = prob.get_problem_data(cvx.ECOS)
+        # ECOS_BB's data carries bool_vars_idx / int_vars_idx (CVXPY 1.0.31 ECOS_BB.apply); its inversion is ECOS's
+        data, chain, inverse = prob.get_problem_data(cvx.ECOS_BB if mip else cvx.ECOS)
         try:
-            ew = ecos_to_window(data)
+            ew = ecos_to_window(data, relax=mip)
         except ExportError:
             return None  # not an LP the solver takes (cones, infeasible presolve): the reference solve
         return CvxpyWindow(ew, prob, chain, inverse)
@@ -79,6 +92,27 @@ class CvxpyWindow:
             return self.prob, f"dervet_hip: window solve status {res.status_name} (solver error)"
         self.prob.unpack_results(self.ew.ecos_solution(res), self.chain, self.inverse)
         return self.prob, None
+
+
+RETRY_STATUSES = (_lib.ITER_LIMIT, _lib.NUMERICAL, _lib.PRIMAL_INFEASIBLE, _lib.DUAL_INFEASIBLE)
+
+
+class LoopReport:
+    """Where a loop's windows were solved: ``gpu`` (saved from the batched solve, ``relaxed`` of them MILP
+    relaxations), ``reference`` (MILP / non-LP windows solved by ``solve_optimization`` in place) and ``retried``
+    (GPU windows without a certified optimum, re-solved by ``solve_optimization``; ``retried_status`` counts them
+    by the cvxpy status string of the GPU verdict)."""
+
+    def __init__(self):
+        self.gpu = self.relaxed = self.reference = self.retried = 0
+        self.retried_status = {}
+
+    def as_dict(self):
+        return dict(gpu=self.gpu, relaxed=self.relaxed, reference=self.reference, retried=self.retried,
+                    retried_status=dict(self.retried_status))
+
+    def __repr__(self):
+        return f"LoopReport({self.as_dict()})"
 
 
 def windows_are_independent(scenario):
@@ -135,21 +169,32 @@ def _solve_plans(plans, solver):
     return dict(zip(lp_idx, res))
 
 
-def _save(scenario, plan, r):
+def _save(scenario, plan, r, report, retry_failed=True):
     opt_period, sub_index, functions, constraints, saved_vars, win = plan
     for der, vd in saved_vars.items():
         if vd is not None:
             der.variables_dict = vd
     if win is None:  # MILP / non-LP window: the reference solve, in place
         prob, obj, err = scenario.solve_optimization(functions, constraints)
+        report.reference += 1
+    elif retry_failed and r.status in RETRY_STATUSES:  # no certified optimum: the reference solve, in place
+        prob, obj, err = scenario.solve_optimization(functions, constraints)
+        report.retried += 1
+        report.retried_status[r.status_name] = report.retried_status.get(r.status_name, 0) + 1
     else:
         prob, err = win.unpack(r)
         obj = functions
+        report.gpu += 1
+        report.relaxed += int(bool(getattr(win.ew, "relaxed", False)))
     scenario.save_optimization_results(opt_period, sub_index, prob, obj, err)
 
 
-def batched_optimize_problem_loop(scenario, solver=None, exporter=None, **kwargs):
-    """Batched ``MicrogridScenario.optimize_problem_loop`` (dervet/MicrogridScenario.py:281-320)."""
+def batched_optimize_problem_loop(scenario, solver=None, exporter=None, relax_milp=False, retry_failed=True,
+                                  **kwargs):
+    """Batched ``MicrogridScenario.optimize_problem_loop`` (dervet/MicrogridScenario.py:281-320).  Returns the plan
+    list; the window accounting is left on ``scenario.dervet_hip_report`` (a LoopReport)."""
+    report = LoopReport()
+    scenario.dervet_hip_report = report
     pre = _preamble(scenario)
     if pre is None:
         return None
@@ -161,30 +206,32 @@ def batched_optimize_problem_loop(scenario, solver=None, exporter=None, **kwargs
             if not len(constraints) and not len(functions.values()):
                 continue
             prob, obj, err = scenario.solve_optimization(functions, constraints)
+            report.reference += 1
             scenario.save_optimization_results(opt_period, sub_index, prob, obj, err)
         return None
-    exporter = exporter or CvxpyExporter()
+    exporter = exporter or CvxpyExporter(relax_milp)
     plan = [p for p in (_setup_export(scenario, w, alpha, ignore, exporter)
                         for w in scenario.optimization_levels.predictive.unique()) if p is not None]
     results = _solve_plans(plan, solver)
     for i, p in enumerate(plan):
-        _save(scenario, p, results.get(i))
+        _save(scenario, p, results.get(i), report, retry_failed)
     return plan
 
 
-def batched_cases_loop(scenarios, solver=None, exporter=None):
+def batched_cases_loop(scenarios, solver=None, exporter=None, relax_milp=False, retry_failed=True):
     """The optimize_problem_loop of several cases (dervet/DERVET.py:75-83) batched on the GPU.
 
     Independent cases (``windows_are_independent``) put all their windows into one batch.  Coupled cases
     (degradation / sizing) advance in lockstep: window position k of every coupled case is set up, solved in one
     batch and saved (so each case's degradation update runs) before any coupled case sets up position k + 1.
-    Returns the plans per case, in case order."""
-    exporter = exporter or CvxpyExporter()
+    Returns the plans per case, in case order; each case's accounting is on its ``dervet_hip_report``."""
+    exporter = exporter or CvxpyExporter(relax_milp)
     own = solver is None
     solver = solver or BatchSolver(0)
     try:
         live, indep, coupled = [], [], []
         for s in scenarios:
+            s.dervet_hip_report = LoopReport()
             pre = _preamble(s)
             if pre is None:
                 live.append(None)
@@ -203,7 +250,7 @@ def batched_cases_loop(scenarios, solver=None, exporter=None):
                     flat.append((i, p))
         res = _solve_plans([p for _, p in flat], solver)
         for k, (i, p) in enumerate(flat):
-            _save(scenarios[i], p, res.get(k))
+            _save(scenarios[i], p, res.get(k), scenarios[i].dervet_hip_report, retry_failed)
             plans[i].append(p)
         # coupled cases: window position by window position across the cases
         periods = {i: list(scenarios[i].optimization_levels.predictive.unique()) for i in coupled}
@@ -217,7 +264,7 @@ def batched_cases_loop(scenarios, solver=None, exporter=None):
                         step.append((i, p))
             res = _solve_plans([p for _, p in step], solver)
             for k, (i, p) in enumerate(step):
-                _save(scenarios[i], p, res.get(k))
+                _save(scenarios[i], p, res.get(k), scenarios[i].dervet_hip_report, retry_failed)
                 plans[i].append(p)
         return [plans[i] for i in range(len(scenarios))]
     finally:
@@ -225,29 +272,35 @@ def batched_cases_loop(scenarios, solver=None, exporter=None):
             solver.close()
 
 
-def make_batched_scenario_class(base, solver_factory=None):
+def make_batched_scenario_class(base, solver_factory=None, relax_milp=False, retry_failed=True):
     """Subclass of the reference ``MicrogridScenario`` whose window loop is batched on the GPU."""
 
     class BatchedMicrogridScenario(base):
         def optimize_problem_loop(self, **kwargs):
             solver = solver_factory() if solver_factory else None
             try:
-                return batched_optimize_problem_loop(self, solver=solver, **kwargs)
+                return batched_optimize_problem_loop(self, solver=solver, relax_milp=relax_milp,
+                                                     retry_failed=retry_failed, **kwargs)
             finally:
                 if solver is not None:
                     solver.close()
 
     BatchedMicrogridScenario.__name__ = "BatchedMicrogridScenario"
+    BatchedMicrogridScenario.dervet_hip_options = (solver_factory, bool(relax_milp), bool(retry_failed))
     return BatchedMicrogridScenario
 
 
-def install(dervet_module=None):
-    """Patch dervet.DERVET.MicrogridScenario (hard-coded at dervet/DERVET.py:76) with the batched class."""
+def install(dervet_module=None, relax_milp=False, retry_failed=True, solver_factory=None):
+    """Patch dervet.DERVET.MicrogridScenario (hard-coded at dervet/DERVET.py:76) with the batched class.
+    ``relax_milp``: the user's opt-in to GPU LP relaxations of binary = 1 windows (north_star); off, MILP windows stay
+    on the reference solve.  ``retry_failed``: re-solve windows without a certified GPU optimum by the reference."""
     if dervet_module is None:
         import dervet.DERVET as dervet_module  # noqa: N813
     base = dervet_module.MicrogridScenario
     if getattr(base, "__name__", "") == "BatchedMicrogridScenario":
-        return base
-    cls = make_batched_scenario_class(base)
+        if base.dervet_hip_options == (solver_factory, bool(relax_milp), bool(retry_failed)):
+            return base
+        base = base.__bases__[0]  # re-install with the new options over the reference class
+    cls = make_batched_scenario_class(base, solver_factory, relax_milp, retry_failed)
     dervet_module.MicrogridScenario = cls
     return cls

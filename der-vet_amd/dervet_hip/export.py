@@ -25,6 +25,13 @@ column of CVXPY's own.  Solved as is, such a window is a generic CSR LP with ~3T
    the end whose original row held the pinned column of largest |value| is taken.  A window of any other shape
    keeps the presolved generic form (ELL / generic kernels).
 
+Mixed-integer windows (binary = 1, ``Model_Parameters_Template_DER.csv:17``: boolean ``on_c`` / ``on_d`` / ICE ``on``
+variables, ``ElectricVehicles.py:120-122``) are exported through CVXPY's ``get_problem_data(cvx.ECOS_BB)``, whose data
+dict carries ``bool_vars_idx`` / ``int_vars_idx`` (the column of every boolean / integer entry).  They are refused
+(``ExportError``: the reference solve, in place) unless the caller opts in with ``relax=True``; then integrality is
+dropped, every boolean column gets the box [0, 1] (intersected with any bound rows), integer columns keep their
+rows' bounds, and the window is the MILP's LP relaxation -- a lower bound on the reference's MILP objective.
+
 ``ExportedWindow.ecos_solution(result)`` maps a solver result back to the dict ECOS returns ({x, y, z, s, info}),
 which CVXPY's ECOS ``invert`` / ``Problem.unpack_results`` consume: x in the original column order (fixed columns
 at their values); ECOS duals from the solver's (c - K'y - lambda = 0 with K = [A; -G]): y_ECOS = -y_E, z = y_I for
@@ -91,6 +98,11 @@ class ExportedWindow:
     def n(self):
         return len(self.c)
 
+    @property
+    def relaxed(self):
+        """True for the LP relaxation of a mixed-integer window (``ecos_to_window(..., relax=True)``)."""
+        return bool(self.meta.get("relaxed_bool", 0) or self.meta.get("relaxed_int", 0))
+
     def x_full(self, x):
         """LP solution -> ECOS column order (substituted columns at their values)."""
         out = np.where(np.isnan(self.fixed_val), 0.0, self.fixed_val)
@@ -99,7 +111,8 @@ class ExportedWindow:
         return out
 
     def duals(self, y):
-        """LP duals (dvh convention) -> ECOS (y, z)."""
+        """LP duals (dvh convention) -> ECOS (y, z).  A relaxed boolean column's [0, 1] box has no ECOS row: what
+        its multiplier carries is dropped (CVXPY reports no duals for a mixed-integer problem anyway)."""
         ya = np.zeros(self.A.shape[0])
         z = np.zeros(self.G.shape[0])
         y = np.asarray(y)
@@ -147,11 +160,14 @@ class _Presolved:
     pass
 
 
-def presolve(c, offset, A, b, G, h, tol=1e-9):
-    """Step 1 of the module docstring.  Returns a _Presolved with the reduced LP pieces and the maps."""
+def presolve(c, offset, A, b, G, h, tol=1e-9, lo0=None, hi0=None):
+    """Step 1 of the module docstring.  Returns a _Presolved with the reduced LP pieces and the maps.  ``lo0`` /
+    ``hi0``: column bounds known before the rows are read (the [0, 1] box of a relaxed boolean column); a bound row
+    replaces them only where it is tighter."""
     n = len(c)
     P = _Presolved()
-    lo, hi = np.full(n, -np.inf), np.full(n, np.inf)
+    lo = np.full(n, -np.inf) if lo0 is None else np.array(lo0, np.float64)
+    hi = np.full(n, np.inf) if hi0 is None else np.array(hi0, np.float64)
     lb_row, ub_row, pin_row = np.full(n, -1), np.full(n, -1), np.full(n, -1)
     fixed = np.full(n, np.nan)
     keep_a, keep_g = np.ones(A.shape[0], bool), np.ones(G.shape[0], bool)
@@ -238,8 +254,17 @@ def presolve(c, offset, A, b, G, h, tol=1e-9):
     return P
 
 
-def ecos_to_window(data, tol=1e-9, band=True):
-    """CVXPY ECOS data dict {c, offset, A, b, G, h, dims} of one window -> ExportedWindow."""
+def integer_columns(data):
+    """(boolean columns, integer columns) of an ECOS_BB data dict (empty for an ECOS one)."""
+    def idx(key):
+        v = data.get(key)
+        return np.zeros(0, np.int64) if v is None else np.unique(np.asarray(v, np.int64).ravel())
+    return idx("bool_vars_idx"), idx("int_vars_idx")
+
+
+def ecos_to_window(data, tol=1e-9, band=True, relax=False):
+    """CVXPY ECOS / ECOS_BB data dict {c, offset, A, b, G, h, dims[, bool_vars_idx, int_vars_idx]} of one window ->
+    ExportedWindow.  A mixed-integer window raises ExportError unless ``relax`` (module docstring)."""
     c = np.asarray(data["c"], np.float64).ravel()
     n = len(c)
     A, G = _csr(data.get("A"), n), _csr(data.get("G"), n)
@@ -248,8 +273,19 @@ def ecos_to_window(data, tol=1e-9, band=True):
     _dims_nonneg(data.get("dims"), G.shape[0])
     offset = float(np.asarray(data.get("offset", 0.0), np.float64).ravel()[0]) if data.get("offset") is not None \
         else 0.0
-    P = presolve(c, offset, A, b, G, h, tol)
-    base = dict(c=c, offset=offset, A=A, b=b, G=G, h=h, pin_row=P.pin_row, lb_row=P.lb_row, ub_row=P.ub_row)
+    bools, ints = integer_columns(data)
+    lo0 = hi0 = None
+    if len(bools) or len(ints):
+        if not relax:
+            raise ExportError(f"mixed-integer window ({len(bools)} boolean, {len(ints)} integer columns): "
+                              "the reference MILP solve (opt in to its LP relaxation with relax=True)")
+        if (len(bools) and (bools.min() < 0 or bools.max() >= n)) or (len(ints) and (ints.min() < 0 or ints.max() >= n)):
+            raise ExportError("integer column index outside the problem")
+        lo0, hi0 = np.full(n, -np.inf), np.full(n, np.inf)
+        lo0[bools], hi0[bools] = 0.0, 1.0
+    P = presolve(c, offset, A, b, G, h, tol, lo0, hi0)
+    base = dict(c=c, offset=offset, A=A, b=b, G=G, h=h, pin_row=P.pin_row, lb_row=P.lb_row, ub_row=P.ub_row,
+                meta={"relaxed_bool": int(len(bools)), "relaxed_int": int(len(ints))})
     if band:
         w = _band(P, base)
         if w is not None:
@@ -411,4 +447,4 @@ def _band(P, base):
         pin_row[restore] = -1          # its pin row is the LP's init row now
     lp = WindowLP.from_csr(Kb, np.asarray(qb, np.float64), cb, lb, ub, T + 1, c0, structure=1)
     return ExportedWindow(lp=lp, col_src=src, row_kind=kind, row_src=rsrc, fixed_val=fixed, banded=True,
-                          meta={"T": T, "J": J, "restored": restore}, **dict(base, pin_row=pin_row))
+                          **dict(base, pin_row=pin_row, meta=dict(base["meta"], T=T, J=J, restored=restore)))

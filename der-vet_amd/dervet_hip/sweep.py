@@ -101,6 +101,8 @@ def seed_partners(fr, fs, q, first=None, power=1.0):
             f0 = np.asarray(first[a:a + 2048], np.int64)
             has = (part == f0[:, None]).any(1)
             part[~has, -1] = f0[~has]  # (a tie at the boundary: the known nearest replaces the last one)
+            rs = np.nonzero(~has)[0]    # ... with its exact distance (a 0 there was an infinite weight)
+            d[rs, f0[rs]] = ((fa[rs] - fs[f0[rs]]) ** 2).sum(1)
             part = np.take_along_axis(part, np.argsort(part != f0[:, None], axis=1, kind="stable"), 1)
         dd = np.sqrt(np.take_along_axis(d, part, 1))
         inv = np.where(dd > 0, 1.0 / np.where(dd > 0, dd, 1.0) ** power, np.inf)

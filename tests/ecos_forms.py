@@ -153,3 +153,51 @@ class FakeProblem:
         r = invert(solution, self.data["offset"])
         self.status, self.value, self.x = r["status"], r["value"], r["x"]
         self.duals = (r["y"], r["z"])
+
+
+def ecos_bb_market_form(win, seed=0):
+    """ECOS_BB data dict of a binary = 1 market-day window (oracle.window_lp market window) as CVXPY 1.0.31 would
+    emit it for the reference's MILP: the build() LP without the relaxation row plus storagevet's boolean on_c / on_d
+    (ElectricVehicles.py:120-122 pattern) with ch_t <= P_ch on_c_t, dis_t <= P_dis on_d_t, on_c_t + on_d_t <= 1,
+    columns shuffled (CVXPY orders by variable id), every bound a one-entry G row, the boolean columns listed in
+    ``bool_vars_idx`` (ECOS_BB.apply) and NOT boxed by any row (integrality is what bounds them).  Returns
+    (data, col) with col[o] = ECOS column of build() column o; the on_c / on_d columns are col[n:n + 2T]."""
+    from oracle import window_lp
+    rng = np.random.default_rng(seed)
+    lp = window_lp.build(dict(win, binary_relax=False))
+    K, q, m_eq, off = lp["K"].tocsr(), lp["q"], lp["m_eq"], lp["layout"]
+    n, T = K.shape[1], int(win["T"])
+    N = n + 2 * T
+    col = rng.permutation(N)
+    Ke = K[:m_eq].tocoo()
+    A = sp.csr_matrix((Ke.data, (Ke.row, col[Ke.col])), shape=(m_eq, N))
+    rows, cols, vals, h = [], [], [], []
+
+    def grow(entries, rhs):
+        r = len(h)
+        for cc, vv in entries:
+            rows.append(r)
+            cols.append(cc)
+            vals.append(vv)
+        h.append(rhs)
+
+    for o in range(n):
+        if np.isfinite(lp["u"][o]):
+            grow([(col[o], 1.0)], lp["u"][o])
+        if np.isfinite(lp["l"][o]):
+            grow([(col[o], -1.0)], -lp["l"][o])
+    for i in range(m_eq, K.shape[0]):
+        p0, p1 = K.indptr[i], K.indptr[i + 1]
+        grow([(col[K.indices[p]], -K.data[p]) for p in range(p0, p1)], -q[i])
+    b = win["bat"]
+    for t in range(T):
+        grow([(col[off["ch"] + t], 1.0), (col[n + t], -float(b["Pch"]))], 0.0)
+        grow([(col[off["dis"] + t], 1.0), (col[n + T + t], -float(b["Pdis"]))], 0.0)
+        grow([(col[n + t], 1.0), (col[n + T + t], 1.0)], 1.0)
+    G = sp.csr_matrix((vals, (rows, cols)), shape=(len(h), N))
+    c = np.zeros(N)
+    c[col[:n]] = lp["c"]
+    data = {"c": c, "offset": float(lp["c0"]), "A": A.tocsc(), "b": np.asarray(q[:m_eq], np.float64),
+            "G": G.tocsc(), "h": np.asarray(h), "dims": {"l": len(h), "q": [], "e": 0},
+            "bool_vars_idx": [int(j) for j in col[n:]], "int_vars_idx": []}
+    return data, col

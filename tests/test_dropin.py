@@ -17,7 +17,7 @@ import scipy.sparse as sp
 import ecos_forms
 from dervet_hip import WindowResult, dropin, export
 from dervet_hip.lp import builder, scenarios
-from oracle import window_lp
+from oracle import cases, window_lp
 
 
 class FakeDER:
@@ -171,13 +171,55 @@ def test_statuses_reach_save_as_the_reference_solve_leaves_them():
             out[3].status = 4   # NUMERICAL
             return out
 
-    dropin.batched_optimize_problem_loop(sc, solver=Mixed(), exporter=FakeExporter([]))
+    dropin.batched_optimize_problem_loop(sc, solver=Mixed(), exporter=FakeExporter([]), retry_failed=False)
     st = {w: (prob.status, err) for w, prob, err, _ in sc.saved}
     assert st[0] == ("optimal", None)
     assert st[1] == ("optimal_inaccurate", None)
     assert st[2] == ("infeasible", None)
     assert st[3][0] is None and "solver error" in st[3][1]
     assert [w for w, *_ in sc.saved] == [0, 1, 2, 3]
+    assert sc.dervet_hip_report.as_dict()["gpu"] == 4 and sc.reference_solves == []
+
+
+def test_failed_windows_are_re_solved_by_the_reference_in_place():
+    """SURVEY.md section 5 failure row: a window without a certified GPU optimum (iteration
+    limit, infeasible verdict, numerical failure) is re-solved by the reference solve_optimization in its place in
+    the order, and saved with what that solve returns (MicrogridScenario.py:319-320)."""
+    sc = FakeScenario(n_windows=5)
+
+    class Mixed(CpuStandInSolver):
+        def solve(self, lps):
+            out = super().solve(lps)
+            out[1].status = 3   # ITER_LIMIT
+            out[2].status = 1   # PRIMAL_INFEASIBLE
+            out[4].status = 4   # NUMERICAL
+            return out
+
+    dropin.batched_optimize_problem_loop(sc, solver=Mixed(), exporter=FakeExporter([]))
+    assert [w for w, *_ in sc.saved] == [0, 1, 2, 3, 4]
+    assert [id(lp) for lp in sc.reference_solves] == [id(sc.lps[w]) for w in (1, 2, 4)]
+    for w, prob, err, vd in sc.saved:
+        assert prob.status == "optimal" and err is None and vd["window"] == w
+        assert prob.value == pytest.approx(_highs(sc.lps[w]).obj, rel=1e-9)
+    rep = sc.dervet_hip_report.as_dict()
+    assert rep["gpu"] == 2 and rep["retried"] == 3 and rep["reference"] == 0
+    assert rep["retried_status"] == {"optimal_inaccurate": 1, "infeasible": 1, "solver_error": 1}
+
+
+def test_forced_iteration_limit_is_re_solved_by_the_reference():
+    """A real solver run out of iterations (the C++ restatement of the GPU algorithm behind the same C ABI, so
+    this runs without a GPU; max_iters far below what the windows need) -> every window ITER_LIMIT -> every window
+    re-solved by the reference."""
+    from oracle import cpu_pdhg
+    sc = FakeScenario(n_windows=3)
+    solver = cpu_pdhg.CpuPdhgSolver(threads=2, max_iters=64)
+    try:
+        dropin.batched_optimize_problem_loop(sc, solver=solver, exporter=FakeExporter([]))
+    finally:
+        solver.close()
+    assert len(sc.reference_solves) == 3
+    assert sc.dervet_hip_report.as_dict()["retried_status"] == {"optimal_inaccurate": 3}
+    assert all(prob.status == "optimal" for _, prob, _, _ in sc.saved)
 
 
 def test_cases_loop_batches_independent_cases_and_steps_coupled_ones_in_lockstep():
@@ -215,6 +257,73 @@ def test_install_patches_the_hard_coded_scenario_class():
     cls = dropin.install(mod)
     assert mod.MicrogridScenario is cls and issubclass(cls, FakeScenario)
     assert dropin.install(mod) is cls
+
+
+class FakeMarketScenario(FakeScenario):
+    """Usecase 3 golden market days (binary = 1): the reference solve is the MILP (HiGHS MILP on the restatement,
+    pinned to the golden objectives by tests/test_market_oracle.py)."""
+
+    def __init__(self, days, name="es"):
+        super().__init__(n_windows=len(days))
+        wins, _ = cases.market_windows(name, relax=False)
+        self.wins = [wins[d] for d in days]
+
+    def set_up_optimization(self, opt_period, annuity_scalar=1, ignore_der_costs=False):
+        self.log.append(("setup", int(opt_period)))
+        for der in self.ders:
+            der.variables_dict = {"window": int(opt_period)}
+        return {"win": self.wins[opt_period]}, ["c"], opt_period
+
+    def solve_optimization(self, functions, constraints):
+        self.reference_solves.append(functions["win"])
+        h = window_lp.solve_highs_milp(functions["win"])
+        return types.SimpleNamespace(status="optimal", value=h["obj"], x=h["x"]), functions, None
+
+
+class FakeMilpExporter:
+    """What CvxpyExporter does with a boolean window: None (reference path) unless relax_milp, else the ECOS_BB
+    data exported with relax=True."""
+
+    def __init__(self, relax_milp):
+        self.relax_milp = relax_milp
+
+    def export(self, functions, constraints):
+        if not self.relax_milp:
+            return None
+        data, col = ecos_forms.ecos_bb_market_form(functions["win"], seed=3)
+        return dropin.CvxpyWindow(export.ecos_to_window(data, relax=True), ecos_forms.FakeProblem(data, col))
+
+
+@pytest.mark.parametrize("relax", [False, True])
+def test_milp_windows_relaxed_only_on_opt_in(relax):
+    """north_star: MILP windows stay on the reference path, and the GPU solves their LP relaxation only when the
+    user opts in.  Off: every day goes to the reference MILP solve (golden objective).  On: every day is solved as
+    its LP relaxation by the batched solver, and each relaxed optimum is <= the golden MILP objective."""
+    days = [5, 120, 250]
+    sc = FakeMarketScenario(days)
+    solver = CpuStandInSolver()
+    dropin.batched_optimize_problem_loop(sc, solver=solver, exporter=FakeMilpExporter(relax), relax_milp=relax)
+    rep = sc.dervet_hip_report.as_dict()
+    assert [w for w, *_ in sc.saved] == [0, 1, 2]
+    for (w, prob, err, _), win in zip(sc.saved, sc.wins):
+        gold = float(win["golden_objective"].sum())
+        assert err is None and prob.status == "optimal"
+        if relax:
+            assert prob.value <= gold + 1e-9 * max(1.0, abs(gold))
+        else:
+            assert prob.value == pytest.approx(gold, rel=1e-7, abs=1e-7)
+    if relax:
+        assert solver.calls == [3] and rep["relaxed"] == 3 and rep["gpu"] == 3 and not sc.reference_solves
+    else:
+        assert solver.calls == [] and rep["reference"] == 3 and len(sc.reference_solves) == 3
+
+
+def test_install_passes_the_opt_in_through():
+    mod = types.SimpleNamespace(MicrogridScenario=FakeScenario)
+    cls = dropin.install(mod, relax_milp=True)
+    assert cls.dervet_hip_options[1:] == (True, True)
+    cls2 = dropin.install(mod)      # re-installed with the default (no relaxation) over the reference class
+    assert cls2 is not cls and cls2.__bases__[0] is FakeScenario and cls2.dervet_hip_options[1:] == (False, True)
 
 
 def test_cvxpy_exporter_requires_cvxpy():

@@ -140,3 +140,56 @@ def test_presolve_detects_inconsistent_rows_and_cones():
             "h": np.array([1.0, 0.0, 0.0]), "dims": {"l": 1, "q": [2], "e": 0}}
     with pytest.raises(export.ExportError):
         export.ecos_to_window(data)
+
+
+# -- mixed-integer windows (binary = 1): refused by default, LP-relaxed on opt-in ----------------------------------
+_MARKET_DAYS = {"es": (0, 91, 200, 364), "es+pv": (17, 180), "es+pv+dg": (45, 300)}
+
+
+@pytest.mark.parametrize("name", sorted(_MARKET_DAYS))
+def test_milp_market_day_is_refused_without_opt_in_and_relaxed_with_it(name):
+    """Usecase 3 golden days (binary = 1, Model_Parameters_Template_DER.csv:17; goldens are the reference's MILP
+    solves): the ECOS_BB form is an ExportError without ``relax``; relaxed, the exported LP's optimum equals the
+    relaxed restatement's (window_lp.build(binary_relax=True), HiGHS) and is <= the golden MILP objective, and the
+    solution comes back through the ECOS inversion with the relaxed objective."""
+    wins, _ = cases.market_windows(name)
+    for d in _MARKET_DAYS[name]:
+        w = wins[d]
+        data, col = ecos_forms.ecos_bb_market_form(w, seed=d)
+        with pytest.raises(export.ExportError, match="mixed-integer"):
+            export.ecos_to_window(data)
+        ew = export.ecos_to_window(data, relax=True)
+        assert ew.relaxed and ew.meta["relaxed_bool"] == 2 * w["T"] and not ew.banded
+        r = _highs_result(ew.lp)
+        ref = window_lp.solve_highs(window_lp.build(dict(w, binary_relax=True)))
+        assert abs(r.obj - ref["obj"]) <= 1e-9 * max(1.0, abs(ref["obj"]))
+        gold = float(w["golden_objective"].sum())
+        assert r.obj <= gold + 1e-9 * max(1.0, abs(gold))
+        sol = ew.ecos_solution(r)
+        inv = ecos_forms.invert(sol, data["offset"])
+        assert inv["status"] == "optimal" and inv["value"] == pytest.approx(r.obj, rel=1e-9, abs=1e-9)
+        x = sol["x"]
+        bools = np.asarray(data["bool_vars_idx"])
+        assert x[bools].min() >= -1e-9 and x[bools].max() <= 1 + 1e-9      # the relaxation's [0, 1] box
+        kkt = ecos_kkt(data, sol)
+        assert kkt["pfeas"] <= 1e-8
+
+
+def test_relaxed_bool_box_meets_bound_rows():
+    """A boolean column that also has bound rows keeps the tighter of the row and the [0, 1] box; an integer column
+    only loses integrality."""
+    c = np.array([-1.0, -1.0, 1.0])
+    G = sp.csr_matrix(np.array([[1.0, 0, 0], [0, 1.0, 0], [0, 0, -1.0], [1.0, 1.0, 1.0]]))
+    h = np.array([0.5, 7.0, -0.25, 10.0])   # x0 <= 0.5 (tighter than 1), x1 <= 7 (looser), x2 >= 0.25
+    data = {"c": c, "offset": 0.0, "A": None, "b": None, "G": G, "h": h, "dims": {"l": 4},
+            "bool_vars_idx": [0, 1], "int_vars_idx": [2]}
+    ew = export.ecos_to_window(data, relax=True)
+    assert ew.meta["relaxed_bool"] == 2 and ew.meta["relaxed_int"] == 1
+    lo = np.full(3, np.nan)
+    hi = np.full(3, np.nan)
+    lo[ew.col_src], hi[ew.col_src] = ew.lp.l, ew.lp.u
+    assert list(lo) == [0.0, 0.0, 0.25] and list(hi) == [0.5, 1.0, np.inf]
+    r = _highs_result(ew.lp)
+    assert r.obj == pytest.approx(-1.5 + 0.25)
+    with pytest.raises(export.ExportError):
+        export.ecos_to_window(dict(data, bool_vars_idx=[5]), relax=True)

@@ -132,6 +132,27 @@ def test_unbounded_column_goes_to_the_plain_form(gpu_solver):
     assert abs(res[2].x[2 * T2 + 5] - l2[2 * T2 + 5]) <= 1e-9 * abs(l2[2 * T2 + 5]), res[2].x[2 * T2 + 5]
 
 
+def test_unbounded_column_with_out_of_range_factors_reaches_the_double_path(gpu_solver):
+    """a window with no box (unbounded ch column: the box form returns it, status -3) whose
+    factors also leave float's range (a DCM row scaled by 1e-70) is refused by the plain form's factor check (-2)
+    AFTER the first -2 list was formed; the cascade lists the -2s again once the plain form has run, so the window
+    still reaches the ELL / generic path and is solved to HiGHS's optimum, not returned with its internal status."""
+    lps = [lp for g in scenarios.config4([2]) for lp in builder.group_window_lps(g)][:3]
+    lp = lps[1]
+    i = lp.m_eq
+    data, q, u = lp.data.copy(), lp.q.copy(), lp.u.copy()
+    data[lp.indptr[i]:lp.indptr[i + 1]] *= 1e-70
+    q[i] *= 1e-70
+    u[3] = np.inf
+    lps[1] = dataclasses.replace(lp, data=data, q=q, u=u)
+    res = gpu_solver.solve(lps)
+    ks = gpu_solver.kernel_stats()
+    assert ks["band_windows"] == 2 and ks["ell_windows"] + ks["generic_windows"] == 1, ks
+    o, h = _highs(lps[1])
+    assert h["status"] == 0 and res[1].status == 0, res[1].status_name
+    assert abs(res[1].obj - h["obj"]) <= 1e-5 * abs(h["obj"]), (res[1].obj, h["obj"])
+
+
 @pytest.mark.parametrize("box", ["1", "2"])
 def test_ice_window_without_a_box_goes_to_the_plain_ice_form(gpu_solver, monkeypatch, box):
     """The ICE form's box (opt-in, DVH_BAND_BOX=2) covers elec / on too: an ICE window whose elec_t has no upper bound

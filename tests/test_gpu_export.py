@@ -78,3 +78,36 @@ def test_dropin_loop_with_exported_windows_on_the_gpu():
     assert [w for w, *_ in saved] == list(range(len(ws)))
     for (w, status, value, err), (_, _, _, gold) in zip(saved, ws):
         assert status == "optimal" and err is None and abs(value - gold) <= 1e-5 * abs(gold)
+
+
+@pytest.mark.parametrize("name", ["es", "es+pv", "es+pv+dg"])
+def test_relaxed_milp_market_days_through_the_exporter(name):
+    """The opt-in LP relaxation of binary = 1 windows end to end: Usecase 3 golden days in the
+    ECOS_BB form CVXPY hands the reference's MILP (boolean on_c / on_d, ``bool_vars_idx``) -> export with relax=True
+    -> the HIP solver -> ECOS inversion.  Bars: within 1e-5 of HiGHS on the relaxed restatement, primal residual
+    <= 1e-6 on the ECOS form, and <= the golden MILP objective of the day."""
+    wins, _ = cases.market_windows(name, relax=False)
+    days = list(range(3, 365, 9))
+    exp = []
+    for d in days:
+        data, col = ecos_forms.ecos_bb_market_form(wins[d], seed=d)
+        exp.append((data, export.ecos_to_window(data, relax=True)))
+    with BatchSolver(0) as s:
+        res = s.solve([ew.lp for _, ew in exp])
+    worst = 0.0
+    for d, (data, ew), r in zip(days, exp, res):
+        assert r.status == 0, (name, d, r.status_name, r.iters)
+        ref = window_lp.solve_highs(window_lp.build(dict(wins[d], binary_relax=True)))
+        sol = ew.ecos_solution(r)
+        inv = ecos_forms.invert(sol, data["offset"])
+        assert inv["status"] == "optimal"
+        rel = abs(inv["value"] - ref["obj"]) / max(abs(ref["obj"]), 1.0)
+        worst = max(worst, rel)
+        assert rel <= 1e-5, (name, d, inv["value"], ref["obj"])
+        gold = float(wins[d]["golden_objective"].sum())
+        assert inv["value"] <= gold + 1e-5 * max(abs(gold), 1.0), (name, d, inv["value"], gold)
+        A, G, b, h, x = data["A"], data["G"], data["b"], data["h"], sol["x"]
+        pres = np.sqrt(np.sum((A @ x - b) ** 2) + np.sum(np.maximum(G @ x - h, 0) ** 2)) / (
+            1 + np.linalg.norm(np.concatenate([b, h])))
+        assert pres <= 1e-6, (name, d, pres)
+    print(f"{name}: {len(days)} relaxed days, worst objective rel err {worst:.2e}")

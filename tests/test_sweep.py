@@ -226,6 +226,24 @@ def test_seed_partners_nearest_first_and_inverse_distance_weights():
     assert w[500, 0] == 1.0 and (w[500, 1:] == 0.0).all()  # a seed at distance 0 takes the whole weight
 
 
+def test_seed_partners_substituted_nearest_gets_its_own_distance():
+    """when the known nearest seed is not among the candidates (a tie at the boundary, here forced by
+    passing a `first` that is not the nearest), it replaces the last partner WITH its exact distance -- not 0, which
+    made its inverse-distance weight infinite and collapsed the blend onto it."""
+    from dervet_hip.sweep import seed_partners
+    rng = np.random.default_rng(3)
+    fs = rng.normal(0, 1, (20, 2))
+    fr = rng.normal(0, 1, (50, 2))
+    d = np.sqrt(((fr[:, None, :] - fs[None, :, :]) ** 2).sum(-1))
+    first = np.argsort(d, axis=1)[:, -1]          # the farthest seed, certainly not a candidate
+    idx, w = seed_partners(fr, fs, 4, first=first)
+    assert np.array_equal(idx[:, 0], first)
+    for i in range(len(fr)):
+        inv = 1.0 / d[i, idx[i]]
+        np.testing.assert_allclose(w[i], inv / inv.sum(), rtol=1e-13)
+        assert w[i, 0] < 0.5
+
+
 def test_blended_transfer_on_host_is_the_weighted_sum_of_partner_transfers():
     """SeededSweep(blend=3): every rest window starts from the weighted sum of its three nearest seeds' transferred
     solutions (the single-partner transfer of each, weights summing to 1); transfer_rows names them for the device."""
