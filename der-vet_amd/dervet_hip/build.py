@@ -63,5 +63,40 @@ def build(force=False, verbose=False):
     return LIB
 
 
+def build_variant(out, defines, recompile=("dvh_band.hip", "dvh_band_persist.hip"), verbose=False):
+    """A/B helper: the library with ``defines`` (e.g. ["-DDVH_BAND_PROBE=1"]) applied to the sources in
+    ``recompile`` (their objects go to build_obj/<name>/), every other object taken from the default build."""
+    build()
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result",
+             "-Wno-unused-value", *defines]
+    name = os.path.splitext(os.path.basename(out))[0]
+    objdir = os.path.join(HERE, "build_obj", name)
+    os.makedirs(objdir, exist_ok=True)
+    objs = {f: os.path.join(HERE, "build_obj", f + ".o") for f in SOURCES}
+
+    def compile_one(f):
+        objs[f] = os.path.join(objdir, f + ".o")
+        cmd = [hipcc, *flags, *EXTRA_FLAGS.get(f, []), "-c", os.path.join(CSRC, f), "-o", objs[f]]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        return f, subprocess.run(cmd, capture_output=True, text=True)
+
+    with ThreadPoolExecutor(max_workers=max(1, len(recompile))) as ex:
+        results = list(ex.map(compile_one, recompile))
+    failed = [(f, r) for f, r in results if r.returncode != 0]
+    for f, r in failed:
+        sys.stderr.write(f"--- {f}\n" + r.stdout + r.stderr)
+    if failed:
+        raise RuntimeError("hipcc failed building variant " + name)
+    os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
+    cmd = [hipcc, "--offload-arch=gfx950", "-fPIC", "-shared", "-o", out] + [objs[f] for f in SOURCES]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError("hipcc failed linking variant " + name)
+    return out
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
