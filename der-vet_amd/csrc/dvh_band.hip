@@ -37,7 +37,7 @@ constexpr int kJMax = 4;         // tau (demand-period) columns per window
 constexpr int kNeedsEll = -2;
 
 // LDS layout (B lanes, S steps per lane, SB = S B steps), doubles then ints:
-//   XE[B+1] YS[B+1] XT[kJMax] red[kNRed(NW+1)+4] TP[kJMax][B] TW[kJMax][NW] XP[NC S][B] YP[NR S][B] (ICE: RO[6 S][B])
+//   XE[B+1] YS[B+1] XT[kJMax] red[kNRed(NW+1)+4] TP[kJMax][B] XP[NC S][B] YP[NR S][B] (ICE: RO[6 S][B])
 //   | ints: dcm[SB] ice_a[SB] ice_b[SB] ice_n[SB] flag[4]
 // Register-relief flags LF (forms with several steps per lane): kLfAnchors -- the Halpern anchors XA[NC S][B] /
 // YA[NR S][B] live in LDS (one FMA operand per iteration, written at restarts; the ints, read only while the lane
@@ -46,33 +46,25 @@ constexpr int kNeedsEll = -2;
 // instead of XP / YP (read back by the same lane at the check).  Layout after TP: [XP YP] (no kLfImages) [XA YA]
 // (kLfAnchors) [RO] (ICE) [CQ] (kLfCosts).
 constexpr int kLfAnchors = 1, kLfCosts = 2, kLfImages = 4;
-// kTauDual (default): a window with one tau column (J = 1: every monthly bench window) updates that column in the
-// DUAL half-step, in every wave, as uniform values.  Each lane keeps its partial K'y of the column (its steps' DCM
-// duals, summed in step order) in a register across the barrier; in the next primal half-step every wave reduces it
-// (one DPP tree, interleaved with its column work) into TW[wid]; after the first barrier every wave adds the NW wave
-// sums in wave order and updates the column -- identical operands in the same order in every wave, so every wave holds
-// the same bits -- and its DCM rows take the column's x-bar from that register instead of LDS.  Before, wave 0 alone
-// reduced the 256 partials and updated the column at the start of the primal half-step, a serial chain (LDS reads,
-// six DPP levels, the update, the XT store) the other waves waited for at the first barrier: per wave
-// (scripts/probe_band_latency.py, profiles/r05b_band_latency.log) wave 0's primal half-step took 996-1024 cycles
-// against 610-640 for the others, who waited 390-440 cycles there.  Wave 0's copy is the one whose movement, KKT terms
-// and output count.  (Round 4 tried per-wave sums with the update still in wave 0's primal half-step: no change,
-// 227.5k vs 227.7k windows/s, profiles/r04g_ab_band_tau_wavesums.log; this round, a per-wave replica updated in the
-// primal half-step: every wave's primal half-step took the chain, 1.099 vs 1.048 us per window-iteration per slot,
-// profiles/r05c_*.)
-#ifndef DVH_BAND_TAUD
-#define DVH_BAND_TAUD 0
+#ifndef DVH_BAND_TAU_WAVESUMS
+#define DVH_BAND_TAU_WAVESUMS 0
 #endif
-// DVH_ABL (dev ablations, wrong results, timing only: scripts/probe_band_queue.py at a fixed iteration count):
-// bit 0 drops the iteration's first barrier, bit 1 the second, bit 2 wave 0's tau reduction and update
-#ifndef DVH_ABL
-#define DVH_ABL 0
-#endif
-constexpr bool kTauDual = DVH_BAND_TAUD != 0;
+// tau_parts (below): per-wave sums of one tau column.  Off: the same-box bench A/B found no difference (227.5k vs
+// 227.7k windows/s, profiles/r04g_ab_band_tau_wavesums.log); the round-3 arithmetic (certified) is kept.
+constexpr bool kTauWaveSums = DVH_BAND_TAU_WAVESUMS != 0;
+// Where the band iteration's time goes (round 5): wave 0 reduces and updates the single tau column of a monthly window
+// (J = 1) at the start of the primal half-step, and the other waves wait for it at the first barrier -- per wave
+// (scripts/probe_band_latency.py, profiles/r05b_band_latency.log) wave 0's primal half-step takes 996-1024 shader cycles
+// against 610-640 for the others, who wait 390-440 cycles there.  Measured and not kept (profiles/r05c_*, r05g_*): a
+// replica of the column in every wave updated in the primal half-step (1.099 vs 1.048 us per window-iteration per
+// slot) and the column updated in the dual half-step by every wave (1.146): every wave then carries the chain; the
+// costs read from LDS ahead of the second barrier (1.136: the compiler holds them through the iteration).  Ablations at
+// a fixed iteration count (wrong results; profiles/r05h_band_ablations.log, r05k_*) bound what is left: without the tau
+// chain -7 %, without both barriers -9 %, without the cost / right-hand-side LDS reads -7.5 %, all together -24 %.
 __host__ __device__ inline size_t band_lds_doubles(int B, int S, bool ice, int LF) {
   const int NW = B / kWave, NC = ice ? 5 : 3, NR = ice ? 4 : 2;
   const size_t SB = (size_t)S * B;
-  return 2 * (size_t)(B + 1) + kJMax + (size_t)kNRed * (NW + 1) + 4 + (size_t)kJMax * B + (size_t)kJMax * NW +
+  return 2 * (size_t)(B + 1) + kJMax + (size_t)kNRed * (NW + 1) + 4 + (size_t)kJMax * B +
          ((LF & kLfImages) ? 0 : (NC + NR) * SB) + ((LF & kLfAnchors) ? (NC + NR) * SB : 0) +
          ((LF & kLfCosts) ? 5 * SB : 0) + (ice ? 6 * SB : 0);
 }
@@ -198,9 +190,8 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
   double* XT = YS + (B + 1);  // x-bar (x+) of the tau columns
   double* red = XT + kJMax;
   double* TP = red + kNRed * (NW + 1) + 4;  // [kJMax][B] per-lane partial K'y of the tau columns
-  double* TW = TP + kJMax * B;              // [NW] per-wave sums of K'y of a single tau column (J = 1, kTauDual)
   constexpr bool LA = LF & kLfAnchors, LC = LF & kLfCosts, LI = LF & kLfImages;
-  double* XP = TW + kJMax * NW;                 // [NC S][B] T(z) of the lane's columns (check iterations)
+  double* XP = TP + kJMax * B;                  // [NC S][B] T(z) of the lane's columns (check iterations)
   double* YP = XP + (LI ? 0 : NC * SB);         // [NR S][B] T(z) of the lane's rows
   double* XA = YP + (LI ? 0 : NR * SB);         // [NC S][B] Halpern anchors of the columns (kLfAnchors)
   double* YA = XA + (LA ? NC * SB : 0);         // [NR S][B] and of the rows
@@ -437,9 +428,6 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
   constexpr int kInitLane = kWave - 1;
   static_assert(kJMax < kInitLane, "tau lanes and the init-row lane are distinct");
   const bool tlane = wid == 0 && lane < J, ilane = wid == 0 && lane == kInitLane;
-  const bool tj1 = kTauDual && J == 1;  // (uniform) the single tau column, updated in the dual half-step (kTauDual)
-  // its state, uniform (the same bits in every lane of every wave): x, Halpern anchor, c, lo, hi, last image
-  double tx = 0.0, txa = 0.0, tcs = 0.0, tlo = 0.0, thi = 0.0, tp1 = 0.0;
   double sp[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
 
   // ---- scaling: setup_kernel's preconditioning (o.ruiz_iters Ruiz inf-norm passes, then one Pock-Chambolle
@@ -638,15 +626,6 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
     dcv[j] = fsp;
     w.fc[W.wn + j] = (float)fsp;
   }
-  if (tj1) {  // the same values as wave 0's lane 0 above, in every lane (XT[0] holds the column's factor since the last
-              // exchange of the scaling)
-    const int j = 3 * T;
-    const double fj = XT[0], cj = craw[j];
-    tlo = uniform(lraw[j] / fj);
-    thi = uniform(uraw[j] / fj);
-    tx = txa = tp1 = uniform(fmin(fmax(o.warm ? xo_g[j] / fj : 0.0, tlo), thi));
-    tcs = uniform(cj * fj);
-  }
   if (ilane) {
     const double q0 = qraw[0];
     sp[3] = q0 * fsp;
@@ -678,7 +657,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
   if (tid < kJMax) XT[tid] = 0.0;
   if (tid == 0) XE[B] = YS[B] = 0.0;
   XE[tid] = YS[tid] = 0.0;
-  for (int u = tid; u < kJMax * (B + NW); u += B) TP[u] = 0.0;  // (TP and TW)
+  for (int u = tid; u < kJMax * B; u += B) TP[u] = 0.0;
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     if constexpr (LI) {  // the outputs hold the last KKT check's T(z_k): the starting point until the first one
@@ -745,14 +724,20 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
       os[3] = fma(kb[s][1], v[4], fma(kb[s][0], v[3], -rhs(s, 3)));
     }
   };
-  // per-lane partial K'y of the tau columns from the DCM rows' values vd[s] (steps summed in order), for wave 0's
-  // reduction (tau_kt: the power iteration, KKT checks, J >= 2, and J = 1 without kTauDual)
+  // per-lane partial K'y of the tau columns from the DCM rows' values vd[s] (steps summed in order).  One column
+  // (J = 1, kTauWaveSums): every wave reduces its lanes' partials itself (one DPP tree, lane 0's sum) into TP[wid],
+  // so the tau update on wave 0 adds NW values instead of reducing B partials on the iteration's critical path.
   auto tau_parts = [&](const double (&vd)[S]) {
     if (J == 1) {
       double a = kd[0][2] * vd[0];
 #pragma unroll
       for (int s = 1; s < S; ++s) a = fma(kd[s][2], vd[s], a);
-      TP[tid] = a;
+      if constexpr (kTauWaveSums) {
+        a = wave_sum_dpp(a);
+        if (lane == 0) TP[wid] = a;
+      } else {
+        TP[tid] = a;
+      }
     } else {
       for (int j = 0; j < J; ++j) {
         double a = (jt[0] == j ? kd[0][2] : 0.0) * vd[0];
@@ -768,31 +753,17 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
     for (int s = 0; s < S; ++s) vd[s] = vr[s][1];
     tau_parts(vd);
   };
-  // kTauDual (J = 1): the lane's partial K'y of the column, steps in order (kept in a register across the barrier)
-  double tpart = 0.0;
-  auto tau_part_of = [&](const double (&vr)[S][NR]) {
-    double a = kd[0][2] * vr[0][1];
-#pragma unroll
-    for (int s = 1; s < S; ++s) a = fma(kd[s][2], vr[s][1], a);
-    return a;
-  };
-  // what the iteration's primal half-step starts from: the lane's partial (kTauDual) or the per-lane partials in LDS
-  auto tau_state_of = [&](const double (&vr)[S][NR]) {
-    if (tj1)
-      tpart = tau_part_of(vr);
-    else if (J > 0)
-      tau_parts_of(vr);
-  };
-  // the wave sums of the single tau column, in wave order (every lane reads the same slots: a broadcast)
+  // the wave sums of a single tau column, in wave order (every lane reads the same slots: a broadcast)
   auto tau_waves = [&]() {
-    double a = TW[0];
+    double a = TP[0];
 #pragma unroll
-    for (int r = 1; r < NW; ++r) a += TW[r];
+    for (int r = 1; r < NW; ++r) a += TP[r];
     return a;
   };
   // wave 0: lane j < J gets the sum over all lanes of TP[j][.] (fixed order; uniform per column)
   auto tau_kt = [&]() {
     double res = 0.0;
+    if (kTauWaveSums && J == 1) return lane == 0 ? tau_waves() : 0.0;
     for (int j = 0; j < J; ++j) {
       double a = 0.0;
 #pragma unroll
@@ -864,7 +835,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
   if (o.warm) {  // y images of the starting point
     YS[tid + 1] = y[S - 1][0];
     if (ilane) YS[0] = sp[0];
-    tau_state_of(y);
+    if (J > 0) tau_parts_of(y);
     __syncthreads();
   }
   eta = uniform(eta);
@@ -1006,10 +977,9 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
   };
   double hw = hload(0);
 
-  // one tau column (J = 1): the fast form -- every wave with kTauDual (the column updated in the dual half-step), else
-  // wave 0 alone in the primal half-step (its reduction interleaved with its own column work: straight-line code, the
-  // partial loads issued first); J >= 2 takes the generic per-column loop on wave 0
-  const bool w0 = J == 1 && (kTauDual || wid == 0);
+  // wave 0 with one tau column: the tau reduction is interleaved with its own column work (straight-line code,
+  // the partial loads are issued first); J >= 2 takes the generic per-column loop
+  const bool w0 = wid == 0 && J == 1;
   double mv0, mv1, mv2, mv3;
   auto tau_update = [&](double kt, double ca, double cb, auto chk_tag) __attribute__((always_inline)) {
     constexpr bool CHECK = decltype(chk_tag)::value;
@@ -1080,10 +1050,8 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
     double kx[S][NR];  // own-lane part of K x-bar for the dual half-step
     {
       double ta0 = 0.0, ta1 = 0.0;
-      if constexpr (W0 && kTauDual) {  // the wave's sum of its lanes' partials, for the dual half-step's update
-        const double a = wave_sum_dpp(tpart);
-        if (lane == 0) TW[wid] = a;
-      } else if constexpr (W0 && (DVH_ABL & 4)) {
+      if constexpr (W0 && kTauWaveSums) {
+        ta0 = tau_waves();
       } else if constexpr (W0) {  // (0 + a == a: the first partials start the two chains)
         ta0 = TP[lane];
         if (NW > 1) ta1 = TP[kWave + lane];
@@ -1133,9 +1101,8 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
         kown_q(s, xb[s], kx[s]);
         if (s < S - 1) kfin_next(s, kx[s], xb[s < S - 1 ? s + 1 : s][2]);  // the next step is the lane's own
       }
-      if constexpr (W0 && kTauDual) {
-        // (the column is updated in the dual half-step)
-      } else if constexpr (W0 && (DVH_ABL & 4)) {
+      if constexpr (W0 && kTauWaveSums) {
+        tau_update(ta0, ca, cb, chk_tag);
       } else if constexpr (W0) {
         tau_update(uniform(wave_sum_dpp(ta0 + ta1)), ca, cb, chk_tag);
       } else {
@@ -1143,10 +1110,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
       }
     }
     pstamp(0);
-    if constexpr (DVH_ABL & 1)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    else
-      lds_barrier();
+    lds_barrier();
     pstamp(1);
     // ---------------- dual half-step
     {
@@ -1154,25 +1118,8 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
       // issued together, one wait instead of one per read
       const double xen = XE[tid + 1];
       double xtv[S];
-      if constexpr (W0 && kTauDual) {  // the column's update, every wave, uniform; every step's DCM row is in column 0
-        const double kt = tau_waves();
-        const double p1 = vmin(vmax(fma(-tau, tcs - kt, tx), tlo), thi);
-        const double xbt = fma(2.0, p1, -tx);
-        if (CHECK) {
-          if (tlane) {  // (the column's movement counted once, by wave 0's lane 0)
-            const double d = tx - p1, da = p1 - txa;
-            mv0 += d * d;
-            mv1 += da * da;
-          }
-          tp1 = uniform(p1);
-        }
-        tx = uniform(fma(ca, xbt, cb * txa));
 #pragma unroll
-        for (int s = 0; s < S; ++s) xtv[s] = xbt;
-      } else {
-#pragma unroll
-        for (int s = 0; s < S; ++s) xtv[s] = lds_ld(xta[s]);
-      }
+      for (int s = 0; s < S; ++s) xtv[s] = lds_ld(xta[s]);
       kfin_next(S - 1, kx[S - 1], xen);
       auto row_step = [&](int s, int r) __attribute__((always_inline)) {
         // row 0 (SOE) is an equality; DCM / ICE rows are >=: duals stay >= 0
@@ -1203,14 +1150,11 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
 #pragma unroll
         for (int r = 1; r < NR; ++r) row_step(s, r);
       }
-      if constexpr (W0 && kTauDual)
-        tpart = tau_part_of(y);
-      else if (J > 0)
-        tau_parts_of(y);
+      if (J > 0) tau_parts_of(y);
 #pragma unroll
       for (int s = 0; s < S; ++s) row_step(s, 0);
       YS[tid + 1] = y[S - 1][0];
-      if ((W0 && !kTauDual) || wid == 0) {  // init row (lane kInitLane): ene_0 = target
+      if (W0 || wid == 0) {  // init row (lane kInitLane): ene_0 = target
         if (ilane) {
           const double y0 = sp[0], ya0 = sp[1];
           const double q1 = fma(sigma, sp[3] - sp[4] * XE[0], y0);
@@ -1229,10 +1173,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
     ++it;
     ++kin;
     pstamp(2);
-    if constexpr (DVH_ABL & 2)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    else
-      lds_barrier();
+    lds_barrier();
     pstamp(3);
   };
 
@@ -1288,7 +1229,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
       XE[tid] = xp[0][2];
       YS[tid + 1] = yp[S - 1][0];
       if (ilane) YS[0] = sp[2];
-      if (tlane) XT[lane] = tj1 ? tp1 : sp[5];
+      if (tlane) XT[lane] = sp[5];
       if (J > 0) tau_parts_of(yp);
       lds_barrier();
       auto col_kkt = [&](int j, double kt, double cj, double loj, double hij, double xj) {
@@ -1330,12 +1271,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
       }
       if (wid == 0 && J > 0) {
         const double ktt = tau_kt();
-        if (tlane) {
-          if (tj1)
-            col_kkt(3 * T, ktt, tcs, tlo, thi, tp1);
-          else
-            col_kkt(3 * T + lane, ktt, sp[2], sp[3], sp[4], sp[5]);
-        }
+        if (tlane) col_kkt(3 * T + lane, ktt, sp[2], sp[3], sp[4], sp[5]);
       }
       const double xen = XE[tid + 1];
 #pragma unroll
@@ -1439,7 +1375,6 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
       }
       if (ilane) sp[0] = sp[1] = sp[2];
       if (tlane) sp[0] = sp[1] = sp[5];
-      if (tj1) tx = txa = tp1;
       kin = 0;
       kbase = 0;
       hw = hload(0);
@@ -1451,7 +1386,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
     if (restart || kkt) {  // the y images must hold z again (after a restart z = T(z_k))
       YS[tid + 1] = y[S - 1][0];
       if (ilane) YS[0] = sp[0];
-      tau_state_of(y);
+      if (J > 0) tau_parts_of(y);
     }
     lds_barrier();
   }
@@ -1477,14 +1412,14 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
       yo_g[rb[s]] = YP[(3 * S + s) * B + tid] * drv[rb[s]];
     }
   }
-  if (tlane) xo_g[3 * T + lane] = (tj1 ? tp1 : sp[5]) * dcv[3 * T + lane];
+  if (tlane) xo_g[3 * T + lane] = sp[5] * dcv[3 * T + lane];
   if (ilane) yo_g[0] = sp[2] * drv[0];
   if constexpr (DVH_BAND_PROBE) {
     pstamp(4);
     pacc[4] += (unsigned)(pt1 - pt2);
-    __syncthreads();
     unsigned hw = 0;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    __syncthreads();
     if (lane == 0) {
       for (int u = 0; u < 5; ++u) xo_g[6 * wid + u] = (double)pacc[u];
       xo_g[6 * wid + 5] = (double)hw;
@@ -1598,7 +1533,11 @@ hipError_t launch_band_one_q(const Batch& b, const Work& w, const Chunk& ch, con
       if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
       slots = std::max(1, nb) * std::max(1, cus);
     }
-    grid = std::min(count, slots);
+    // DVH_BAND_RESERVE = k: leave 2k workgroup slots to other kernels, e.g. an all-gather issued on another stream
+    // after this grid launched, which otherwise waits for the grid's tail (scripts/probe_overlap.py,
+    // profiles/r05i_overlap_reserve*.log: k = 32 lets a 2 GiB copy run beside the grid at +12.6 % band time)
+    static const int reserve = [] { const char* e = getenv("DVH_BAND_RESERVE"); return e ? std::max(0, atoi(e)) : 0; }();
+    grid = std::min(count, std::max(1, slots - 2 * reserve));
     if ((e = hipMemsetAsync(w.queue, 0, sizeof(int32_t), s)) != hipSuccess) return e;
   }
   const BandArgs args{b, w, ch, o, list, count, w.queue};
