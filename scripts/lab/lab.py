@@ -27,13 +27,14 @@ class Lab:
     def __init__(self):
         self.lib = _lib.load(LIB)
         self.lib.lab_set_traj.argtypes = [ctypes.c_void_p]
+        self.lib.lab_set_pw.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         self.opts = _lib.Options()
         self.lib.dvh_default_options(ctypes.byref(self.opts))
         h = ctypes.c_void_p()
         assert self.lib.dvh_create(1, ctypes.byref(self.opts), ctypes.byref(h)) == 0
         self.h = h
 
-    def solve(self, lps, starts=None, **opts):
+    def solve(self, lps, starts=None, pw_in=None, **opts):
         o = _lib.Options()
         ctypes.memmove(ctypes.byref(o), ctypes.byref(self.opts), ctypes.sizeof(o))
         for k, v in opts.items():
@@ -62,14 +63,19 @@ class Lab:
             res[k].y = y.ctypes.data_as(_lib.c_double_p)
         traj = np.full((n, 3), -1, np.int32)
         self.lib.lab_set_traj(traj.ctypes.data)
+        pw_out, pw0_out = np.zeros(n), np.zeros(n)
+        pin = None if pw_in is None else np.ascontiguousarray(pw_in, np.float64)
+        self.lib.lab_set_pw(None if pin is None else pin.ctypes.data, pw_out.ctypes.data, pw0_out.ctypes.data)
         t = time.perf_counter()
         assert self.lib.dvh_solve_batch(self.h, arr, n, res) == 0
         wall = time.perf_counter() - t
         self.lib.lab_set_traj(None)
+        self.lib.lab_set_pw(None, None, None)
         it = np.array([res[k].iters for k in range(n)])
         st = np.array([res[k].status for k in range(n)])
         obj = np.array([res[k].obj for k in range(n)])
-        return dict(iters=it, status=st, obj=obj, x=[o[0] for o in outs], y=[o[1] for o in outs], traj=traj, wall=wall)
+        return dict(iters=it, status=st, obj=obj, x=[o[0] for o in outs], y=[o[1] for o in outs], traj=traj, wall=wall,
+                    pw=pw_out, pw0=pw0_out)
 
 
 def transfer(lp_r, lp_s, xs, ys):
@@ -165,7 +171,15 @@ def main():
                                        sum(wq * aa[1] for wq, aa in zip(wgt[i], a))))
                     else:
                         starts.append(transfer(w[s], seed_lps[k], rs["x"][k], rs["y"][k]))
-            r = lab.solve(lps, starts, check_every=64, kkt_every=1, warm_start=1, **wo)
+            pw_in = None
+            pwt = int(env.get("LAB_PWT", 0))
+            if pwt and warm_mode != "nearest":  # the partners' final primal weights (mode 1) or final / data ratios (2)
+                src = rs["pw"] if pwt == 1 else rs["pw"] / rs["pw0"]
+                pw_in = []
+                for wi in range(len(wins)):
+                    for i in range(len(rest)):
+                        pw_in.append(float(np.exp(sum(wq * np.log(src[wi * ns + p]) for wq, p in zip(wgt[i], pick2[i])))))
+            r = lab.solve(lps, starts, pw_in=pw_in, check_every=64, kkt_every=1, warm_start=1, **wo)
             summary("warm " + tag, r)
 
 

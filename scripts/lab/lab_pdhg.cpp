@@ -30,6 +30,8 @@ static double envd(const char* k, double d) {
 thread_local int g_first[3];
 static int* g_traj = nullptr;  // [count][3]
 thread_local bool g_trace = false;
+thread_local int g_k = 0;                 // the window being solved (LAB_PWT hooks)
+static double *g_pw_in = nullptr, *g_pw_out = nullptr, *g_pw0_out = nullptr;
 
 struct dvh_handle {
   dvh_options opts;
@@ -173,6 +175,7 @@ void solve_one(const dvh_lp& lp, const dvh_options& o, const double* x0, const d
   const double eta = o.step_safety / (a > 0 && b > 0 ? std::sqrt(b / a) : 1.0);
   const double nc = norm2(ct), nq = norm2(qt);
   double w = (nc > 1e-10 && nq > 1e-10) ? nc / nq : 1.0;
+  const double w_data = w;
   double qn = 0, cn = 0;
   for (int r = 0; r < m; ++r) qn += lp.q[r] * lp.q[r];
   for (int c = 0; c < n; ++c) cn += lp.c[c] * lp.c[c];
@@ -189,6 +192,11 @@ void solve_one(const dvh_lp& lp, const dvh_options& o, const double* x0, const d
     for (double v : y) ny += v * v;
     if (nx > 1e-20 && ny > 1e-20) w = std::sqrt(std::sqrt(ny / nx) * w);
   }
+  if (g_pw_in && g_pw_in[g_k] > 0.0) {  // LAB_PWT study: 1 absolute weight, 2 ratio to this window's data weight
+    const int mode = (int)envd("LAB_PWT", 1.0);
+    w = mode == 2 ? w_data * g_pw_in[g_k] : g_pw_in[g_k];
+  }
+  if (g_pw0_out) g_pw0_out[g_k] = w_data;
   xa = x;
   ya = y;
   auto T = [&](const std::vector<double>& xi, const std::vector<double>& yi) {
@@ -353,6 +361,7 @@ void solve_one(const dvh_lp& lp, const dvh_options& o, const double* x0, const d
   out.dres = last.dres;
   out.gap = last.gap;
   out.iters = it;
+  if (g_pw_out) g_pw_out[g_k] = w;
 }
 
 }  // namespace
@@ -427,6 +436,7 @@ int dvh_solve_batch(dvh_handle* h, const dvh_lp* lps, int32_t count, dvh_result*
   for (int k = 0; k < count; ++k) {
     Out r;
     g_trace = getenv("LAB_TRACE") && atoi(getenv("LAB_TRACE")) == k;
+    g_k = k;
     solve_one(lps[k], o, o.warm_start ? out[k].x : nullptr, o.warm_start ? out[k].y : nullptr, r);
     if (out[k].x) std::memcpy(out[k].x, r.x.data(), sizeof(double) * r.x.size());
     if (out[k].y && !r.y.empty()) std::memcpy(out[k].y, r.y.data(), sizeof(double) * r.y.size());
@@ -490,6 +500,11 @@ const char* dvh_last_warning(const dvh_handle*) { return ""; }
 int dvh_set_kernel_path(dvh_handle*, int) { return DVH_OK; }
 int dvh_set_launch_order(dvh_handle*, const int32_t*, int32_t) { return DVH_OK; }
 void lab_set_traj(int* t) { g_traj = t; }
+void lab_set_pw(double* in, double* out, double* out0) {
+  g_pw_in = in;
+  g_pw_out = out;
+  g_pw0_out = out0;
+}
 int dvh_outage_coverage(dvh_handle*, const dvh_outage_case*, int32_t, int32_t*, double*) { return DVH_ERR_UNSUPPORTED; }
 int dvh_outage_min_soe(dvh_handle*, const dvh_outage_case*, int32_t, const int32_t*, double*) {
   return DVH_ERR_UNSUPPORTED;
