@@ -134,6 +134,15 @@ __device__ __noinline__ RowKkt row_kkt_fn(double kv, double qi, double yi, float
 // once the constant c lo is added.  A window with an unbounded ch / dis / ene (/ elec / on) column is returned with
 // status kNeedsPlain and re-run by the plain form (dvh_api.cpp device_cascade).
 constexpr int kNeedsPlain = -3;
+// kBoxRescale (box form): the checks and restarts stop re-reading the columns' box widths from the window's workspace
+// in HBM.  A restart rescales the per-column steps tau / w^2 by tau_new / tau_old (one uniform quotient, no per-column
+// division), and the check iteration's movement norms, in x units, weigh each column's d'^2 by w^2 = tau / step (an
+// approximate reciprocal: the norms only steer restarts and the primal weight).  Before, each check iteration loaded
+// the 9 widths of its three steps and each restart loaded them again and divided 9 times.
+#ifndef DVH_BAND_RSTEP
+#define DVH_BAND_RSTEP 1
+#endif
+constexpr bool kBoxRescale = DVH_BAND_RSTEP != 0;
 // DVH_BAND_PROBE (A/B builds only, scripts/probe_band_latency.py): every wave accumulates the shader-clock cycles of
 // its iterations' four segments -- primal half-step, wait at the first barrier, dual half-step, wait at the second --
 // and of the checks, and lane 0 writes them over x[6 wid .. 6 wid + 4] of its window at the end, with the wave's
@@ -952,6 +961,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
   const int chk = o.check_every > 0 ? o.check_every : 64;
   double tau = uniform(eta / pw), sigma = uniform(eta * pw);
   double sigma2n = uniform(-2.0 * sigma);  // the equality rows' fused dual step (non-check iterations)
+  double tau_bs = tau;                     // (kBoxRescale) the tau the box steps were last formed for
   auto box_steps = [&]() {
     if constexpr (BOX) {
 #pragma unroll
@@ -967,6 +977,26 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
     }
   };
   box_steps();
+  // (kBoxRescale) the steps for a new tau from the current ones: tau / w^2 = (tau / tau_bs) (tau_bs / w^2)
+  auto box_steps_rescale = [&]() {
+    if constexpr (BOX) {
+      if constexpr (kBoxRescale) {
+        const double f = uniform(tau / tau_bs);
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+#pragma unroll
+          for (int v = 0; v < NC; ++v) {
+            if (v < 3)
+              tj[s][v < 3 ? v : 0] *= f;
+            else
+              ro(v - 1, s) *= f;
+          }
+        tau_bs = tau;
+      } else {
+        box_steps();
+      }
+    }
+  };
   const int kkt_every = o.kkt_every > 0 ? o.kkt_every : 1;
   int ck = chk, kk_ = kkt_every;
   KktGate gate;  // dvh_options.kkt_predict (dvh_device.h)
@@ -981,6 +1011,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
   // the partial loads are issued first); J >= 2 takes the generic per-column loop
   const bool w0 = wid == 0 && J == 1;
   double mv0, mv1, mv2, mv3;
+  double mvb0 = 0.0, mvb1 = 0.0;  // (kBoxRescale) the box columns' movements, d'^2 / step
   auto tau_update = [&](double kt, double ca, double cb, auto chk_tag) __attribute__((always_inline)) {
     constexpr bool CHECK = decltype(chk_tag)::value;
     if (tlane) {
@@ -1046,6 +1077,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
     }
     const double cb = readlane_f64(hw, kin - kbase), ca = 1.0 - cb;
     mv0 = mv1 = mv2 = mv3 = 0.0;
+    mvb0 = mvb1 = 0.0;
     // ---------------- primal half-step (reflected Halpern, rho = 1)
     double kx[S][NR];  // own-lane part of K x-bar for the dual half-step
     {
@@ -1079,13 +1111,20 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
           xb[s][v] = fma(2.0, p1, -x[s][v]);
           if (CHECK) {
             double d = x[s][v] - p1, da = p1 - axv(s, v);
-            if constexpr (BOX) {  // movements in x units
-              const double wv = wcol(s, v);
-              d *= wv;
-              da *= wv;
+            if constexpr (BOX && kBoxRescale) {  // movements in x units: w^2 = tau_bs / step (0 for a fixed column)
+              const double st = v < 3 ? tj[s][v < 3 ? v : 0] : ro(v - 1, s);
+              const double iw = st > 0.0 ? (double)__builtin_amdgcn_rcp(st) : 0.0;
+              mvb0 = fma(d * d, iw, mvb0);
+              mvb1 = fma(da * da, iw, mvb1);
+            } else {
+              if constexpr (BOX) {  // movements in x units
+                const double wv = wcol(s, v);
+                d *= wv;
+                da *= wv;
+              }
+              mv0 += d * d;
+              mv1 += da * da;
             }
-            mv0 += d * d;
-            mv1 += da * da;
             if constexpr (LI) {
               if (val[s]) xim[opaque(col(s, v))] = p1;
             } else {
@@ -1202,8 +1241,8 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
     // on config 5 at unchanged iterations (register pressure of its check path; profiles/r04ab_ab_kkt_rdx.log)
     constexpr int NRED = (ICE && DVH_KKT_RDX) ? kNRed - 1 : kNRed;
     double acc[NRED];
-    acc[0] = mv0;
-    acc[1] = mv1;
+    acc[0] = fma(tau_bs, mvb0, mv0);  // (mvb0 = mvb1 = 0 without kBoxRescale)
+    acc[1] = fma(tau_bs, mvb1, mv1);
     acc[2] = mv2;
     acc[3] = mv3;
 #pragma unroll
@@ -1351,7 +1390,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
       tau = uniform(eta / pw);
       sigma = uniform(eta * pw);
       sigma2n = uniform(-2.0 * sigma);
-      box_steps();
+      box_steps_rescale();
       double xp[S][NC], yp[S][NR];
       load_images(xp, yp);
 #pragma unroll
