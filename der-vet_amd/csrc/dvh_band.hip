@@ -83,13 +83,25 @@ __host__ __device__ inline size_t band_lds_bytes(int B, int S, bool ice, int LF)
 // no factor at all.  Only the residual norms and ||y|| are unscaled, with fd = the factor in single precision
 // (Work::fc / fr) and a 1-ulp v_rcp_f32 reciprocal: each term moves by a relative 2e-7 at most, i.e. each norm by a
 // relative 2e-7 of itself.  The outputs are unscaled with the exact factors.
+// DVH_KKT_INLINE (default 1): the KKT helpers below inlined.  Out of line (round 1-4: kept out of line so as not to
+// raise the kernel's register allocation) every call bound the caller's live registers to the call ABI: inlined, the
+// persistent battery form runs 1.5 % faster per iteration with no checks at all and 0.8-1.2 % on the sweep's check
+// schedules (profiles/r05s_check_cost_*.log).
+#ifndef DVH_KKT_INLINE
+#define DVH_KKT_INLINE 1
+#endif
+#if DVH_KKT_INLINE
+#define DVH_KKT_FN __forceinline__
+#else
+#define DVH_KKT_FN __noinline__
+#endif
 struct ColKkt {
   double rd2, cx, bt;
 };
 struct ColKktX : ColKkt {
   double rdx;  // |r_d| |x| of the column, unscaled (the battery forms' objective gate)
 };
-__device__ __noinline__ ColKkt col_kkt_fn(double kt, double cj, double loj, double hij, double xj, float fd) {
+__device__ DVH_KKT_FN ColKkt col_kkt_fn(double kt, double cj, double loj, double hij, double xj, float fd) {
   const double id = (double)__builtin_amdgcn_rcpf(fd);
   const double rs = cj - kt;  // scaled reduced cost
   const bool fl = isfinite(loj), fh = isfinite(hij);
@@ -97,7 +109,7 @@ __device__ __noinline__ ColKkt col_kkt_fn(double kt, double cj, double loj, doub
   const double rd = (rs - lam) * id;
   return {rd * rd, cj * xj, (fl ? loj * fmax(lam, 0.0) : 0.0) + (fh ? hij * fmin(lam, 0.0) : 0.0)};
 }
-__device__ __noinline__ ColKktX col_kkt_fn_x(double kt, double cj, double loj, double hij, double xj, float fd) {
+__device__ DVH_KKT_FN ColKktX col_kkt_fn_x(double kt, double cj, double loj, double hij, double xj, float fd) {
   const double id = (double)__builtin_amdgcn_rcpf(fd);
   const double rs = cj - kt;  // scaled reduced cost
   const bool fl = isfinite(loj), fh = isfinite(hij);
@@ -113,7 +125,7 @@ __device__ __noinline__ ColKktX col_kkt_fn_x(double kt, double cj, double loj, d
 struct RowKkt {
   double rp2, y2;
 };
-__device__ __noinline__ RowKkt row_kkt_fn(double kv, double qi, double yi, float fd, int ge) {
+__device__ DVH_KKT_FN RowKkt row_kkt_fn(double kv, double qi, double yi, float fd, int ge) {
   const double dr = (double)fd, idr = (double)__builtin_amdgcn_rcpf(fd);
   double r = (qi - kv) * idr;
   if (ge) r = fmax(r, 0.0);
