@@ -74,7 +74,15 @@ typedef __attribute__((address_space(1))) int gi32;
 struct ColKktC {
   double rd2, cx, bt, rdx;
 };
-__device__ __noinline__ ColKktC col_kkt_c(double kt, double cj, double loj, double hij, double xj, double d) {
+#ifndef DVH_CHAIN_KKT_INLINE
+#define DVH_CHAIN_KKT_INLINE 1
+#endif
+#if DVH_CHAIN_KKT_INLINE
+#define DVH_CHAIN_KKT_FN __forceinline__
+#else
+#define DVH_CHAIN_KKT_FN __noinline__
+#endif
+__device__ DVH_CHAIN_KKT_FN ColKktC col_kkt_c(double kt, double cj, double loj, double hij, double xj, double d) {
   const double rc = (cj - kt) / d;
   const bool fl = isfinite(loj), fh = isfinite(hij);
   const double lam = (fl && fh) ? rc : (fl ? fmax(rc, 0.0) : (fh ? fmin(rc, 0.0) : 0.0));
@@ -85,7 +93,7 @@ __device__ __noinline__ ColKktC col_kkt_c(double kt, double cj, double loj, doub
 struct RowKktC {
   double rp2, y2;
 };
-__device__ __noinline__ RowKktC row_kkt_c(double kv, double qi, double yi, double dr, bool ge) {
+__device__ DVH_CHAIN_KKT_FN RowKktC row_kkt_c(double kv, double qi, double yi, double dr, bool ge) {
   double r = (qi - kv) / dr;
   if (ge) r = fmax(r, 0.0);
   return {r * r, (yi * dr) * (yi * dr)};
