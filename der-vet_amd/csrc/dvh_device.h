@@ -68,9 +68,18 @@ __device__ __forceinline__ double row_sum16(double v) {
 }
 
 // Primal-weight update w <- exp(theta log(ratio) + (1 - theta) log(w)) (PDLP smoothing).  theta = 1 and
-// theta = 0.5 have closed forms; the general case is a separate (non-inlined) function so that the
-// exp / log polynomial constants are not hoisted into the iteration loop's registers.
+// theta = 0.5 have closed forms.  [r5] The general case is inlined too (DVH_PW_INLINE, default 1): as a call it
+// bound the kernels' live registers to the call ABI at its call site -- inlined, the market days run 11.1 / 14.8 ms
+// (market options / defaults) instead of 11.4 / 15.7 and config 3 168 instead of 174 ms
+// (profiles/r05v_pw_inline.log).
+#ifndef DVH_PW_INLINE
+#define DVH_PW_INLINE 1
+#endif
+#if DVH_PW_INLINE
+__device__ __forceinline__ double pw_update_general(double ratio, double w, double theta) {
+#else
 __device__ __noinline__ double pw_update_general(double ratio, double w, double theta) {
+#endif
   return exp(theta * log(ratio) + (1.0 - theta) * log(w));
 }
 __device__ __forceinline__ double pw_update(double ratio, double w, double theta) {
