@@ -14,7 +14,7 @@ namespace {
 #endif
 constexpr int kNRed = 10 + DVH_KKT_RDX;  // values reduced by a termination (KKT) check ([10]: sum_j |r_d,j| |x_j|)
 constexpr int kRdx = DVH_KKT_RDX ? 10 : 0;  // its slot (an unused 0 slot without it)
-__host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
+__host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
 constexpr int kOptimal = 0, kIterLimit = 3, kNumerical = 4;
 

@@ -115,7 +115,7 @@ hipError_t launch_pdhg(const Batch& b, const Work& w, const Chunk& ch, const Opt
 // ELL fast-path kernel over the whole chunk, or over the listed windows (wx, wy: ELL widths for K^T and K).
 // Windows that do not fit its shape come back with istats status -1 (kNeedsGeneric) and must be re-run by
 // launch_pdhg.
-// latency: skip the several-windows-per-CU small variants (a list of at most two windows per CU).
+// latency: a list of at most two windows per CU (small variants only where they beat the 512-thread kernels).
 hipError_t launch_pdhg_ell(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n, int max_m,
                            int wx, int wy, hipStream_t s, int* variant_out, const int32_t* list, int nlist,
                            bool latency = false);

@@ -852,13 +852,13 @@ __device__ __forceinline__ void wave_scatter(double v, int tgt, double* part) {
 // KR bit 0: the ELL values of K^T live in VGPRs (else in LDS, [WX][RX] column-major slices); bit 1: those of K
 // (else [WY][RY] in LDS).  KR != 0 variants also keep T(z_k) = (x+, y+) of the last check in LDS images
 // (else in the x / y output arrays in HBM).
-__host__ __device__ inline size_t ell_lds_doubles(int n, int m, int B, int XS, int YS, int WX, int WY, int KR) {
+__host__ __device__ constexpr size_t ell_lds_doubles(int n, int m, int B, int XS, int YS, int WX, int WY, int KR) {
   const int NW = B / kWave;
   const size_t img = (size_t)n + m + 2 * (size_t)B;
   return img + (KR ? img : 0) + ((KR & 1) ? 0 : (size_t)WX * XS * B) + ((KR & 2) ? 0 : (size_t)WY * YS * B) +
          2 * (size_t)NW * kLMax + (size_t)kNRed * (NW + 1) + 4 + 12 * kLMax;
 }
-__host__ __device__ inline size_t ell_lds_bytes(int n, int m, int B, int XS, int YS, int WX, int WY, int KR) {
+__host__ __device__ constexpr size_t ell_lds_bytes(int n, int m, int B, int XS, int YS, int WX, int WY, int KR) {
   const size_t d = ell_lds_doubles(n, m, B, XS, YS, WX, WY, KR);
   return align16(sizeof(double) * d) + align16(sizeof(int32_t) * 4 * kLMax);
 }
@@ -1647,6 +1647,7 @@ hipError_t dispatch_xy(int xs, int ys, const Batch& b, const Work& w, const Chun
   DVH_CASE(2, 2)
   DVH_CASE(5, 3)
   DVH_CASE(6, 4)
+  DVH_CASE(6, 6)
   DVH_CASE(8, 8)
 #undef DVH_CASE
   return hipErrorInvalidValue;
@@ -1673,22 +1674,30 @@ hipError_t launch_ell_one(const Batch& b, const Work& w, const Chunk& ch, const 
 #define DVH_KR768 -1
 #endif
 // K and K^T in VGPRs for the narrow <2,4> slices (the monthly battery + DCM window: measured 1.40 vs 1.59
-// us per window-iteration per CU against K^T in LDS); only K for the <4,8> slices, whose K^T registers
-// would spill.
+// us per window-iteration per CU against K^T in LDS).
 template <int WX, int WY>
-constexpr int kr768() { return DVH_KR768 >= 0 ? DVH_KR768 : (WX <= 2 && WY <= 4 ? 3 : 2); }
+constexpr int kr768() { return DVH_KR768 >= 0 ? DVH_KR768 : 3; }
 template <int WX, int WY>
 hipError_t ell_dispatch_xy(int max_n, int max_m, const Batch& b, const Work& w, const Chunk& ch, const Opts& o,
                            hipStream_t s, int* variant_out, const int32_t* list, int nlist) {
-#define DVH_CASE(B_, X_, Y_, KR_)                                                                          \
-  if (max_n <= X_ * B_ && max_m <= Y_ * B_ && ell_lds_bytes(max_n, max_m, B_, X_, Y_, WX, WY, KR_) <= 160 * 1024) { \
-    if (variant_out) *variant_out = (2000000 + 1000000 * KR_) + WX * 100000 + WY * 10000 + (B_ / 64) * 100 + X_ * 10 + Y_; \
-    return launch_ell_one<B_, X_, Y_, WX, WY, KR_>(b, w, ch, o, max_n, max_m, s, list, nlist);                          \
+  // (instantiations whose ELL slices alone exceed the LDS are never launchable and are not compiled: <512,5,3>,
+  // <512,6,4> and <512,8,6> of the <4,8> slices, <512,8,6> of the <2,4> ones; they had spilled 78-698 VGPRs)
+#define DVH_CASE(B_, X_, Y_, KR_)                                                                                 \
+  if constexpr (ell_lds_bytes(0, 0, B_, X_, Y_, WX, WY, KR_) <= 160 * 1024) {                                     \
+    if (max_n <= X_ * B_ && max_m <= Y_ * B_ && ell_lds_bytes(max_n, max_m, B_, X_, Y_, WX, WY, KR_) <= 160 * 1024) { \
+      if (variant_out)                                                                                            \
+        *variant_out = (2000000 + 1000000 * KR_) + WX * 100000 + WY * 10000 + (B_ / 64) * 100 + X_ * 10 + Y_;     \
+      return launch_ell_one<B_, X_, Y_, WX, WY, KR_>(b, w, ch, o, max_n, max_m, s, list, nlist);                  \
+    }                                                                                                             \
   }
   DVH_CASE(512, 1, 1, 3)
   DVH_CASE(512, 2, 2, 3)
 #ifndef DVH_NO768
-  DVH_CASE(768, 3, 2, (kr768<WX, WY>()))
+  // <2,4> slices only: the <4,8> form (K in VGPRs) spilled 144-165 VGPRs at the 768-thread budget, and no measured
+  // workload reached it (POI windows of 1,921 columns refuse the ELL shape, profiles/r05y_poi_paths.log)
+  if constexpr (WX <= 2 && WY <= 4) {
+    DVH_CASE(768, 3, 2, (kr768<WX, WY>()))
+  }
 #endif
   DVH_CASE(512, 5, 3, 0)
   DVH_CASE(512, 6, 4, 0)
@@ -1754,16 +1763,25 @@ hipError_t launch_pdhg(const Batch& b, const Work& w, const Chunk& ch, const Opt
               : dispatch_xy<false>(xs, ys, b, w, ch, o, lds, s, list, nlist);
 }
 
-// Small windows (the daily market-service window: T = 24, n = 168, m <= 217, K^T rows <= 6, K rows <= 8): one
-// single-wave workgroup per window, so the loop's barriers are one-wave barriers and several windows share a
-// CU (a 512-thread workgroup per window would leave most lanes without a column or a row).
-static int small_variant() {  // DVH_SMALL=-1: off (A/B against the 512-thread kernels); 0..6: force a variant
+// Small windows (the daily market-service window: T = 24, n = 168, m <= 265, K^T rows <= 6, K rows <= 8; with
+// SR + NSR n = 264, with load following n = 408, m <= 505): one four-wave workgroup per window with K and K^T values
+// in VGPRs (one column and two rows per lane up to n = 256, two and two up to 512) -- spill-free, two windows per CU.
+// 1,095 Usecase 3 days (MARKET_OPTIONS): 5.3 ms (DA + FR), 5.7 ms (+ SR + NSR), 9.9 ms (+ LF), 15.5 ms (CombinedMarket
+// LF), against 11.3 / 17.4 / 11.2 / 47.7 ms for the round-4 table of one- and two-wave variants, whose register
+// budgets spilled 19-245 VGPRs (profiles/r05w_market_variants.log, r05x_market_candidates*.log).
+static int small_variant() {  // DVH_SMALL=-1: off (A/B against the 512-thread kernels); 0..2: force a variant
   static const int v = getenv("DVH_SMALL") ? atoi(getenv("DVH_SMALL")) : 99;
+  return v;
+}
+// DVH_SMALL_LATENCY=0/1: skip all / take all small variants for batches of at most two windows per CU (A/B)
+static int small_latency() {
+  static const int v = getenv("DVH_SMALL_LATENCY") ? atoi(getenv("DVH_SMALL_LATENCY")) : -1;
   return v;
 }
 
 hipError_t small_dispatch(int max_n, int max_m, int wx, int wy, const Batch& b, const Work& w, const Chunk& ch,
-                          const Opts& o, hipStream_t s, int* variant_out, const int32_t* list, int nlist) {
+                          const Opts& o, hipStream_t s, int* variant_out, const int32_t* list, int nlist,
+                          bool latency) {
   const int sv = small_variant();
 #define DVH_SMALL(V_, B_, X_, Y_, WX_, WY_, KR_, WPE_)                                                          \
   if ((sv == 99 || sv == V_) && max_n <= X_ * B_ && max_m <= Y_ * B_ && wx <= WX_ && wy <= WY_) {             \
@@ -1771,21 +1789,17 @@ hipError_t small_dispatch(int max_n, int max_m, int wx, int wy, const Batch& b, 
       *variant_out = (2000000 + 1000000 * KR_) + WX_ * 100000 + WY_ * 10000 + (B_ / 64) * 100 + X_ * 10 + Y_; \
     return launch_ell_one<B_, X_, Y_, WX_, WY_, KR_, WPE_>(b, w, ch, o, max_n, max_m, s, list, nlist);       \
   }
-  DVH_SMALL(0, 64, 3, 5, 6, 8, 3, 1)
-  DVH_SMALL(1, 64, 3, 5, 6, 8, 0, 2)
-  DVH_SMALL(2, 128, 2, 3, 6, 8, 3, 2)
-  DVH_SMALL(3, 128, 2, 3, 6, 8, 1, 3)
-  DVH_SMALL(4, 128, 2, 3, 6, 8, 0, 4)
-  // market windows with load following + reserves (n <= 384, m <= 512: 24-step days with 15 column blocks):
-  // two waves, K and K^T values in LDS (their SOE rows are long rows, reduced by several targets per wave,
-  // which the register-resident KR variants do not take)
-  DVH_SMALL(5, 128, 3, 4, 6, 8, 0, 2)
-  // ... with CombinedMarket load following (one more equality block: n = 17 T = 408, m ~ 22 T at T = 24; the LF
-  // columns sit in 5 rows, beyond the 512-thread kernels' K^T width 4).  Only for those: windows the 512-thread
-  // kernels take (K^T width <= 4, e.g. load following without CombinedMarket, m just above 512) run 2.9x faster
-  // there (profiles/r02zj_market_variants.log)
-  if (wx > 4 || sv == 6) {
-    DVH_SMALL(6, 256, 2, 3, 6, 8, 0, 2)
+  DVH_SMALL(0, 256, 1, 2, 6, 8, 3, 1)
+  // two columns per lane: behind the 512-thread ELL kernel for batches of at most two windows per CU (load-following
+  // days, n = 408: 7.6 vs 6.5 ms for 366 windows), ahead of it beyond (9.98 vs 11.3 ms for 1,095); ahead of the
+  // generic kernel, which takes K^T rows wider than 4, at every size (SR + NSR days: 1.9 vs 3.9 ms for 15 windows)
+  if (latency && small_latency() != 1 && wx <= 4) return hipErrorInvalidValue;
+  DVH_SMALL(1, 256, 2, 2, 6, 8, 3, 1)
+  // m up to 768 with K^T rows of 5-6 entries (beyond the 512-thread kernels' width 4): K and K^T values in LDS.
+  // Windows the 512-thread kernels take (K^T width <= 4, m just above 512) run 2.9x faster there
+  // (profiles/r02zj_market_variants.log)
+  if (wx > 4 || sv == 2) {
+    DVH_SMALL(2, 256, 2, 3, 6, 8, 0, 2)
   }
 #undef DVH_SMALL
   return hipErrorInvalidValue;
@@ -1795,11 +1809,11 @@ static bool small_enabled() { return small_variant() >= 0; }
 hipError_t launch_pdhg_ell(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, int max_n, int max_m,
                            int wx, int wy, hipStream_t s, int* variant_out, const int32_t* list, int nlist,
                            bool latency) {
-  // latency: few windows (at most two per CU) -- the small variants pack several windows per CU for throughput and
-  // lose to the one-window-per-CU kernels then (market days: 14.7 vs 11.0 ms for 365 windows, 15.3 vs 18.8 ms for
-  // 1,095, profiles/r03h_market_paths.log), so only the 512-thread ELL kernels or the generic kernel are tried
-  if (max_n <= 512 && max_m <= 768 && wx <= 6 && wy <= 8 && small_enabled() && !latency) {
-    const hipError_t e = small_dispatch(max_n, max_m, wx, wy, b, w, ch, o, s, variant_out, list, nlist);
+  // latency: few windows (at most two per CU) -- the small variants that beat the 512-thread kernels there (DA + FR
+  // days: 1.7 vs 3.8 ms for 15 windows, 3.7 vs 8.8 ms for 366 against the generic kernel,
+  // profiles/r05y_market_table.log; DVH_SMALL_LATENCY=0 skips them, =1 takes all)
+  if (max_n <= 512 && max_m <= 768 && wx <= 6 && wy <= 8 && small_enabled() && (!latency || small_latency() != 0)) {
+    const hipError_t e = small_dispatch(max_n, max_m, wx, wy, b, w, ch, o, s, variant_out, list, nlist, latency);
     if (e != hipErrorInvalidValue) return e;
     (void)hipGetLastError();  // no small variant covers the shape (e.g. DVH_SMALL forcing one): the 512-thread kernels
   }

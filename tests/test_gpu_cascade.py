@@ -2,7 +2,7 @@
 batch that mixes every tier the drop-in can send at once (dervet/DERVET.py:75-83 puts every case's windows in one
 batch): Usecase 3 market days, config-4 monthly windows, config-5 LP-relaxed ICE windows, POI + curtailable-PV
 windows, annual hourly windows and the 5-minute annual window.  Each tier takes its windows (the next tier is sized for
-the windows that reach it: the market days run on the small ELL kernels, not the generic one), every window agrees
+the windows that reach it: the market days run on the small ELL kernel, the POI windows on the generic one), every window agrees
 with HiGHS within 1e-5, and the host waits once per tier that ran.  scripts/ab_cascade.sh compares the same batch bit
 for bit with the previous library (profiles/r03g_ab_cascade.log)."""
 import numpy as np
@@ -37,9 +37,9 @@ def test_mixed_batch_takes_every_tier_with_one_wait_per_tier(gpu_solver):
     res = gpu_solver.solve(lps)
     ks = gpu_solver.kernel_stats()
     assert ks["band_windows"] == n["config4"] + n["config5"], ks
-    # the market days and the POI windows are few (<= two per CU): both size classes end on the one-window-per-CU
-    # generic kernel (the POI windows fit no ELL instantiation), in one launch
-    assert ks["ell_windows"] == 0 and ks["generic_windows"] == n["market"] + n["poi"], ks
+    # the market days are few (<= two per CU) and take the four-wave small ELL variant; the POI windows fit no ELL
+    # instantiation and end on the one-window-per-CU generic kernel
+    assert ks["ell_windows"] == n["market"] and ks["generic_windows"] == n["poi"], ks
     assert ks["chain_windows"] == n["annual"] and ks["large_windows"] == 0, ks
     # band pass + ICE pass (its refusals' count, then their size classes once set up) + ELL pass read-backs, the
     # medium tier's plan / setup / team hand-offs, the final wait
@@ -68,11 +68,11 @@ def test_a_batch_the_band_kernel_takes_whole_waits_once_in_the_cascade(gpu_solve
     assert gpu_solver.host_syncs() == 2, gpu_solver.host_syncs()
 
 
-@pytest.mark.parametrize("days,key", [(122, "generic_windows"), (1095, "ell_windows")])
-def test_market_days_take_the_generic_kernel_when_few_and_the_small_ell_kernels_when_many(gpu_solver, days, key):
-    """Latency vs throughput (profiles/r03h_market_paths.log): up to two windows per CU the one-window-per-CU generic
-    kernel is faster (365 days: 11.0 vs 14.7 ms), beyond that the small ELL variants that pack several windows per
-    CU (1,095 days: 15.3 vs 18.8 ms)."""
+@pytest.mark.parametrize("days", [122, 1095])
+def test_market_days_take_the_small_ell_kernel_at_every_batch_size(gpu_solver, days):
+    """The four-wave small ELL variant (one column per lane, K and K^T in VGPRs, two windows per CU) takes the DA + FR
+    days for few windows as for many (profiles/r05y_market_table.log: 3.6 vs 8.0 ms for 120 days against the generic
+    kernel, 5.4 vs 11.3 ms for 1,095 against the round-4 one-wave variant)."""
     arr, meta = cases.load_market()
     names = ("es", "es+pv", "es+pv+dg")
     gl = []
@@ -82,5 +82,6 @@ def test_market_days_take_the_generic_kernel_when_few_and_the_small_ell_kernels_
                                         days=list(range(0, 365, 3 if days < 365 else 1))[:days // 3 + 1]))
     lps = [lp for g in gl for lp in builder.group_window_lps(g)][:days]
     res = gpu_solver.solve(lps)
-    assert gpu_solver.kernel_stats()[key] == len(lps), gpu_solver.kernel_stats()
+    st = gpu_solver.kernel_stats()
+    assert st["ell_windows"] == len(lps) and st["variant"] == 5680412, st
     assert all(r.status == 0 for r in res)

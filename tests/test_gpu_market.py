@@ -8,6 +8,7 @@ Bars: objective within 1e-5 relative of HiGHS on the same relaxed LP (oracle/win
 """
 import numpy as np
 import pytest
+import torch
 
 from dervet_hip import BatchSolver
 from dervet_hip.lp import builder, scenarios
@@ -31,10 +32,10 @@ def test_market_days_match_highs_and_bound_golden(gpu_solver, name):
     g = scenarios.market_days(sig, meta["params"], days=days)
     lps = builder.group_window_lps(g)
     res = gpu_solver.solve(lps)
-    # 73 days (at most two per CU): the latency regime of the cascade -- the one-window-per-CU generic kernel, not the
-    # small ELL variants (tests/test_gpu_cascade.py pins the routing; test_small_window_kernel_agrees_with_generic the
-    # small ELL kernel on these windows)
-    assert gpu_solver.kernel_stats()["generic_windows"] == len(lps)
+    # 73 days (at most two per CU): the latency regime of the cascade, also taken by the four-wave small ELL variant
+    # (tests/test_gpu_cascade.py pins the routing; test_small_window_kernel_agrees_with_generic compares it with the
+    # generic kernel on these windows)
+    assert gpu_solver.kernel_stats()["ell_windows"] == len(lps)
     wins, keys = cases.market_windows(name)
     worst = 0.0
     for k, (d, r) in enumerate(zip(days, res)):
@@ -86,7 +87,7 @@ def test_market_days_without_relaxation_row(gpu_solver):
 
 
 def test_small_window_kernel_agrees_with_generic():
-    """Single-wave ELL kernel (small windows) vs the generic CSR kernel on the same market days: same algorithm,
+    """Small-window ELL kernel vs the generic CSR kernel on the same market days: same algorithm,
     objectives within 1e-7, iteration counts within two check periods."""
     sig, meta = _signals("es+pv+dg")
     g = scenarios.market_days(sig, meta["params"], days=list(range(0, 365, 30)))
@@ -112,7 +113,8 @@ def test_reserve_windows_match_highs(gpu_solver):
     days = list(range(0, 365, 15))
     g = scenarios.market_days(sig, meta["params"], days=days, reserves=reserve_series(sig, pdis))
     res = gpu_solver.solve(builder.group_window_lps(g))
-    assert gpu_solver.kernel_stats()["generic_windows"] == len(days), gpu_solver.kernel_stats()  # latency regime
+    # latency regime: K^T rows of 5-6 entries, the two-columns-per-lane small variant
+    assert gpu_solver.kernel_stats()["ell_windows"] == len(days), gpu_solver.kernel_stats()
     for k, (d, r) in enumerate(zip(days, res)):
         o = dict(K=sp_csr(g, k), q=g.q[k], c=g.c[k], c0=float(g.c0[k]), l=g.l[k], u=g.u[k], m_eq=g.m_eq)
         h = window_lp.solve_highs(o)
@@ -136,14 +138,17 @@ def test_load_following_windows_match_highs(gpu_solver, combined):
                               lf=_lf(sig, pdis, combined=combined))
     res = gpu_solver.solve(builder.group_window_lps(g))
     st = gpu_solver.kernel_stats()
-    # without CombinedMarket (K^T width <= 4) the 512-thread ELL kernel takes the days (2.5x faster than the generic
-    # one here); CombinedMarket LF (width 5) fits only the small variant 6, which few windows skip for the generic
-    # kernel (profiles/r03h_market_paths.log)
-    assert st["ell_windows" if not combined else "generic_windows"] == len(days), st
-    with BatchSolver(0) as se:  # the ELL path alone still takes the CombinedMarket days with variant 6
-        se.set_kernel_path("ell")
-        se.solve(builder.group_window_lps(g))
-        assert (se.kernel_stats()["variant"] == 2680423) == combined, se.kernel_stats()
+    # few windows: without CombinedMarket (K^T width <= 4) the 512-thread ELL kernel takes the days (2.5x faster than
+    # the generic one here); CombinedMarket LF (width 5) the two-columns-per-lane small variant
+    assert st["ell_windows"] == len(days) and (st["variant"] == 5680422) == combined, st
+    # many windows: the two-columns-per-lane small variant takes both (9.98 / 15.4 ms for 1,095 days against 11.3 /
+    # 40.5 ms, profiles/r05x_market_candidates2.log); replicate the days past two windows per CU
+    lps = builder.group_window_lps(g)
+    with BatchSolver(0) as se:
+        rr = se.solve(lps * (1 + 2 * torch.cuda.get_device_properties(0).multi_processor_count // len(lps)))
+        assert se.kernel_stats()["variant"] == 5680422 and se.kernel_stats()["ell_windows"] == len(rr), se.kernel_stats()
+        for k, r in enumerate(rr):
+            assert r.status == 0 and abs(r.obj - res[k % len(res)].obj) <= 1e-5 * max(abs(r.obj), 1.0), (k, r.obj)
     # the oracle's direct form (options written into the SOE rows, no aggregate columns; tests/test_market_reserves)
     from test_market_reserves import _oracle_window
     wins, _ = cases.market_windows("es")
