@@ -83,25 +83,25 @@ __host__ __device__ inline size_t band_lds_bytes(int B, int S, bool ice, int LF)
 // no factor at all.  Only the residual norms and ||y|| are unscaled, with fd = the factor in single precision
 // (Work::fc / fr) and a 1-ulp v_rcp_f32 reciprocal: each term moves by a relative 2e-7 at most, i.e. each norm by a
 // relative 2e-7 of itself.  The outputs are unscaled with the exact factors.
-// DVH_KKT_INLINE (default 1): the KKT helpers below inlined.  Out of line (round 1-4: kept out of line so as not to
-// raise the kernel's register allocation) every call bound the caller's live registers to the call ABI: inlined, the
-// persistent battery form runs 1.5 % faster per iteration with no checks at all and 0.8-1.2 % on the sweep's check
-// schedules (profiles/r05s_check_cost_*.log).
+// DVH_KKT_INLINE: 1 (default) the KKT helpers below inlined into the battery forms and called out of line from the ICE
+// form; 2 inlined everywhere; 0 out of line everywhere (rounds 1-4, so as not to raise the kernel's register
+// allocation).  Out of line, every call binds the caller's live registers to the call ABI: inlined, the persistent
+// battery form runs 1.5 % faster per iteration with no checks at all and 0.8-1.2 % on the sweep's check schedules
+// (profiles/r05s_check_cost_*.log).  The ICE form (168-VGPR budget, already spilling) runs config 5 5.6 % slower with
+// them inlined (106.5k vs 112.9k windows/s, identical iterations; profiles/r05za_config5_bisect.log), although a
+// fixed-iteration run with checks that never converge had it 9.4 % faster (profiles/r05u_kkt_inline_ice_chain.log).
 #ifndef DVH_KKT_INLINE
 #define DVH_KKT_INLINE 1
 #endif
-#if DVH_KKT_INLINE
-#define DVH_KKT_FN __forceinline__
-#else
-#define DVH_KKT_FN __noinline__
-#endif
+template <bool ICE>
+constexpr bool kkt_inline() { return DVH_KKT_INLINE == 2 || (DVH_KKT_INLINE == 1 && !ICE); }
 struct ColKkt {
   double rd2, cx, bt;
 };
 struct ColKktX : ColKkt {
   double rdx;  // |r_d| |x| of the column, unscaled (the battery forms' objective gate)
 };
-__device__ DVH_KKT_FN ColKkt col_kkt_fn(double kt, double cj, double loj, double hij, double xj, float fd) {
+__device__ __forceinline__ ColKkt col_kkt_i(double kt, double cj, double loj, double hij, double xj, float fd) {
   const double id = (double)__builtin_amdgcn_rcpf(fd);
   const double rs = cj - kt;  // scaled reduced cost
   const bool fl = isfinite(loj), fh = isfinite(hij);
@@ -109,7 +109,7 @@ __device__ DVH_KKT_FN ColKkt col_kkt_fn(double kt, double cj, double loj, double
   const double rd = (rs - lam) * id;
   return {rd * rd, cj * xj, (fl ? loj * fmax(lam, 0.0) : 0.0) + (fh ? hij * fmin(lam, 0.0) : 0.0)};
 }
-__device__ DVH_KKT_FN ColKktX col_kkt_fn_x(double kt, double cj, double loj, double hij, double xj, float fd) {
+__device__ __forceinline__ ColKktX col_kkt_x_i(double kt, double cj, double loj, double hij, double xj, float fd) {
   const double id = (double)__builtin_amdgcn_rcpf(fd);
   const double rs = cj - kt;  // scaled reduced cost
   const bool fl = isfinite(loj), fh = isfinite(hij);
@@ -125,11 +125,35 @@ __device__ DVH_KKT_FN ColKktX col_kkt_fn_x(double kt, double cj, double loj, dou
 struct RowKkt {
   double rp2, y2;
 };
-__device__ DVH_KKT_FN RowKkt row_kkt_fn(double kv, double qi, double yi, float fd, int ge) {
+__device__ __forceinline__ RowKkt row_kkt_i(double kv, double qi, double yi, float fd, int ge) {
   const double dr = (double)fd, idr = (double)__builtin_amdgcn_rcpf(fd);
   double r = (qi - kv) * idr;
   if (ge) r = fmax(r, 0.0);
   return {r * r, (yi * dr) * (yi * dr)};
+}
+__device__ __noinline__ ColKkt col_kkt_o(double kt, double cj, double loj, double hij, double xj, float fd) {
+  return col_kkt_i(kt, cj, loj, hij, xj, fd);
+}
+__device__ __noinline__ ColKktX col_kkt_x_o(double kt, double cj, double loj, double hij, double xj, float fd) {
+  return col_kkt_x_i(kt, cj, loj, hij, xj, fd);
+}
+__device__ __noinline__ RowKkt row_kkt_o(double kv, double qi, double yi, float fd, int ge) {
+  return row_kkt_i(kv, qi, yi, fd, ge);
+}
+template <bool INL>
+__device__ __forceinline__ ColKkt col_kkt_fn(double kt, double cj, double loj, double hij, double xj, float fd) {
+  if constexpr (INL) return col_kkt_i(kt, cj, loj, hij, xj, fd);
+  else return col_kkt_o(kt, cj, loj, hij, xj, fd);
+}
+template <bool INL>
+__device__ __forceinline__ ColKktX col_kkt_fn_x(double kt, double cj, double loj, double hij, double xj, float fd) {
+  if constexpr (INL) return col_kkt_x_i(kt, cj, loj, hij, xj, fd);
+  else return col_kkt_x_o(kt, cj, loj, hij, xj, fd);
+}
+template <bool INL>
+__device__ __forceinline__ RowKkt row_kkt_fn(double kv, double qi, double yi, float fd, int ge) {
+  if constexpr (INL) return row_kkt_i(kv, qi, yi, fd, ge);
+  else return row_kkt_o(kv, qi, yi, fd, ge);
 }
 
 // GATE: the predicted KKT gate (dvh_options.kkt_predict > 0) is compiled in only where the host asks for it -- its
@@ -1286,13 +1310,13 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
       auto col_kkt = [&](int j, double kt, double cj, double loj, double hij, double xj) {
         const int jj = opaque(j);
         if constexpr (NRED > kRdx && DVH_KKT_RDX) {
-          const ColKktX r = col_kkt_fn_x(kt, cj, loj, hij, xj, w.fc[W.wn + jj]);
+          const ColKktX r = col_kkt_fn_x<kkt_inline<ICE>()>(kt, cj, loj, hij, xj, w.fc[W.wn + jj]);
           acc[5] += r.rd2;
           acc[6] += r.cx;
           acc[8] += r.bt;
           acc[kRdx] += r.rdx;
         } else {
-          const ColKkt r = col_kkt_fn(kt, cj, loj, hij, xj, w.fc[W.wn + jj]);
+          const ColKkt r = col_kkt_fn<kkt_inline<ICE>()>(kt, cj, loj, hij, xj, w.fc[W.wn + jj]);
           acc[5] += r.rd2;
           acc[6] += r.cx;
           acc[8] += r.bt;
@@ -1300,7 +1324,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
       };
       auto row_kkt = [&](int i, double kv, double qi, double yi, bool ge) {
         const int ii = opaque(i);
-        const RowKkt r = row_kkt_fn(kv, qi, yi, w.fr[W.wm + ii], ge);
+        const RowKkt r = row_kkt_fn<kkt_inline<ICE>()>(kv, qi, yi, w.fr[W.wm + ii], ge);
         acc[4] += r.rp2;
         acc[7] += qi * yi;
         acc[9] += r.y2;
@@ -1398,7 +1422,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
                          ((double)kin >= o.b_art * (double)it);
     if (restart) {
       const double ddx = sqrt(acc[1]), ddy = sqrt(acc[3]);
-      if (ddx > 1e-10 && ddy > 1e-10) pw = uniform(pw_update(ddy / ddx, pw, o.theta));
+      if (ddx > 1e-10 && ddy > 1e-10) pw = uniform(pw_update<!ICE>(ddy / ddx, pw, o.theta));
       tau = uniform(eta / pw);
       sigma = uniform(eta * pw);
       sigma2n = uniform(-2.0 * sigma);

@@ -75,17 +75,19 @@ __device__ __forceinline__ double row_sum16(double v) {
 #ifndef DVH_PW_INLINE
 #define DVH_PW_INLINE 1
 #endif
-#if DVH_PW_INLINE
-__device__ __forceinline__ double pw_update_general(double ratio, double w, double theta) {
-#else
-__device__ __noinline__ double pw_update_general(double ratio, double w, double theta) {
-#endif
+__device__ __forceinline__ double pw_update_general_i(double ratio, double w, double theta) {
   return exp(theta * log(ratio) + (1.0 - theta) * log(w));
 }
+__device__ __noinline__ double pw_update_general_o(double ratio, double w, double theta) {
+  return pw_update_general_i(ratio, w, theta);
+}
+// INL = false: the general case out of line regardless (the band kernel's ICE form, whose 168-VGPR budget it strains)
+template <bool INL = true>
 __device__ __forceinline__ double pw_update(double ratio, double w, double theta) {
   if (theta == 1.0) return ratio;
   if (theta == 0.5) return sqrt(ratio * w);
-  return pw_update_general(ratio, w, theta);
+  if constexpr (INL && DVH_PW_INLINE) return pw_update_general_i(ratio, w, theta);
+  else return pw_update_general_o(ratio, w, theta);
 }
 
 // Makes an index opaque to the optimiser so that address arithmetic of cold (check-phase) code is not

@@ -1,0 +1,10 @@
+#!/bin/bash
+# Final round-5 sources: full GPU suite + smoke, then the full-population certification dump (seeded + cold).
+set -o pipefail
+O=gpurun_out/r05z; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo "tests failed"; tail -40 $O/gpu_tests.log; exit 1; }
+tail -1 $O/gpu_tests.log
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log | cut -c1-200
+timeout -k 10 400 python -u scripts/certify_dump.py --label r05z --blend 4 > $O/certify.log 2>&1 || { echo "dump failed"; tail -20 $O/certify.log; exit 1; }
+grep -E "seeded|cold" $O/certify.log | cut -c1-160
