@@ -4,7 +4,9 @@ The long window goes to the grid-wide large-LP path, whose PDHG needs tens of th
 cold start.  Its sub-windows (e.g. the 365 days of the year, each returning to the SOE target) are small
 battery windows that the batched band kernel solves together in a few milliseconds, and their solutions
 concatenated are a feasible, near-optimal point of the long window (it only drops the end-of-sub-window SOE
-targets).  ``solve_stitched`` solves the sub-windows as one batch, stitches their primal and dual solutions
+targets).  Monthly sub-windows (the long window's own demand-charge periods) carry their DCM epigraph duals over too:
+the long window's DCM row of step t for its k-th charge covering t starts from the sub-window's row of the same step
+and rank.  ``solve_stitched`` solves the sub-windows as one batch, stitches their primal and dual solutions
 into the long window's layout and starts the long window from there (``dvh_options.warm_start``).
 
 Layout (lp/builder.py battery_group): x = [ch (T), dis (T), ene (T), tau (J)]; rows
@@ -12,7 +14,8 @@ Layout (lp/builder.py battery_group): x = [ch (T), dis (T)
 (DCM epigraph: tau_j - net_t >= base_t).  Sub-window s covering steps [a, a + T_s) maps its rows 1..T_s - 1
 onto the long window's rows a + 1 .. a + T_s - 1 and its final row onto row a + T_s (the recurrence across
 the boundary, or the final row for the last sub-window).  tau_j is set to the smallest value its >= rows allow
-at the stitched (ch, dis); the DCM duals start at zero.
+at the stitched (ch, dis); the DCM duals start from the sub-windows' duals of the same (step, charge rank) rows where
+a sub-window has them (monthly sub-windows), else at zero.
 """
 import numpy as np
 
@@ -24,7 +27,24 @@ def _check_battery(g):
         raise ValueError(f"not a battery (+ DCM) window layout: n={g.n}, m_eq={g.m_eq}, T={g.T}, J={g.J}")
 
 
-def stitched_start(long, subs, sub_x, sub_y):
+def _dcm_rows(g):
+    """(step t, rank k among the DCM rows of step t, row index) of every DCM epigraph row of window group g: the >= rows
+    whose entries are ch_t, dis_t and one tau column (builder.battery_group's first >= block)."""
+    T, out, seen = g.T, [], {}
+    if not g.J:
+        return out
+    for r in range(g.m_eq, g.m):
+        cols = g.indices[g.indptr[r]:g.indptr[r + 1]]
+        if len(cols) < 3 or not (cols[0] < T and T <= cols[1] < 2 * T and 3 * T <= cols[2] < 3 * T + g.J):
+            break
+        t = int(cols[0])
+        k = seen.get(t, 0)
+        seen[t] = k + 1
+        out.append((t, k, r))
+    return out
+
+
+def stitched_start(long, subs, sub_x, sub_y, dcm_duals=False):
     """Starting point (x0, y0) of the long window `long` (WindowGroup, G = 1) from the solutions (sub_x[s],
     sub_y[s]) of its consecutive sub-windows `subs` (WindowGroups, G = 1, covering the long window's steps
     in order)."""
@@ -47,6 +67,17 @@ def stitched_start(long, subs, sub_x, sub_y):
         y0[a + 1: a + Ts] = ys[1: Ts]
         y0[a + Ts] = ys[Ts]
         a += Ts
+    if long.J and dcm_duals:
+        # DCM duals: rows of the long window keyed by (global step, rank of the charge among those covering it)
+        sub_dual = {}
+        a = 0
+        for s, g in enumerate(subs):
+            ys = np.asarray(sub_y[s], np.float64)
+            for t, k, r in _dcm_rows(g):
+                sub_dual[(a + t, k)] = ys[r]
+            a += g.T
+        for t, k, r in _dcm_rows(long):
+            y0[r] = sub_dual.get((t, k), 0.0)
     if long.J:
         K = sp.csr_matrix((long.data[0], long.indices, long.indptr), shape=(long.m, long.n))
         ge = K[long.m_eq:]
@@ -60,14 +91,14 @@ def stitched_start(long, subs, sub_x, sub_y):
     return x0, y0
 
 
-def solve_stitched(solver, long, subs):
+def solve_stitched(solver, long, subs, dcm_duals=False):
     """Solve the long window from the stitched solution of its sub-windows.  Returns (result of the long
     window, results of the sub-windows, {"subs_ms", "long_ms"} kernel times)."""
     from .lp import builder
     lps = [builder.group_window_lps(g)[0] for g in subs]
     sres = solver.solve(lps)
     subs_ms = solver.timing()["total_ms"]
-    x0, y0 = stitched_start(long, subs, [r.x for r in sres], [r.y for r in sres])
+    x0, y0 = stitched_start(long, subs, [r.x for r in sres], [r.y for r in sres], dcm_duals)
     w0 = solver.options().warm_start
     solver.set_options(warm_start=1)
     try:

@@ -82,3 +82,25 @@ def test_config3_stitched_from_daily_windows_on_gpu(gpu_solver):
     assert window_lp.primal_residual_rel(_lp(long), res.x)[0] <= 1e-6
     print(f"config 3: cold {cold.iters} iterations, stitched {res.iters} (+365 daily windows in "
           f"{tm['subs_ms']:.1f} ms), long-window solve {tm['long_ms']:.1f} ms")
+
+
+def test_monthly_sub_windows_carry_their_demand_charge_duals_over():
+    """dcm_duals=True: the long window's DCM epigraph row of step t takes the dual of the monthly sub-window's row of the
+    same step (the sub-windows are the long window's own demand-charge periods); without it those rows start at 0."""
+    long = _groups("year", True)[0]
+    subs = _groups("month", True)
+    sub_y = [np.arange(g.m, dtype=np.float64) + 1e6 * (s + 1) for s, g in enumerate(subs)]
+    sub_x = [np.zeros(g.n) for g in subs]
+    _, y0 = stitched_start(long, subs, sub_x, sub_y, dcm_duals=True)
+    _, y_off = stitched_start(long, subs, sub_x, sub_y)
+    from dervet_hip.stitch import _dcm_rows
+    rows = _dcm_rows(long)
+    assert len(rows) == long.m - long.m_eq  # every >= row of the retail + DCM window is a DCM row
+    a, want = 0, {}
+    for s, g in enumerate(subs):
+        for t, k, r in _dcm_rows(g):
+            want[(a + t, k)] = sub_y[s][r]
+        a += g.T
+    for t, k, r in rows:
+        assert y0[r] == want[(t, k)] and y_off[r] == 0.0
+    np.testing.assert_array_equal(y0[:long.m_eq], y_off[:long.m_eq])
