@@ -40,21 +40,55 @@ __global__ __launch_bounds__(kSwB) void warm_transfer_kernel(const int64_t* desc
   const double* wq = wts + (int64_t)Q * blockIdx.x;
   const int64_t onw = dw[6], omw = dw[7];
   const int tid = threadIdx.x;
-  for (int64_t j = tid; j < n; j += kSwB) {
-    const double ur = u[onw + j];
-    double acc = 0.0;
-    for (int i = 0; i < Q; ++i) {
-      const int64_t onp = desc[8 * (int64_t)row[1 + i] + 6];
-      const double us = u[onp + j];
-      const bool ok = isfinite(ur) && isfinite(us) && us > 0.0;
-      acc += wq[i] * (x[onp + j] * (ok ? ur / us : 1.0));
+  // the partners' offsets and weights, loaded once (uniform; slots q >= Q unused)
+  int64_t onp[kMaxBlend], omp[kMaxBlend];
+  double wqv[kMaxBlend];
+#pragma unroll
+  for (int q = 0; q < kMaxBlend; ++q) {
+    const int64_t* dp = desc + 8 * (int64_t)row[1 + (q < Q ? q : 0)];
+    onp[q] = dp[6];
+    omp[q] = dp[7];
+    wqv[q] = q < Q ? wq[q] : 0.0;
+  }
+  // [r5] every load of a chunk of kU elements per thread is issued before its arithmetic and stores (the window's
+  // x / y never overlap a partner's: a partner is a solved seed, never a listed window), so a thread has 2 kU Q loads
+  // in flight instead of one element's; the arithmetic per element is unchanged (bit-identical results)
+  constexpr int kU = 2;
+  for (int64_t j0 = tid; j0 < n; j0 += kU * kSwB) {
+    double ur[kU], uv[kMaxBlend][kU], xv[kMaxBlend][kU];
+#pragma unroll
+    for (int e = 0; e < kU; ++e) {
+      const int64_t j = j0 + e * kSwB;
+      ur[e] = j < n ? u[onw + j] : 0.0;
+#pragma unroll
+      for (int q = 0; q < kMaxBlend; ++q) {
+        uv[q][e] = (q < Q && j < n) ? u[onp[q] + j] : 1.0;
+        xv[q][e] = (q < Q && j < n) ? x[onp[q] + j] : 0.0;
+      }
     }
-    x[onw + j] = acc;
+#pragma unroll
+    for (int e = 0; e < kU; ++e) {
+      const int64_t j = j0 + e * kSwB;
+      if (j >= n) break;
+      double acc = 0.0;
+#pragma unroll
+      for (int q = 0; q < kMaxBlend; ++q) {
+        if (q >= Q) break;
+        const double us = uv[q][e];
+        const bool ok = isfinite(ur[e]) && isfinite(us) && us > 0.0;
+        acc += wqv[q] * (xv[q][e] * (ok ? ur[e] / us : 1.0));
+      }
+      x[onw + j] = acc;
+    }
   }
   if (T <= 0) {
     for (int64_t i = tid; i < m; i += kSwB) {
       double acc = 0.0;
-      for (int q = 0; q < Q; ++q) acc += wq[q] * y[desc[8 * (int64_t)row[1 + q] + 7] + i];
+#pragma unroll
+      for (int q = 0; q < kMaxBlend; ++q) {
+        if (q >= Q) break;
+        acc += wqv[q] * y[omp[q] + i];
+      }
       y[omw + i] = acc;
     }
     return;
@@ -63,19 +97,26 @@ __global__ __launch_bounds__(kSwB) void warm_transfer_kernel(const int64_t* desc
   const int lane = tid & 63, wid = tid >> 6;
   double a = 0.0;
   double bq[kMaxBlend];
+#pragma unroll
   for (int q = 0; q < kMaxBlend; ++q) bq[q] = 0.0;
   for (int j = tid; j < T; j += kSwB) {
     a += fabs(c[onw + j]);
-    for (int q = 0; q < Q; ++q) bq[q] += fabs(c[desc[8 * (int64_t)row[1 + q] + 6] + j]);
+#pragma unroll
+    for (int q = 0; q < kMaxBlend; ++q)
+      if (q < Q) bq[q] += fabs(c[onp[q] + j]);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     a += __shfl_xor(a, o, kWave);
-    for (int q = 0; q < Q; ++q) bq[q] += __shfl_xor(bq[q], o, kWave);
+#pragma unroll
+    for (int q = 0; q < kMaxBlend; ++q)
+      if (q < Q) bq[q] += __shfl_xor(bq[q], o, kWave);
   }
   if (lane == 0) {
     red[(kMaxBlend + 1) * wid] = a;
-    for (int q = 0; q < Q; ++q) red[(kMaxBlend + 1) * wid + 1 + q] = bq[q];
+#pragma unroll
+    for (int q = 0; q < kMaxBlend; ++q)
+      if (q < Q) red[(kMaxBlend + 1) * wid + 1 + q] = bq[q];
   }
   __syncthreads();
   if (tid < Q) {
@@ -84,16 +125,37 @@ __global__ __launch_bounds__(kSwB) void warm_transfer_kernel(const int64_t* desc
       sa += red[(kMaxBlend + 1) * v];
       sb += red[(kMaxBlend + 1) * v + 1 + tid];
     }
-    const int64_t onp = desc[8 * (int64_t)row[1 + tid] + 6];
+    const int64_t onq = desc[8 * (int64_t)row[1 + tid] + 6];
     cps[tid] = (sa / T) / fmax(sb / T, 1e-12);
-    cds[tid] = c[onw + 3 * (int64_t)T] / fmax(c[onp + 3 * (int64_t)T], 1e-12);
+    cds[tid] = c[onw + 3 * (int64_t)T] / fmax(c[onq + 3 * (int64_t)T], 1e-12);
   }
   __syncthreads();
-  for (int64_t i = tid; i < m; i += kSwB) {
-    double acc = 0.0;
-    for (int q = 0; q < Q; ++q)
-      acc += wq[q] * (y[desc[8 * (int64_t)row[1 + q] + 7] + i] * (i <= T ? cps[q] : cds[q]));
-    y[omw + i] = acc;
+  double cp[kMaxBlend], cd[kMaxBlend];
+#pragma unroll
+  for (int q = 0; q < kMaxBlend; ++q) {
+    cp[q] = q < Q ? cps[q] : 0.0;
+    cd[q] = q < Q ? cds[q] : 0.0;
+  }
+  for (int64_t i0 = tid; i0 < m; i0 += kU * kSwB) {
+    double yv[kMaxBlend][kU];
+#pragma unroll
+    for (int e = 0; e < kU; ++e) {
+      const int64_t i = i0 + e * kSwB;
+#pragma unroll
+      for (int q = 0; q < kMaxBlend; ++q) yv[q][e] = (q < Q && i < m) ? y[omp[q] + i] : 0.0;
+    }
+#pragma unroll
+    for (int e = 0; e < kU; ++e) {
+      const int64_t i = i0 + e * kSwB;
+      if (i >= m) break;
+      double acc = 0.0;
+#pragma unroll
+      for (int q = 0; q < kMaxBlend; ++q) {
+        if (q >= Q) break;
+        acc += wqv[q] * (yv[q][e] * (i <= T ? cp[q] : cd[q]));
+      }
+      y[omw + i] = acc;
+    }
   }
 }
 
