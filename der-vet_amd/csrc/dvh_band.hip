@@ -1656,8 +1656,9 @@ hipError_t launch_band_one(const Batch& b, const Work& w, const Chunk& ch, const
 // workspace (kLfImages) 5 % slower and 10x the HBM writes, with the anchors in LDS too (kLfAnchors) 8 % slower.
 // form 1: 768 threads, one step per lane, 12 waves, one window per CU (A/B, dvh_set_kernel_path 3).  The LP-relaxed
 // ICE windows keep the one-step form (twice the per-step state).
-#if DVH_BAND_PERSIST_TU
-// The persistent forms (three-step battery, ICE), compiled in dvh_band_persist.hip (this file with DVH_BAND_PERSIST_TU) without
+#if DVH_BAND_PERSIST_TU == 1
+// The persistent forms (three-step battery: dvh_band_persist.hip, DVH_BAND_PERSIST_TU 1; ICE: dvh_band_persist_ice.hip, 2),
+// each this file in a translation unit of its own, compiled without
 // machine-level loop-invariant code motion: hoisted out of the persistent loop, the window setup's invariants stayed live
 // across every window's iterations (56 spilled dwords, 12.6 % slower per iteration than one workgroup per window at
 // equal durations; 1.6 % without the hoisting, profiles/r04al_band_persist_nolicm.log).  The one-workgroup forms keep
@@ -1672,6 +1673,7 @@ hipError_t launch_band_persist(bool gate, bool box, const Batch& b, const Work& 
   if (box) return launch_band_one_q<B, 3, false, DVH_BAND3_LF, 2, false, true, true>(b, w, ch, o, s, list, nlist, variant_out);
   return launch_band_one_q<B, 3, false, DVH_BAND3_LF, 2, false, false, true>(b, w, ch, o, s, list, nlist, variant_out);
 }
+#elif DVH_BAND_PERSIST_TU == 2
 hipError_t launch_band_persist_ice(bool gate, bool box, const Batch& b, const Work& w, const Chunk& ch, const Opts& o,
                                    hipStream_t s, const int32_t* list, int nlist, int* variant_out) {
   constexpr int B = kBandSteps;

@@ -10,12 +10,15 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "..", "csrc")
 LIB = os.path.join(HERE, "libdervet_hip.so")
-SOURCES = ["dvh_kernels.hip", "dvh_band.hip", "dvh_band_persist.hip", "dvh_chain.hip", "dvh_build.hip", "dvh_sweep.hip", "dvh_series.hip", "dvh_route.hip", "dvh_large.hip", "dvh_outage.hip",
+SOURCES = ["dvh_kernels.hip", "dvh_band.hip", "dvh_band_persist.hip", "dvh_band_persist_ice.hip", "dvh_chain.hip", "dvh_build.hip", "dvh_sweep.hip", "dvh_series.hip", "dvh_route.hip", "dvh_large.hip", "dvh_outage.hip",
            "dvh_api.cpp", "dvh_validate.cpp"]
-# per-source flags: the band kernel's persistent form without machine-level loop-invariant code motion (its loop
-# invariants, hoisted out of the loop over windows, spilled; csrc/dvh_band_persist.hip)
-EXTRA_FLAGS = {"dvh_band_persist.hip": ["-mllvm", "-disable-machine-licm"]}
-INCLUDES = {"dvh_band_persist.hip": "dvh_band.hip"}  # (a one-line source around another: its compile time)
+# per-source flags: the band kernel's persistent forms without machine-level loop-invariant code motion (their loop
+# invariants, hoisted out of the loop over windows, spilled; csrc/dvh_band_persist.hip), the battery form with the
+# AMDGPU scheduler's register-pressure trackers (+2.1 % on the bench; the ICE form is slower with them)
+EXTRA_FLAGS = {"dvh_band_persist.hip": ["-mllvm", "-disable-machine-licm", "-mllvm", "-amdgpu-use-amdgpu-trackers=1"],
+               "dvh_band_persist_ice.hip": ["-mllvm", "-disable-machine-licm"]}
+INCLUDES = {"dvh_band_persist.hip": "dvh_band.hip",  # (a one-line source around another: its compile time)
+            "dvh_band_persist_ice.hip": "dvh_band.hip"}
 HEADERS = ["dvh_internal.h", "dvh_device.h", "dvh_validate.h", "dvh_rng.h", "dvh_ziggurat.h", os.path.join("..", "..", "include", "dervet_hip.h")]
 
 
@@ -63,7 +66,8 @@ def build(force=False, verbose=False):
     return LIB
 
 
-def build_variant(out, defines, recompile=("dvh_band.hip", "dvh_band_persist.hip"), verbose=False):
+def build_variant(out, defines, recompile=("dvh_band.hip", "dvh_band_persist.hip", "dvh_band_persist_ice.hip"),
+                  verbose=False):
     """A/B helper: the library with ``defines`` (e.g. ["-DDVH_BAND_PROBE=1"]) applied to the sources in
     ``recompile`` (their objects go to build_obj/<name>/), every other object taken from the default build."""
     build()

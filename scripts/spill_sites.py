@@ -5,7 +5,7 @@ forms depth 1 is the loop over windows (per-window set-up and write-back), depth
 depth 2 may still sit in a rarely taken branch (check iterations, restarts, the Halpern-table reload every 64
 iterations) -- the listing with --lines shows each one's block.
 
-Usage: python scripts/spill_sites.py [file.hip ...] [--lines]   (default: dvh_band_persist.hip dvh_kernels.hip)
+Usage: python scripts/spill_sites.py [file.hip ...] [--lines]   (default: dvh_band_persist.hip dvh_band_persist_ice.hip dvh_kernels.hip)
 """
 import os
 import re
@@ -49,7 +49,7 @@ def sites(lines):
 
 def main(argv):
     show = "--lines" in argv
-    files = [a for a in argv if not a.startswith("--")] or ["dvh_band_persist.hip", "dvh_kernels.hip"]
+    files = [a for a in argv if not a.startswith("--")] or ["dvh_band_persist.hip", "dvh_band_persist_ice.hip", "dvh_kernels.hip"]
     for f in files:
         p = f if os.path.exists(f) else os.path.join(CSRC, f)
         for name, found in sites(isa(p)):

@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "der-vet_amd", "csrc")
 sys.path.insert(0, os.path.join(ROOT, "der-vet_amd"))
 from dervet_hip.build import EXTRA_FLAGS  # noqa: E402  (per-source flags of the library build)
-DEFAULT = ["dvh_band.hip", "dvh_band_persist.hip", "dvh_kernels.hip", "dvh_chain.hip", "dvh_large.hip", "dvh_build.hip", "dvh_sweep.hip",
+DEFAULT = ["dvh_band.hip", "dvh_band_persist.hip", "dvh_band_persist_ice.hip", "dvh_kernels.hip", "dvh_chain.hip", "dvh_large.hip", "dvh_build.hip", "dvh_sweep.hip",
            "dvh_outage.hip"]
 
 
