@@ -16,7 +16,11 @@ SOURCES = ["dvh_kernels.hip", "dvh_band.hip", "dvh_band_persist.hip", "dvh_band_
 # invariants, hoisted out of the loop over windows, spilled; csrc/dvh_band_persist.hip), the battery form with the
 # AMDGPU scheduler's register-pressure trackers (+2.1 % on the bench; the ICE form is slower with them)
 EXTRA_FLAGS = {"dvh_band_persist.hip": ["-mllvm", "-disable-machine-licm", "-mllvm", "-amdgpu-use-amdgpu-trackers=1"],
-               "dvh_band_persist_ice.hip": ["-mllvm", "-disable-machine-licm"]}
+               "dvh_band_persist_ice.hip": ["-mllvm", "-disable-machine-licm"],
+               # the team kernel (config 3 DCM + PV 162 -> 151 ms) and the ELL / generic kernels (1,095 market days
+               # 5.35 -> 5.12 ms) without machine LICM too: profiles/r05zj_chain_kernels_flags.log
+               "dvh_chain.hip": ["-mllvm", "-disable-machine-licm"],
+               "dvh_kernels.hip": ["-mllvm", "-disable-machine-licm"]}
 INCLUDES = {"dvh_band_persist.hip": "dvh_band.hip",  # (a one-line source around another: its compile time)
             "dvh_band_persist_ice.hip": "dvh_band.hip"}
 HEADERS = ["dvh_internal.h", "dvh_device.h", "dvh_validate.h", "dvh_rng.h", "dvh_ziggurat.h", os.path.join("..", "..", "include", "dervet_hip.h")]
@@ -26,7 +30,9 @@ def _stale():
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(os.path.join(CSRC, f)) > t for f in SOURCES + HEADERS)
+    # this file too: its per-source flags change the objects
+    return os.path.getmtime(os.path.abspath(__file__)) > t or \
+        any(os.path.getmtime(os.path.join(CSRC, f)) > t for f in SOURCES + HEADERS)
 
 
 def build(force=False, verbose=False):
