@@ -1,6 +1,6 @@
 """A/B of kernels on daily market-service windows (dev helper): the three Usecase 3 golden cases (365 days each,
 DA + frequency regulation, LP relaxation of binary = 1), replicated R times.  Kernel variant from the
-environment (DVH_SMALL=-1 off, 0..5 a small-window variant; see dvh_kernels.hip small_dispatch).
+environment (DVH_SMALL=-1 off, 0..2 a small-window variant; see dvh_kernels.hip small_dispatch).
 
 Usage: DVH_SMALL=<v> python scripts/ab_market.py [R] [path]
 """
