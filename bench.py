@@ -299,6 +299,10 @@ def main():
                     help="seeded schedule: every warm window starts from the inverse-distance-weighted blend of its "
                          "BLEND nearest seeds' transferred solutions (1: the nearest seed alone)")
     ap.add_argument("--blend-power", type=float, default=1.0, help="blend weights 1 / distance^POWER")
+    ap.add_argument("--blend-lam", type=float, default=-1.0,
+                    help="> 0: blend weights moved toward the partners' affine combination that reproduces the window's "
+                         "features, regularised toward the inverse-distance weights by LAM (dervet_hip.sweep."
+                         "affine_weights); <= 0: inverse-distance weights")
     ap.add_argument("--no-cold-ref", action="store_true", help="skip the untimed all-cold reference solve")
     ap.add_argument("--kkt-predict", type=int, default=4,
                     help="dvh_options.kkt_predict for cold solves (--schedule cold and the cold reference; the seeded "
@@ -367,7 +371,8 @@ def main():
     if args.schedule == "seeded":
         P = series.parameters() if series is not None else scenarios.sweep_parameters(scen)
         sweep = SeededSweep(make, scen, P["E"], stride=args.seed_stride, features=scenarios.sweep_features(P),
-                            blend=args.blend, blend_power=args.blend_power)
+                            blend=args.blend, blend_power=args.blend_power,
+                            blend_lam=args.blend_lam if args.blend_lam > 0 else None)
         t1 = time.time()
         dev = sweep.to_device(solver, f"cuda:{local}")
         desc = sweep.desc

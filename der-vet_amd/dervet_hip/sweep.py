@@ -72,10 +72,26 @@ def standardise(features, S=None):
     return (f - f.mean(0)) / np.where(f.std(0) > 0, f.std(0), 1.0)
 
 
-def seed_partners(fr, fs, q, first=None, power=1.0):
+def affine_weights(fr, fs, idx, w0, lam):
+    """Blend weights moved from w0 toward the affine combination of the partners' features that reproduces the row's own:
+    per row, w = argmin |F'w - f|^2 + lam |w - w0|^2 subject to sum w = 1 (F: the q partners' features), in closed form
+    (a regularised barycentric interpolation; weights may be negative).  fr [R, d], fs [S, d], idx / w0 [R, q]."""
+    F = fs[idx]                                                  # [R, q, d]
+    q = idx.shape[1]
+    A = F @ np.swapaxes(F, 1, 2) + lam * np.eye(q)[None]         # [R, q, q]
+    rhs = (F @ fr[:, :, None])[:, :, 0] + lam * w0               # [R, q]
+    one = np.ones((len(idx), q))
+    sol = np.linalg.solve(A, np.stack([rhs, one], axis=2))      # [R, q, 2]
+    ai, a1 = sol[:, :, 0], sol[:, :, 1]
+    mu = (ai.sum(1) - 1.0) / a1.sum(1)
+    return ai - mu[:, None] * a1
+
+
+def seed_partners(fr, fs, q, first=None, power=1.0, lam=None):
     """The q nearest seeds of every row of fr among the rows of fs (exact squared distances, nearest first; `first`:
     the nearest already known, e.g. from ``_nearest``) and inverse-distance weights 1 / d^power summing to 1 (a seed at
-    distance 0 takes the whole weight).  Returns (idx [R, q] int64, w [R, q] float64)."""
+    distance 0 takes the whole weight); lam: the weights then moved toward the partners' affine combination that
+    reproduces the row's features (``affine_weights``).  Returns (idx [R, q] int64, w [R, q] float64)."""
     fr = np.ascontiguousarray(fr, np.float64)
     fs = np.ascontiguousarray(fs, np.float64)
     q = max(1, min(int(q), len(fs)))
@@ -109,6 +125,8 @@ def seed_partners(fr, fs, q, first=None, power=1.0):
         ww = np.where(np.isinf(inv).any(1, keepdims=True), np.isinf(inv).astype(np.float64), inv)
         w[a:a + 2048] = ww / ww.sum(1, keepdims=True)
         idx[a:a + 2048] = part
+    if lam is not None and q > 1:
+        w = affine_weights(fr, fs, idx, w, float(lam))
     return idx, w
 
 
@@ -360,7 +378,7 @@ class SeededSweep:
     windows on the GPU, lp/gpu_builder.py); keys: similarity key per scenario (same order as `scenario_ids`)."""
 
     def __init__(self, make_groups, scenario_ids, keys, stride=8, features=None, cover=False, blend=1,
-                 blend_power=1.0):
+                 blend_power=1.0, blend_lam=None):
         from .lp import builder
         ids = np.asarray(list(scenario_ids), np.int64)
         seed_i, rest_i, pick = seed_split(keys, stride, features, cover)
@@ -372,7 +390,7 @@ class SeededSweep:
         self.blend = 1
         if blend > 1 and features is not None and len(seed_i) > 1 and len(rest_i):
             f = standardise(features, len(ids))
-            idx, w = seed_partners(f[rest_i], f[seed_i], blend, first=pick, power=blend_power)
+            idx, w = seed_partners(f[rest_i], f[seed_i], blend, first=pick, power=blend_power, lam=blend_lam)
             self.blend = idx.shape[1]
             bl = (self.rest_ids, self.seed_ids[idx], w)
         sg = make_groups(self.seed_ids)

@@ -128,8 +128,11 @@ def main():
         feats = np.concatenate([feats, (wgt * (col - col.mean()) / col.std())[:, None]], axis=1)
     seeds, rest, pick = seed_split(P["E"], stride, feats)
     warm_mode = os.environ.get("LAB_WARM", "nearest")
-    if warm_mode.startswith("avg") or warm_mode.startswith("idw"):  # the q nearest seeds in standardised features
-        q = int(warm_mode[3:].split("p")[0])
+    if warm_mode.startswith("avg") or warm_mode.startswith("idw") or warm_mode.startswith("lin"):
+        # the q nearest seeds in standardised features; lin<q>l<lam>: IDW weights moved toward the affine combination
+        # that reproduces the window's own features (min |F'w - f|^2 + lam |w - w_idw|^2, sum w = 1)
+        lam = float(warm_mode.split("l")[-1]) if warm_mode.startswith("lin") else 0.0
+        q = int(warm_mode[3:].split("p")[0].split("l")[0])
         pw_ = float(warm_mode.split("p")[1]) if "p" in warm_mode[3:] else 1.0
         f = feats
         f = (f - f.mean(0)) / np.where(f.std(0) > 0, f.std(0), 1.0)
@@ -138,6 +141,14 @@ def main():
         dd = np.sqrt(np.take_along_axis(d, pick2, 1))
         wgt = np.full(dd.shape, 1.0 / q) if warm_mode.startswith("avg") else \
             (1.0 / np.maximum(dd, 1e-9) ** pw_) / (1.0 / np.maximum(dd, 1e-9) ** pw_).sum(1, keepdims=True)
+        if warm_mode.startswith("lin"):
+            one = np.ones(q)
+            for i in range(len(rest)):
+                F = f[seeds][pick2[i]]  # [q, d]
+                A = F @ F.T + lam * np.eye(q)
+                rhs = F @ f[rest[i]] + lam * wgt[i]
+                ai, a1 = np.linalg.solve(A, rhs), np.linalg.solve(A, one)
+                wgt[i] = ai - (one @ ai - 1.0) / (one @ a1) * a1
     lab = Lab()
     ref = None
     for v in variants:

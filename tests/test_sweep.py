@@ -324,3 +324,21 @@ def test_device_blend_transfer_equals_host_blend_transfer():
             w_bad = np.array([[0.5, np.nan, 0.5]])
             s._check(s._lib.dvh_warm_transfer_blend(s._h, ctypes.byref(p), bad.ctypes.data_as(ctypes.c_void_p),
                                                     w_bad.ctypes.data_as(ctypes.c_void_p), 1, 3), "blend")
+
+
+def test_affine_blend_weights_sum_to_one_and_approach_the_features():
+    """sweep.affine_weights (bench.py --blend-lam): the weights sum to 1, large lam returns the inverse-distance
+    weights, small lam reproduces the window's features from its partners' (when q > d)."""
+    from dervet_hip.sweep import affine_weights, seed_partners
+    rng = np.random.default_rng(3)
+    fs, fr = rng.normal(size=(40, 3)), rng.normal(size=(25, 3))
+    idx, w0 = seed_partners(fr, fs, 8)
+    for lam in (1e-9, 1.0, 1e9):
+        w = affine_weights(fr, fs, idx, w0, lam)
+        np.testing.assert_allclose(w.sum(1), 1.0, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(affine_weights(fr, fs, idx, w0, 1e9), w0, atol=1e-7)
+    w = affine_weights(fr, fs, idx, w0, 1e-9)
+    np.testing.assert_allclose((w[:, :, None] * fs[idx]).sum(1), fr, atol=1e-6)
+    i1, w1 = seed_partners(fr, fs, 8, lam=1.0)
+    assert np.array_equal(i1, idx)
+    np.testing.assert_allclose(w1, affine_weights(fr, fs, idx, w0, 1.0))
