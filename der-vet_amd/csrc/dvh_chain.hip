@@ -69,13 +69,15 @@ static_assert(kPMax - 1 <= kPollU - kPollC, "the window hand-out's acknowledgeme
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) int gi32;
 
-// KKT pieces of one column / one row (out of line, as in dvh_band.hip: the check runs every kkt_every * check_every
-// iterations and inlined it would raise the kernel's register allocation)
+// KKT pieces of one column / one row, out of line (DVH_CHAIN_KKT_INLINE 0, the default): the check runs every
+// kkt_every * check_every iterations.  Inlined they were 1 % faster while this unit was built with machine LICM; built
+// without it (build.py), out of line is faster: config 3 DCM + PV 148 -> 146 ms, medium annual 646 -> 618 ms
+// (profiles/r05zz_chain_kkt_outofline.log)
 struct ColKktC {
   double rd2, cx, bt, rdx;
 };
 #ifndef DVH_CHAIN_KKT_INLINE
-#define DVH_CHAIN_KKT_INLINE 1
+#define DVH_CHAIN_KKT_INLINE 0
 #endif
 #if DVH_CHAIN_KKT_INLINE
 #define DVH_CHAIN_KKT_FN __forceinline__
