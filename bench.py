@@ -138,7 +138,7 @@ def roofline_object(alg, pdhg_s, prof, kname, launches, copy_gbps):
 
 # the full-population certification of the bench kernel: every one of the 120,000 windows, seeded and cold, re-solved
 # by HiGHS on the host (scripts/certify_dump.py + scripts/certify_highs.py)
-CERTIFICATION = ("profiles/r05z4_certify.json (all 120,000 windows vs HiGHS, seeded with blended warm starts and cold; "
+CERTIFICATION = ("profiles/r05z5_certify.json (all 120,000 windows vs HiGHS, seeded with blended warm starts and cold; "
                  "final round-5 library: box steps rescaled at restarts, KKT helpers inlined, scheduler options)")
 
 
