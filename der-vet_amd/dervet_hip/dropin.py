@@ -39,8 +39,16 @@ saved results (battery degradation, Battery.py:87-110; sizing, MicrogridScenario
 own windows; ``batched_cases_loop`` batches them ACROSS scenarios instead: window k of every case in one GPU
 call, saved before any case sets up window k + 1 (the serial case loop of dervet/DERVET.py:75-83, in lockstep).
 ``DERVET.solve`` hard-codes ``MicrogridScenario`` (dervet/DERVET.py:76), so ``install`` patches that name with
-the batched subclass.
+the batched subclass; ``install(batch_cases=True)`` also replaces ``DERVET.solve`` (DERVET.py:72-90) so that the
+windows of every sensitivity case reach the GPU in one batch (``make_batched_dervet_solve``).
+
+Every window is saved with the state its own set-up left: the active-DER list ``poi.grab_active_ders`` chose for
+its year (MicrogridScenario.py:342, MicrogridPOI.py:85-91) and its DERs' ``variables_dict``, restored before the
+save and before an in-place reference solve (the reference saves each window right after setting it up).
 """
+import collections
+import time
+
 from . import _lib
 from .export import ExportError, ecos_to_window
 from .solver import BatchSolver
@@ -144,25 +152,48 @@ def _preamble(scenario):
     return alpha, sa.post_facto_reliability_only()
 
 
+WindowPlan = collections.namedtuple(
+    "WindowPlan", "opt_period sub_index functions constraints saved_vars win active_ders")
+WindowPlan.__doc__ = """One window between its set-up and its save: what ``set_up_optimization`` returned, the
+variables_dict of each active DER (re-created per window), the export (None: reference solve) and the window's own
+active-DER list (``poi.grab_active_ders(sub_index)``, MicrogridScenario.py:342 / MicrogridPOI.py:85-91)."""
+
+
 def _setup_export(scenario, opt_period, alpha, ignore, exporter):
     """set_up_optimization of one window + its export; None for a window with nothing to optimize (:316-318)."""
     functions, constraints, sub_index = scenario.set_up_optimization(opt_period, annuity_scalar=alpha,
                                                                      ignore_der_costs=ignore)
     if not len(constraints) and not len(functions.values()):
         return None
-    saved_vars = {der: getattr(der, "variables_dict", None) for der in getattr(scenario.poi, "active_ders", [])}
-    return (opt_period, sub_index, functions, constraints, saved_vars, exporter.export(functions, constraints))
+    active = getattr(scenario.poi, "active_ders", None)
+    active = None if active is None else list(active)
+    saved_vars = {der: getattr(der, "variables_dict", None) for der in (active or [])}
+    return WindowPlan(opt_period, sub_index, functions, constraints, saved_vars,
+                      exporter.export(functions, constraints), active)
+
+
+def _restore_window_state(scenario, plan):
+    """Put back what this window's set-up left on the scenario before anything of the reference reads it: the
+    window's active-DER list (the save iterates ``poi.active_ders``, MicrogridScenario.py:361 and storagevet's save
+    through ``super()`` at :360; a DER not operational in this window's year -- construction year, end of life --
+    must not be saved, DERExtension.py:116-125) and each of those DERs' ``variables_dict``.  The reference loop
+    saves each window right after its set-up, so this is the state its save sees."""
+    if plan.active_ders is not None:
+        scenario.poi.active_ders = list(plan.active_ders)
+    for der, vd in plan.saved_vars.items():
+        if vd is not None:
+            der.variables_dict = vd
 
 
 def _solve_plans(plans, solver):
     """One batched solve over the LP windows of `plans` (list of plan tuples); returns {index: WindowResult}."""
-    lp_idx = [i for i, p in enumerate(plans) if p[5] is not None]
+    lp_idx = [i for i, p in enumerate(plans) if p.win is not None]
     if not lp_idx:
         return {}
     own = solver is None
     solver = solver or BatchSolver(0)
     try:
-        res = solver.solve([plans[i][5].lp for i in lp_idx])
+        res = solver.solve([plans[i].win.lp for i in lp_idx])
     finally:
         if own:
             solver.close()
@@ -170,10 +201,8 @@ def _solve_plans(plans, solver):
 
 
 def _save(scenario, plan, r, report, retry_failed=True):
-    opt_period, sub_index, functions, constraints, saved_vars, win = plan
-    for der, vd in saved_vars.items():
-        if vd is not None:
-            der.variables_dict = vd
+    opt_period, sub_index, functions, constraints, _, win, _ = plan
+    _restore_window_state(scenario, plan)  # before the in-place reference solves too
     if win is None:  # MILP / non-LP window: the reference solve, in place
         prob, obj, err = scenario.solve_optimization(functions, constraints)
         report.reference += 1
@@ -272,14 +301,15 @@ def batched_cases_loop(scenarios, solver=None, exporter=None, relax_milp=False, 
             solver.close()
 
 
-def make_batched_scenario_class(base, solver_factory=None, relax_milp=False, retry_failed=True):
+def make_batched_scenario_class(base, solver_factory=None, relax_milp=False, retry_failed=True, exporter_factory=None):
     """Subclass of the reference ``MicrogridScenario`` whose window loop is batched on the GPU."""
 
     class BatchedMicrogridScenario(base):
         def optimize_problem_loop(self, **kwargs):
             solver = solver_factory() if solver_factory else None
+            exporter = exporter_factory() if exporter_factory else None
             try:
-                return batched_optimize_problem_loop(self, solver=solver, relax_milp=relax_milp,
+                return batched_optimize_problem_loop(self, solver=solver, exporter=exporter, relax_milp=relax_milp,
                                                      retry_failed=retry_failed, **kwargs)
             finally:
                 if solver is not None:
@@ -290,17 +320,85 @@ def make_batched_scenario_class(base, solver_factory=None, relax_milp=False, ret
     return BatchedMicrogridScenario
 
 
-def install(dervet_module=None, relax_milp=False, retry_failed=True, solver_factory=None):
+def make_batched_dervet_solve(dervet_module, solver_factory=None, relax_milp=False, retry_failed=True,
+                              case_batch=None, exporter_factory=None):
+    """``DERVET.solve`` (dervet/DERVET.py:72-90) with every case's windows in one batched solve.
+
+    The reference runs its cases one after the other -- preamble, ``optimize_problem_loop``, ``add_instance`` --
+    so the GPU would see one case's 12-36 windows per call (DERVET.py:75-83).  This version runs each case's
+    unchanged preamble (``MicrogridScenario(value)``, ``set_up_poi_and_service_aggregator``, ``initialize_cba``,
+    ``fill_and_drop_extra_data``, ``sizing_module``: :76-80), then ``batched_cases_loop`` over the cases
+    (independent cases: every window of every case in one solve; degradation / sizing-coupled cases in lockstep by
+    window position), then ``MicrogridResult.add_instance(key, run)`` in the reference's key order and
+    ``sensitivity_summary()`` (:83-85).  ``case_batch`` bounds how many cases are held at once (None: all); the
+    scenarios of one batch are alive together, which is the memory this costs over the serial loop.  A case's
+    results are handed to ``add_instance`` after the batch is solved instead of right after its own loop; each
+    ``MicrogridResult`` instance is built from its own scenario object, so what it reads is the same."""
+    mod = dervet_module
+
+    def solve(self):
+        starts = time.time()
+        keys = list(self.cases.keys())
+        step = len(keys) if not case_batch else int(case_batch)
+        for lo in range(0, len(keys), max(step, 1)):
+            chunk = keys[lo:lo + max(step, 1)]
+            runs = []
+            for key in chunk:
+                run = mod.MicrogridScenario(self.cases[key])
+                run.set_up_poi_and_service_aggregator()
+                run.initialize_cba()
+                run.fill_and_drop_extra_data()
+                run.sizing_module()
+                runs.append(run)
+            solver = solver_factory() if solver_factory else None
+            exporter = exporter_factory() if exporter_factory else None
+            try:
+                batched_cases_loop(runs, solver=solver, exporter=exporter, relax_milp=relax_milp,
+                                   retry_failed=retry_failed)
+            finally:
+                if solver is not None:
+                    solver.close()
+            for key, run in zip(chunk, runs):
+                mod.MicrogridResult.add_instance(key, run)
+        mod.MicrogridResult.sensitivity_summary()
+        tell = getattr(mod, "TellUser", None)
+        if tell is not None:
+            tell.info(f"DERVET runtime: {time.time() - starts}")
+        return mod.MicrogridResult
+
+    solve.dervet_hip_batched = True
+    return solve
+
+
+def install(dervet_module=None, relax_milp=False, retry_failed=True, solver_factory=None, batch_cases=False,
+            case_batch=None, exporter_factory=None):
     """Patch dervet.DERVET.MicrogridScenario (hard-coded at dervet/DERVET.py:76) with the batched class.
     ``relax_milp``: the user's opt-in to GPU LP relaxations of binary = 1 windows (north_star); off, MILP windows stay
-    on the reference solve.  ``retry_failed``: re-solve windows without a certified GPU optimum by the reference."""
+    on the reference solve.  ``retry_failed``: re-solve windows without a certified GPU optimum by the reference.
+    ``batch_cases``: also patch ``DERVET.solve`` (DERVET.py:72-90) so that every case's windows go to the GPU
+    together (``make_batched_dervet_solve``; ``case_batch`` cases at a time); off, the reference's serial case loop
+    is kept (and a previous ``batch_cases`` install is undone)."""
     if dervet_module is None:
         import dervet.DERVET as dervet_module  # noqa: N813
     base = dervet_module.MicrogridScenario
     if getattr(base, "__name__", "") == "BatchedMicrogridScenario":
         if base.dervet_hip_options == (solver_factory, bool(relax_milp), bool(retry_failed)):
-            return base
-        base = base.__bases__[0]  # re-install with the new options over the reference class
-    cls = make_batched_scenario_class(base, solver_factory, relax_milp, retry_failed)
-    dervet_module.MicrogridScenario = cls
+            cls = base
+        else:
+            base = base.__bases__[0]  # re-install with the new options over the reference class
+            cls = None
+    else:
+        cls = None
+    if cls is None:
+        cls = make_batched_scenario_class(base, solver_factory, relax_milp, retry_failed, exporter_factory)
+        dervet_module.MicrogridScenario = cls
+    driver = getattr(dervet_module, "DERVET", None)
+    if driver is not None:
+        if not hasattr(driver, "_dervet_hip_reference_solve"):
+            driver._dervet_hip_reference_solve = driver.solve
+        if batch_cases:
+            driver.solve = make_batched_dervet_solve(dervet_module, solver_factory, relax_milp, retry_failed,
+                                                     case_batch, exporter_factory)
+        else:
+            driver.solve = driver._dervet_hip_reference_solve
     return cls

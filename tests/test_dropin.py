@@ -116,6 +116,9 @@ class CpuStandInSolver:
         self.calls.append(len(lps))
         return [_highs(lp) for lp in lps]
 
+    def close(self):
+        pass
+
 
 def test_batched_loop_orders_saves_and_repoints_variables():
     sc = FakeScenario(n_windows=6, empty={2})
@@ -332,3 +335,214 @@ def test_cvxpy_exporter_requires_cvxpy():
     except ImportError:
         with pytest.raises(ImportError):
             dropin.CvxpyExporter()
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# each window is saved with its own active-DER set; cases batched behind DERVET.solve
+# ---------------------------------------------------------------------------------------------------------------
+
+class YearDER(FakeDER):
+    """A DER with an operational window (DERExtension.operational, DERExtension.py:116-125)."""
+
+    def __init__(self, name, years):
+        super().__init__(name)
+        self.years = set(years)
+
+    def operational(self, year):
+        return year in self.years
+
+
+class YearScenario(FakeScenario):
+    """Windows spread over opt years; set_up_optimization runs ``poi.grab_active_ders`` on the window's year as
+    MicrogridScenario.set_up_optimization does (:342, MicrogridPOI.py:85-91).  A DER that is not operational in the
+    window's year is dropped from ``poi.active_ders``; the save records the active set it sees, and so does the
+    in-place reference solve."""
+
+    def __init__(self, years=(2017, 2017, 2018, 2018, 2019), value=None, journal=None, scen=0, milp=(), **kw):
+        value = dict(value or {})
+        years = value.pop("years", years)
+        scen = value.pop("scen", scen)
+        super().__init__(n_windows=len(years), scen=scen, journal=journal, **kw)
+        self.years = list(years)
+        self.ders = [YearDER("es", {2017, 2018, 2019}), YearDER("pv", {2017, 2019}), YearDER("ice", {2018})]
+        self.poi = types.SimpleNamespace(der_list=self.ders, active_ders=list(self.ders),
+                                         is_sizing_optimization=False,
+                                         grab_active_ders=self._grab)
+        self.milp_windows = set(milp)
+        self.solve_active = []
+        self.value = value
+
+    def _grab(self, year):
+        self.poi.active_ders = [d for d in self.poi.der_list if d.operational(year)]
+
+    def set_up_optimization(self, opt_period, annuity_scalar=1, ignore_der_costs=False):
+        self.log.append(("setup", int(opt_period)))
+        self.journal.append((self.scen, "setup", int(opt_period)))
+        self.poi.grab_active_ders(self.years[opt_period])
+        for der in self.poi.active_ders:
+            der.variables_dict = {"window": int(opt_period), "der": der.name}
+        return {"lp": self.lps[opt_period]}, ["c"], opt_period
+
+    def solve_optimization(self, functions, constraints):
+        self.solve_active.append([d.name for d in self.poi.active_ders])
+        return super().solve_optimization(functions, constraints)
+
+    def save_optimization_results(self, opt_window_num, sub_index, prob, obj_expression, cvx_error_msg):
+        self.log.append(("save", int(opt_window_num)))
+        self.journal.append((self.scen, "save", int(opt_window_num)))
+        seen = [(d.name, dict(d.variables_dict)) for d in self.poi.active_ders]
+        self.saved.append((int(opt_window_num), prob, cvx_error_msg, seen))
+
+    # the reference's per-case preamble (DERVET.py:76-80) and serial loop (MicrogridScenario.py:281-320)
+    def set_up_poi_and_service_aggregator(self):
+        self.journal.append((self.scen, "preamble", 0))
+
+    def initialize_cba(self):
+        pass
+
+    def fill_and_drop_extra_data(self):
+        pass
+
+    def sizing_module(self):
+        pass
+
+    def optimize_problem_loop(self, **kwargs):
+        self.system_requirements = self.service_agg.identify_system_requirements(self.poi.der_list, self.opt_years,
+                                                                                 self.frequency)
+        for w in self.optimization_levels.predictive.unique():
+            functions, constraints, sub_index = self.set_up_optimization(w)
+            prob, obj, err = self.solve_optimization(functions, constraints)
+            self.save_optimization_results(w, sub_index, prob, obj, err)
+
+
+def _expected_active(years, w):
+    y = years[w]
+    return [n for n, ys in (("es", {2017, 2018, 2019}), ("pv", {2017, 2019}), ("ice", {2018})) if y in ys]
+
+
+def _saved_record(sc):
+    return [(w, prob.status, round(float(prob.value), 6), err, seen) for w, prob, err, seen in sc.saved]
+
+
+@pytest.mark.parametrize("path", ["gpu", "milp", "retried"])
+def test_each_window_is_saved_with_its_own_active_ders(path):
+    """A DER not operational in opt year 2 (and one operational only there): every saved window -- GPU-solved,
+    MILP fallback or re-solved after a failed GPU verdict -- sees exactly the active set its own set-up chose,
+    with that window's variables_dict, as in the reference loop where each save follows its own set-up."""
+    sc = YearScenario()
+    milp = [sc.lps[w] for w in (1, 2)] if path == "milp" else []
+
+    class Failing(CpuStandInSolver):
+        def solve(self, lps):
+            out = super().solve(lps)
+            for r in out[1:3]:
+                r.status = 3  # ITER_LIMIT
+            return out
+
+    solver = Failing() if path == "retried" else CpuStandInSolver()
+    dropin.batched_optimize_problem_loop(sc, solver=solver, exporter=FakeExporter(milp))
+    assert [w for w, *_ in sc.saved] == list(range(5))
+    for w, prob, err, seen in sc.saved:
+        assert [n for n, _ in seen] == _expected_active(sc.years, w), (path, w, seen)
+        assert all(vd == {"window": w, "der": n} for n, vd in seen), (path, w, seen)
+    if path != "gpu":  # the in-place reference solves of windows 1 and 2 ran with their own sets too
+        assert sc.solve_active == [_expected_active(sc.years, w) for w in (1, 2)]
+    # identical to the serial reference loop's saves
+    ref = YearScenario()
+    ref.optimize_problem_loop()
+    assert _saved_record(sc) == _saved_record(ref)
+
+
+def test_cases_loop_restores_active_ders_in_coupled_lockstep():
+    cases_ = [YearScenario(scen=0), YearScenario(scen=1, degrade=True, years=(2017, 2018, 2019))]
+    for c in cases_:
+        c.ders[0].incl_cycle_degrade = c.scen == 1
+    dropin.batched_cases_loop(cases_, solver=CpuStandInSolver(), exporter=FakeExporter([]))
+    for c in cases_:
+        for w, prob, err, seen in c.saved:
+            assert [n for n, _ in seen] == _expected_active(c.years, w)
+
+
+class FakeResultRegistry:
+    """MicrogridResult's class-level registry as DERVET.solve uses it (DERVET.py:83-85)."""
+    records = []
+
+    @classmethod
+    def add_instance(cls, key, run):
+        cls.records.append(("instance", key, _saved_record(run)))
+
+    @classmethod
+    def sensitivity_summary(cls):
+        cls.records.append(("summary",))
+
+
+class FakeDERVET:
+    """The reference driver's solve (dervet/DERVET.py:72-90) over fake cases."""
+
+    def __init__(self, cases_):
+        self.cases = cases_
+
+    def solve(self):
+        for key, value in self.cases.items():
+            run = fake_dervet_module.MicrogridScenario(value)
+            run.set_up_poi_and_service_aggregator()
+            run.initialize_cba()
+            run.fill_and_drop_extra_data()
+            run.sizing_module()
+            run.optimize_problem_loop()
+            fake_dervet_module.MicrogridResult.add_instance(key, run)
+        fake_dervet_module.MicrogridResult.sensitivity_summary()
+        return fake_dervet_module.MicrogridResult
+
+
+fake_dervet_module = types.SimpleNamespace()
+
+
+class CaseScenario(YearScenario):
+    """MicrogridScenario(value) as DERVET.solve constructs it (DERVET.py:76)."""
+
+    def __init__(self, value):
+        super().__init__(value=value)
+
+
+def _fake_cases():
+    return {"case a": {"years": (2017, 2018, 2019), "scen": 0},
+            "case b": {"years": (2018, 2018), "scen": 1},
+            "case c": {"years": (2019, 2017, 2018, 2017), "scen": 2}}
+
+
+@pytest.mark.parametrize("case_batch", [None, 2])
+def test_install_batch_cases_saves_what_the_serial_case_loop_saves(case_batch):
+    """install(batch_cases=True) patches DERVET.solve: every case's preamble, one batched solve over all their
+    windows, add_instance in key order, sensitivity_summary -- and each case is saved exactly as the reference's
+    serial case loop saves it, in the same order."""
+    def fresh_module():
+        fake_dervet_module.MicrogridScenario = CaseScenario
+        fake_dervet_module.MicrogridResult = FakeResultRegistry
+        fake_dervet_module.DERVET = type("DERVET", (FakeDERVET,), {})
+        FakeResultRegistry.records = []
+        return fake_dervet_module
+
+    mod = fresh_module()
+    mod.DERVET(_fake_cases()).solve()                      # the reference's serial case loop
+    serial = list(FakeResultRegistry.records)
+
+    mod = fresh_module()
+    calls = []
+
+    class Counting(CpuStandInSolver):
+        def solve(self, lps):
+            calls.append(len(lps))
+            return super().solve(lps)
+
+    dropin.install(mod, batch_cases=True, case_batch=case_batch, solver_factory=Counting,
+                   exporter_factory=lambda: FakeExporter([]))
+    assert getattr(mod.DERVET.solve, "dervet_hip_batched", False)
+    mod.DERVET(_fake_cases()).solve()
+    batched = list(FakeResultRegistry.records)
+    assert [r[:2] for r in batched] == [r[:2] for r in serial]
+    assert batched == serial
+    assert calls == ([9] if case_batch is None else [5, 4])  # all 9 windows in one batch (or 2 + 1 cases)
+    # re-installing without batch_cases restores the reference's solve
+    dropin.install(mod, solver_factory=Counting)
+    assert not getattr(mod.DERVET.solve, "dervet_hip_batched", False)

@@ -111,3 +111,88 @@ def test_relaxed_milp_market_days_through_the_exporter(name):
             1 + np.linalg.norm(np.concatenate([b, h])))
         assert pres <= 1e-6, (name, d, pres)
     print(f"{name}: {len(days)} relaxed days, worst objective rel err {worst:.2e}")
+
+
+def test_two_cases_batched_through_dervet_solve_on_the_gpu():
+    """DERVET.solve patched by install(batch_cases=True) -- two cases (the es and es+pv+dg golden
+    years) set up by their preambles, all 24 exported windows in ONE solve on the band kernel, saved per case in the
+    reference order through the ECOS inversion, add_instance in key order.  Each case's DER set changes in its last
+    window (a DER not operational that year): the save sees the window's own set."""
+    import types
+
+    import pandas as pd
+
+    class Exporter:
+        def export(self, functions, constraints):
+            data, col, ew, _ = functions["w"]
+            return dropin.CvxpyWindow(ew, ecos_forms.FakeProblem(data, col))
+
+    class DER:
+        def __init__(self, name, last):
+            self.name, self.last, self.variables_dict = name, last, None
+
+        def operational(self, w):
+            return w <= self.last
+
+    class Case:
+        def __init__(self, value):
+            self.name = value
+            self.ws = _windows(value)
+            n = len(self.ws)
+            self.ders = [DER("es", n), DER("pv", n - 2)]
+            self.optimization_levels = pd.DataFrame({"predictive": np.arange(n)})
+            self.poi = types.SimpleNamespace(der_list=self.ders, active_ders=list(self.ders),
+                                             is_sizing_optimization=False)
+            self.service_agg = types.SimpleNamespace(
+                identify_system_requirements=lambda *a: {}, post_facto_reliability_only=lambda: False,
+                post_facto_reliability_only_and_user_defined_constraints=lambda: False, value_streams={})
+            self.opt_years, self.frequency, self.opt_engine, self.saved = [2017], "1h", True, []
+
+        set_up_poi_and_service_aggregator = initialize_cba = fill_and_drop_extra_data = sizing_module = \
+            lambda self: None
+
+        def set_up_optimization(self, w, annuity_scalar=1, ignore_der_costs=False):
+            self.poi.active_ders = [d for d in self.ders if d.operational(w)]
+            for d in self.poi.active_ders:
+                d.variables_dict = {"window": w}
+            return {"w": self.ws[w]}, ["c"], w
+
+        def save_optimization_results(self, w, si, prob, obj, err):
+            self.saved.append((w, prob.status, prob.value, err,
+                               [(d.name, d.variables_dict["window"]) for d in self.poi.active_ders]))
+
+    added = []
+    calls = []
+
+    class Registry:
+        @staticmethod
+        def add_instance(key, run):
+            added.append((key, run))
+
+        @staticmethod
+        def sensitivity_summary():
+            added.append(("summary", None))
+
+    class Solver(BatchSolver):
+        def solve(self, lps):
+            calls.append(len(lps))
+            out = super().solve(lps)
+            calls.append(self.kernel_stats()["band_windows"])
+            return out
+
+    class Driver:
+        def __init__(self, cases_):
+            self.cases = cases_
+
+    mod = types.SimpleNamespace(MicrogridScenario=Case, MicrogridResult=Registry, DERVET=Driver)
+    Driver.solve = lambda self: None
+    dropin.install(mod, batch_cases=True, solver_factory=lambda: Solver(0), exporter_factory=Exporter)
+    mod.DERVET({"a": "es", "b": "es+pv+dg"}).solve()
+    assert calls == [24, 24]
+    assert [k for k, _ in added] == ["a", "b", "summary"]
+    for key, run in added[:2]:
+        n = len(run.ws)
+        assert [s[0] for s in run.saved] == list(range(n))
+        for (w, status, value, err, seen), (_, _, _, gold) in zip(run.saved, run.ws):
+            assert status == "optimal" and err is None and abs(value - gold) <= 1e-5 * abs(gold)
+            assert seen == [(d.name, w) for d in run.ders if d.operational(w)]
