@@ -53,14 +53,24 @@ def alg_bytes_per_iter(desc):
 FP64_PEAK_TFLOPS = 256 * 4 * 16 * 2 * 2.4e9 / 1e12
 
 
-def source_key():
-    """Hash of the kernel sources: PMC profiles under profiles/ are used only for the kernels they measured."""
+@functools.lru_cache(maxsize=None)
+def source_key(config=None):
+    """Hash of what decides the kernels' machine code -- the sources (csrc/, the public header) AND the build
+    configuration (dervet_hip/build.py FLAGS + per-source EXTRA_FLAGS, and the hipcc / clang version): PMC profiles
+    under profiles/ are used only for the kernels they measured, so a flag-only change nulls the roofline until it
+    is re-profiled.  ``config`` (a JSON string) overrides the build configuration (tests)."""
     import hashlib
     h = hashlib.sha1()
     csrc = os.path.join(ROOT, "der-vet_amd", "csrc")
     for f in sorted(os.listdir(csrc)):
         with open(os.path.join(csrc, f), "rb") as fh:
             h.update(f.encode() + fh.read())
+    with open(os.path.join(ROOT, "include", "dervet_hip.h"), "rb") as fh:
+        h.update(b"include/dervet_hip.h" + fh.read())
+    if config is None:
+        from dervet_hip import build as _build
+        config = json.dumps(_build.build_config(), sort_keys=True)
+    h.update(config.encode())
     return h.hexdigest()[:12]
 
 
@@ -427,6 +437,18 @@ def main():
             raise SystemExit(f"bench.py: unequal windows per rank {per_rank} under weak scaling")
 
     pending = None  # the previous step's all-gather, still in flight (--overlap-gather)
+    # the all-gather through the library's own RCCL communicator (dvh_comm_init / dvh_gather_results; torch.distributed
+    # only carries the unique id); DVH_GATHER=torch keeps torch.distributed's, and gloo rehearsals always use it
+    lib_gather = None
+    if dist is not None and backend == "nccl" and os.environ.get("DVH_GATHER", "library") == "library":
+        lib_gather = parallel.LibraryGather.from_torch(solver)
+    if dist is not None:
+        gather["impl"] = "libdervet_hip dvh_gather_results (RCCL)" if lib_gather else f"torch.distributed ({backend})"
+
+    def all_gather(rows, async_op):
+        if lib_gather is not None:
+            return lib_gather.gather(rows, async_op=async_op)
+        return parallel.gather_rows(rows, counts=[count] * world, async_op=async_op)
 
     def step():
         nonlocal gathered, pending
@@ -448,9 +470,9 @@ def main():
                 if pending is not None:
                     gathered = pending.wait()
                 gather.update(wait_ms=round(1e3 * (time.perf_counter() - tw), 2))
-                pending = parallel.gather_rows(rows, counts=[count] * world, async_op=True)
+                pending = all_gather(rows, True)
             else:
-                gathered = parallel.gather_rows(rows, counts=[count] * world)
+                gathered = all_gather(rows, False)
                 torch.cuda.synchronize()
             gather.update(ms=round(1e3 * (time.perf_counter() - tg), 2), bytes_per_rank=int(rows.numel() * 8),
                           bytes_total=int(rows.numel() * 8 * world), cols=int(rows.shape[1]), tmax=int(tmax),

@@ -95,6 +95,7 @@ struct dvh_handle {
   // host-buffer batch is split into contiguous, cost-balanced ranges, one per device, solved concurrently (one host
   // thread per device, no inter-device traffic), results written straight into the caller's buffers.
   std::vector<dvh_handle*> peers;
+  dvh::Comm* comm = nullptr;  // dvh_comm_init: the result all-gather's RCCL communicator (dvh_comm.cpp)
 };
 
 // Every host wait on a solve's stream goes through here (dvh_last_host_syncs reports the count of the last solve).
@@ -253,12 +254,50 @@ int dvh_destroy(dvh_handle* h) {
       if (e) hipEventDestroy(e);
   h->chunk_events.clear();
   if (h->large) dvh::large_destroy(h->large);
+  if (h->comm) dvh::comm_destroy(h->comm);
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;
   return DVH_OK;
 }
 
 const char* dvh_last_error(const dvh_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
+// ---- the result all-gather across ranks (dvh_comm.cpp)
+int dvh_comm_unique_id(dvh_handle* h, uint8_t* id) {
+  if (!h || !id) return DVH_ERR_ARG;
+  return dvh::comm_unique_id(id, &h->err);
+}
+
+int dvh_comm_init(dvh_handle* h, int32_t rank, int32_t world, const uint8_t* id) {
+  if (!h || !id || world < 1 || rank < 0 || rank >= world) return fail(h, DVH_ERR_ARG, "dvh_comm_init: rank / world");
+  if (!h->peers.empty())
+    return fail(h, DVH_ERR_ARG, "dvh_comm_init: one communicator rank per device; this handle spans several");
+  if (h->comm) return fail(h, DVH_ERR_ARG, "dvh_comm_init: the handle already has a communicator");
+  return dvh::comm_init(h->device, rank, world, id, &h->comm, &h->err);
+}
+
+int dvh_comm_info(const dvh_handle* h, int32_t* rank_world) {
+  if (!h || !rank_world) return DVH_ERR_ARG;
+  if (!h->comm) {
+    rank_world[0] = 0;
+    rank_world[1] = 0;
+    return DVH_OK;
+  }
+  int r = 0, w = 0;
+  dvh::comm_info(h->comm, &r, &w);
+  rank_world[0] = r;
+  rank_world[1] = w;
+  return DVH_OK;
+}
+
+int dvh_gather_results(dvh_handle* h, const void* rows, uint64_t bytes_per_rank, void* out, void* stream) {
+  if (!h || !rows || !out) return DVH_ERR_ARG;
+  if (!h->comm) return fail(h, DVH_ERR_ARG, "dvh_gather_results: no communicator (dvh_comm_init)");
+  if (bytes_per_rank == 0) return DVH_OK;
+  hipSetDevice(h->device);
+  hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+  return dvh::comm_all_gather(h->comm, rows, out, (size_t)bytes_per_rank, s, &h->err);
+}
 const char* dvh_last_warning(const dvh_handle* h) { return h ? h->warn.c_str() : "null handle"; }
 
 int dvh_warm_transfer_blend(dvh_handle* h, const dvh_packed* b, const int32_t* rows, const double* weights,

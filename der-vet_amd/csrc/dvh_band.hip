@@ -179,6 +179,44 @@ constexpr int kNeedsPlain = -3;
 #define DVH_BAND_RSTEP 1
 #endif
 constexpr bool kBoxRescale = DVH_BAND_RSTEP != 0;
+// kNoWidths (round 6, box form): the columns' widths are not kept in the window's workspace -- the steps are formed
+// from the registers at set-up, the restarts rescale them (kBoxRescale), and the write-back recomputes w = u / d - l / d
+// with the operations of the set-up (bit-identical): one write and one read of 8 bytes per column less per window.
+#ifndef DVH_BAND_NOWIDTHS
+#define DVH_BAND_NOWIDTHS 1
+#endif
+constexpr bool kNoWidths = kBoxRescale && DVH_BAND_NOWIDTHS != 0;
+// DVH_BAND_F32F (A/B, off): the Ruiz / Pock-Chambolle factors rounded to single precision once, when the scaling passes
+// end (1: the outputs unscaled from the single-precision copy, which is then the factor exactly, and the factors no
+// longer written in double; -1: rounded only).  Measured and not kept (profiles/r06b_t2_rounded_factors.log): the
+// degenerate two-step window of tests/test_gpu_configs.py::test_band_kernel_forms_agree[2] (two demand periods of one
+// step each) converges in 10,496 / 3,968 iterations (three-step / one-step form) with the exact factors and not at all
+// (20,000) with the rounded ones -- a 1e-8 change of the preconditioner moves PDHG's path on that window that much.
+#ifndef DVH_BAND_F32F
+#define DVH_BAND_F32F 0
+#endif
+constexpr bool kF32Factors = DVH_BAND_F32F > 0;
+constexpr bool kF32Round = kF32Factors || DVH_BAND_F32F == -1;
+// kHalpernDiv (round 6): the 64 Halpern weights 1 / (k + 2) of the next block of iterations are divided in the lanes
+// (one correctly rounded quotient per lane: the table's values, bit for bit) instead of loaded from the global table.
+// The load sat on the restart path: a restart resets k to 0 and the very next iteration reads weight 0, so every
+// restart waited for a global load (and the table pointer was one of the values the persistent loop spilled).
+#ifndef DVH_BAND_HDIV
+#define DVH_BAND_HDIV 1
+#endif
+constexpr bool kHalpernDiv = DVH_BAND_HDIV != 0;
+// DVH_BAND_PRIO (A/B): wave 0, whose primal half-step carries the tau column's reduction and update, raises its issue
+// priority (s_setprio) until the first barrier, so that the SIMD it shares with the other window's wave issues its
+// instructions first.
+#ifndef DVH_BAND_PRIO
+#define DVH_BAND_PRIO 0
+#endif
+// DVH_BAND_EARLY_SOE (A/B): the waves other than wave 0 update the SOE rows of their lanes' first S - 1 steps in the
+// primal half-step, before the first barrier (those rows need only the lane's own columns), instead of after it: the
+// work fills their wait for wave 0 and shortens the dual half-step that follows.
+#ifndef DVH_BAND_EARLY_SOE
+#define DVH_BAND_EARLY_SOE 0
+#endif
 // DVH_BAND_PROBE (A/B builds only, scripts/probe_band_latency.py): every wave accumulates the shader-clock cycles of
 // its iterations' four segments -- primal half-step, wait at the first barrier, dual half-step, wait at the second --
 // and of the checks, and lane 0 writes them over x[6 wid .. 6 wid + 4] of its window at the end, with the wave's
@@ -262,8 +300,11 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
   const double* lraw = b.l + W.on;
   const double* uraw = b.u + W.on;
   const double* qraw = b.q + W.om;
-  double* dcv = w.dc + W.wn;  // the factors this kernel computes (outputs are unscaled with them)
+  double* dcv = w.dc + W.wn;  // the factors this kernel computes (outputs are unscaled with them; !kF32Factors)
   double* drv = w.dr + W.wm;
+  // the factor of column j / row i at the write-back: the single-precision copy is the factor itself (kF32Factors)
+  auto dcf = [&](int j) -> double { return kF32Factors ? (double)w.fc[W.wn + j] : dcv[j]; };
+  auto drf = [&](int i) -> double { return kF32Factors ? (double)w.fr[W.wm + i] : drv[i]; };
   double* xo_g = b.x + W.on;
   double* yo_g = b.y + W.om;
 
@@ -564,6 +605,17 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
   {  // the KKT checks unscale with single-precision copies of the factors: a window whose factors leave
      // [2^-100, 2^100] (far inside float's normal range) goes to the ELL / generic path, which keeps them in double
     auto oor = [](double f) { return !(f >= 0x1p-100 && f <= 0x1p100); };
+    if constexpr (kF32Round) {  // (round 6) every factor rounded to single precision once, here: the float copy in
+                                  // the workspace is then the factor itself, exactly
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+#pragma unroll
+        for (int v = 0; v < NC; ++v) fcv[s][v] = (double)(float)fcv[s][v];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) frv[s][r] = (double)(float)frv[s][r];
+      }
+      fsp = (double)(float)fsp;
+    }
     bool out = oor(fsp);
 #pragma unroll
     for (int s = 0; s < S; ++s) {
@@ -631,7 +683,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
       x[s][v] = xa[s][v] = fmin(fmax(o.warm ? xo_g[j] / d : 0.0, lsj), usj);
       nrm[0] += csj * csj;
       nrm[2] += cj * cj;
-      dcv[j] = d;
+      if constexpr (!kF32Factors) dcv[j] = d;
       w.fc[W.wn + j] = (float)d;
     }
 #pragma unroll
@@ -655,7 +707,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
       if (o.warm) y[s][r] = ya[s][r] = r == 0 ? yo_g[i] / d : fmax(yo_g[i] / d, 0.0);
       nrm[1] += qsi * qsi;
       nrm[3] += qi * qi;
-      drv[i] = d;
+      if constexpr (!kF32Factors) drv[i] = d;
       w.fr[W.wm + i] = (float)d;
     }
   }
@@ -668,7 +720,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
     sp[4] = h0;
     nrm[0] += sp[2] * sp[2];
     nrm[2] += cj * cj;
-    dcv[j] = fsp;
+    if constexpr (!kF32Factors) dcv[j] = fsp;
     w.fc[W.wn + j] = (float)fsp;
   }
   if (ilane) {
@@ -678,7 +730,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
     if (o.warm) sp[0] = sp[1] = sp[2] = yo_g[0] / fsp;
     nrm[1] += sp[3] * sp[3];
     nrm[3] += q0 * q0;
-    drv[0] = fsp;
+    if constexpr (!kF32Factors) drv[0] = fsp;
     w.fr[W.wm] = (float)fsp;
   }
   block_sum<B, 4>(nrm, red);
@@ -708,12 +760,12 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
     if constexpr (LI) {  // the outputs hold the last KKT check's T(z_k): the starting point until the first one
       if (val[s]) {
 #pragma unroll
-        for (int v = 0; v < NC; ++v) xo_g[col(s, v)] = x[s][v] * dcv[col(s, v)];
+        for (int v = 0; v < NC; ++v) xo_g[col(s, v)] = x[s][v] * dcf(col(s, v));
       }
 #pragma unroll
       for (int r = 0; r < NR; ++r) {
         const int i = row_of(s, r);
-        if (i >= 0) yo_g[i] = y[s][r] * drv[i];
+        if (i >= 0) yo_g[i] = y[s][r] * drf(i);
       }
     } else {
 #pragma unroll
@@ -978,7 +1030,13 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
         x[s][v] = xa[s][v] = xv;
         if constexpr (LA) XA[(v * S + s) * B + tid] = xv;
         XP[(v * S + s) * B + tid] = xv;
-        if (val[s]) wbox[col(s, v)] = wv;
+        if constexpr (!kNoWidths) {
+          if (val[s]) wbox[col(s, v)] = wv;
+        } else if (v < 3) {  // the steps tau / w^2 from the registers (box_steps below reads them back otherwise)
+          tj[s][v < 3 ? v : 0] = wv > 0.0 ? uniform(eta / pw) / (wv * wv) : 0.0;
+        } else {
+          ro(v - 1, s) = wv > 0.0 ? uniform(eta / pw) / (wv * wv) : 0.0;
+        }
       }
     }
     if (ilane) {
@@ -1012,7 +1070,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
         }
     }
   };
-  box_steps();
+  if constexpr (!kNoWidths) box_steps();  // (kNoWidths: formed at the box set-up)
   // (kBoxRescale) the steps for a new tau from the current ones: tau / w^2 = (tau / tau_bs) (tau_bs / w^2)
   auto box_steps_rescale = [&]() {
     if constexpr (BOX) {
@@ -1039,7 +1097,10 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
   int kbase = 0;
   auto hload = [&](int k0_) {
     const int kq = k0_ + lane;
-    return kq < kHalpernTab ? w.hinv[kq] : 1.0 / (kq + 2.0);
+    if constexpr (kHalpernDiv)  // (round 6) no global load on the restart path: the IEEE quotient the table holds
+      return 1.0 / (kq + 2.0);
+    else
+      return kq < kHalpernTab ? w.hinv[kq] : 1.0 / (kq + 2.0);
   };
   double hw = hload(0);
 
@@ -1103,9 +1164,11 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
       }
     }
   };
-  auto iterate = [&](auto chk_tag, auto w0_tag) __attribute__((always_inline)) {
+  auto iterate = [&](auto chk_tag, auto w0_tag, auto early_tag) __attribute__((always_inline)) {
     constexpr bool CHECK = decltype(chk_tag)::value;
     constexpr bool W0 = decltype(w0_tag)::value;
+    constexpr bool EARLY = decltype(early_tag)::value;  // (DVH_BAND_EARLY_SOE) SOE rows of steps 0 .. S - 2 before the barrier
+    if constexpr (W0 && DVH_BAND_PRIO) __builtin_amdgcn_s_setprio(DVH_BAND_PRIO);
     pstamp(4);  // (the check code since the last iteration, or the loop entry)
     if (kin - kbase >= kWave) {
       kbase = kin;
@@ -1116,6 +1179,27 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
     mvb0 = mvb1 = 0.0;
     // ---------------- primal half-step (reflected Halpern, rho = 1)
     double kx[S][NR];  // own-lane part of K x-bar for the dual half-step
+    // the dual update of step s's r-th row from kx (row 0, SOE, is an equality; DCM / ICE rows are >=: duals >= 0)
+    auto row_step = [&](int s, int r) __attribute__((always_inline)) {
+      if (!CHECK && r == 0) {  // equality row, no image needed: 2 (y - sigma Kx) - y = y - 2 sigma Kx
+        y[s][0] = fma(ca, fma(sigma2n, kx[s][0], y[s][0]), cb * ayv(s, 0));
+        return;
+      }
+      double p1 = fma(-sigma, kx[s][r], y[s][r]);
+      if (r > 0) p1 = vmax(p1, 0.0);
+      if (CHECK) {
+        const double d = y[s][r] - p1, da = p1 - ayv(s, r);
+        mv2 += d * d;
+        mv3 += da * da;
+        if constexpr (LI) {
+          const int i = row_of(s, r);
+          if (i >= 0) yim[opaque(i)] = p1;
+        } else {
+          YP[(r * S + s) * B + tid] = p1;
+        }
+      }
+      y[s][r] = fma(ca, fma(2.0, p1, -y[s][r]), cb * ayv(s, r));
+    };
     {
       double ta0 = 0.0, ta1 = 0.0;
       if constexpr (W0 && kTauWaveSums) {
@@ -1176,6 +1260,10 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
         kown_q(s, xb[s], kx[s]);
         if (s < S - 1) kfin_next(s, kx[s], xb[s < S - 1 ? s + 1 : s][2]);  // the next step is the lane's own
       }
+      if constexpr (EARLY) {  // (the SOE rows of steps 0 .. S - 2 need only the lane's own columns)
+#pragma unroll
+        for (int s = 0; s < S - 1; ++s) row_step(s, 0);
+      }
       if constexpr (W0 && kTauWaveSums) {
         tau_update(ta0, ca, cb, chk_tag);
       } else if constexpr (W0) {
@@ -1186,6 +1274,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
     }
     pstamp(0);
     lds_barrier();
+    if constexpr (W0 && DVH_BAND_PRIO) __builtin_amdgcn_s_setprio(0);
     pstamp(1);
     // ---------------- dual half-step
     {
@@ -1196,27 +1285,6 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
 #pragma unroll
       for (int s = 0; s < S; ++s) xtv[s] = lds_ld(xta[s]);
       kfin_next(S - 1, kx[S - 1], xen);
-      auto row_step = [&](int s, int r) __attribute__((always_inline)) {
-        // row 0 (SOE) is an equality; DCM / ICE rows are >=: duals stay >= 0
-        if (!CHECK && r == 0) {  // equality row, no image needed: 2 (y - sigma Kx) - y = y - 2 sigma Kx
-          y[s][0] = fma(ca, fma(sigma2n, kx[s][0], y[s][0]), cb * ayv(s, 0));
-          return;
-        }
-        double p1 = fma(-sigma, kx[s][r], y[s][r]);
-        if (r > 0) p1 = vmax(p1, 0.0);
-        if (CHECK) {
-          const double d = y[s][r] - p1, da = p1 - ayv(s, r);
-          mv2 += d * d;
-          mv3 += da * da;
-          if constexpr (LI) {
-            const int i = row_of(s, r);
-            if (i >= 0) yim[opaque(i)] = p1;
-          } else {
-            YP[(r * S + s) * B + tid] = p1;
-          }
-        }
-        y[s][r] = fma(ca, fma(2.0, p1, -y[s][r]), cb * ayv(s, r));
-      };
       // the >= rows first: their duals feed the tau partials, whose wave reduction then has the SOE rows' work
       // beside it
 #pragma unroll
@@ -1227,7 +1295,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
       }
       if (J > 0) tau_parts_of(y);
 #pragma unroll
-      for (int s = 0; s < S; ++s) row_step(s, 0);
+      for (int s = EARLY ? S - 1 : 0; s < S; ++s) row_step(s, 0);
       YS[tid + 1] = y[S - 1][0];
       if (W0 || wid == 0) {  // init row (lane kInitLane): ene_0 = target
         if (ilane) {
@@ -1254,20 +1322,27 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
 
   using F = std::integral_constant<bool, false>;
   using Tt = std::integral_constant<bool, true>;
+  using Early = std::integral_constant<bool, (DVH_BAND_EARLY_SOE != 0 && S > 1)>;
+  // (DVH_BAND_EARLY_SOE) the waves that do not carry the single tau column's update, in windows with one tau column
+  const bool early = DVH_BAND_EARLY_SOE != 0 && S > 1 && J == 1 && wid != 0;
   pstamp(-1);
   while (it < o.max_iters) {
     if (--ck != 0) {
       if (w0)
-        iterate(F(), Tt());
+        iterate(F(), Tt(), F());
+      else if (early)
+        iterate(F(), F(), Early());
       else
-        iterate(F(), F());
+        iterate(F(), F(), F());
       continue;
     }
     ck = chk;
     if (w0)
-      iterate(Tt(), Tt());
+      iterate(Tt(), Tt(), F());
+    else if (early)
+      iterate(Tt(), F(), Early());
     else
-      iterate(Tt(), F());
+      iterate(Tt(), F(), F());
     // ---------------- check: fixed-point residual of z_k, restart test; every kkt_every-th check the relative
     // KKT error of T(z_k) in the unscaled space (as pdhg_ell_kernel)
     const bool last = it + chk > o.max_iters;
@@ -1363,13 +1438,13 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
 #pragma unroll
             for (int v = 0; v < NC; ++v) {
               const int j = opaque(col(s, v));
-              xo_g[j] = xp[s][v] * dcv[j];
+              xo_g[j] = xp[s][v] * dcf(j);
             }
           }
 #pragma unroll
           for (int r = 0; r < NR; ++r) {
             const int i = row_of(s, r);
-            if (i >= 0) yo_g[opaque(i)] = yp[s][r] * drv[opaque(i)];
+            if (i >= 0) yo_g[opaque(i)] = yp[s][r] * drf(opaque(i));
           }
         }
         if (ICE && val[s]) {
@@ -1474,21 +1549,28 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
     for (int v = 0; v < NC; ++v) {
       const int j = col(s, v);
       if constexpr (BOX) {  // x = lo + w x' (clipped to the box against the rounding), then unscaled
-        const double d = dcv[j], lo = lraw[j] / d, hv = uraw[j] / d;
-        xo_g[j] = fmin(fmax(fma(wbox[j], XP[(v * S + s) * B + tid], lo), lo), hv) * d;
+        const double d = dcf(j), lo = lraw[j] / d, hv = uraw[j] / d;
+        double wv;
+        if constexpr (kNoWidths) {  // the set-up's width, by the set-up's operations
+          wv = hv - (v == 2 ? lo : 0.0);
+          if (!(wv >= 0x1p-500)) wv = 0.0;
+        } else {
+          wv = wbox[j];
+        }
+        xo_g[j] = fmin(fmax(fma(wv, XP[(v * S + s) * B + tid], lo), lo), hv) * d;
       } else {
-        xo_g[j] = XP[(v * S + s) * B + tid] * dcv[j];
+        xo_g[j] = XP[(v * S + s) * B + tid] * dcf(j);
       }
     }
-    yo_g[t + 1] = YP[s * B + tid] * drv[t + 1];
-    if (drow[s] >= 0) yo_g[drow[s]] = YP[(S + s) * B + tid] * drv[drow[s]];
+    yo_g[t + 1] = YP[s * B + tid] * drf(t + 1);
+    if (drow[s] >= 0) yo_g[drow[s]] = YP[(S + s) * B + tid] * drf(drow[s]);
     if (ICE) {
-      yo_g[ra[s]] = YP[(2 * S + s) * B + tid] * drv[ra[s]];
-      yo_g[rb[s]] = YP[(3 * S + s) * B + tid] * drv[rb[s]];
+      yo_g[ra[s]] = YP[(2 * S + s) * B + tid] * drf(ra[s]);
+      yo_g[rb[s]] = YP[(3 * S + s) * B + tid] * drf(rb[s]);
     }
   }
-  if (tlane) xo_g[3 * T + lane] = sp[5] * dcv[3 * T + lane];
-  if (ilane) yo_g[0] = sp[2] * drv[0];
+  if (tlane) xo_g[3 * T + lane] = sp[5] * dcf(3 * T + lane);
+  if (ilane) yo_g[0] = sp[2] * drf(0);
   if constexpr (DVH_BAND_PROBE) {
     pstamp(4);
     pacc[4] += (unsigned)(pt1 - pt2);
@@ -1629,7 +1711,7 @@ hipError_t launch_band_one_g(const Batch& b, const Work& w, const Chunk& ch, con
     if (!(q && atoi(q) == 0)) return launch_band_persist(GATE, BOX, b, w, ch, o, s, list, nlist, variant_out);
   }
   if constexpr (ICE) {  // the ICE form's persistent grid (DVH_BAND_QUEUE=0 or DVH_BAND_QUEUE_ICE=0: off, A/B)
-    static_assert(B == kBandSteps && S == 1 && LF == DVH_BANDI_LF && WPS == 3, "dvh_band_persist.hip instantiates this form");
+    static_assert(B == kBandSteps && S == 1 && LF == DVH_BANDI_LF && WPS == 3, "dvh_band_persist_ice.hip instantiates this form");
     const char* q = getenv("DVH_BAND_QUEUE");
     const char* qi = getenv("DVH_BAND_QUEUE_ICE");
     if (!(q && atoi(q) == 0) && !(qi && atoi(qi) == 0))

@@ -202,6 +202,16 @@ hipError_t launch_outage_min_soe(const OutageCase* d_cases, int ncase, int max_s
 struct LargeSolver;
 LargeSolver* large_create();
 void large_destroy(LargeSolver* ls);
+
+// The result all-gather's RCCL communicator (dvh_comm.cpp; dvh_comm_init / dvh_gather_results).  Return codes are the
+// DVH_* codes; messages go to *err.
+constexpr int kCommIdBytes = 128;  // ncclUniqueId
+struct Comm;
+int comm_unique_id(unsigned char* id, std::string* err);
+int comm_init(int device, int rank, int world, const unsigned char* id, Comm** out, std::string* err);
+int comm_all_gather(Comm* c, const void* send, void* recv, size_t bytes, hipStream_t s, std::string* err);
+void comm_info(const Comm* c, int* rank, int* world);
+void comm_destroy(Comm* c);
 // Solves window k (desc row d) of the batch on stream s; writes b.x / b.y / b.stats / b.istats of window k.
 hipError_t large_solve(LargeSolver* ls, const Batch& b, int k, const int64_t* d, const Opts& o, const double* hinv,
                        hipStream_t s, std::string* err, float* setup_ms, float* pdhg_ms);

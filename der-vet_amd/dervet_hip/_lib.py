@@ -126,7 +126,13 @@ SYMBOLS = {
     "dvh_outage_min_soe": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(OutageCase), ctypes.c_int32, c_int32_p,
                                           c_double_p]),
     "dvh_last_outage_ms": (ctypes.c_int, [ctypes.c_void_p, c_double_p]),
+    "dvh_comm_unique_id": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p]),
+    "dvh_comm_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p]),
+    "dvh_comm_info": (ctypes.c_int, [ctypes.c_void_p, c_int32_p]),
+    "dvh_gather_results": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                          ctypes.c_void_p]),
 }
+COMM_ID_BYTES = 128  # DVH_COMM_ID_BYTES
 
 _lib = None
 
@@ -142,6 +148,8 @@ def load(path=None):
                            "(there is no CPU fallback)")
     lib = ctypes.CDLL(p)
     for name, (res, args) in SYMBOLS.items():
+        if os.environ.get("DVH_LIB") and not hasattr(lib, name):
+            continue  # an A/B build of an earlier library (scripts/): the entry points it has
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args

@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "..", "csrc")
 LIB = os.path.join(HERE, "libdervet_hip.so")
 SOURCES = ["dvh_kernels.hip", "dvh_band.hip", "dvh_band_persist.hip", "dvh_band_persist_ice.hip", "dvh_chain.hip", "dvh_build.hip", "dvh_sweep.hip", "dvh_series.hip", "dvh_route.hip", "dvh_large.hip", "dvh_outage.hip",
-           "dvh_api.cpp", "dvh_validate.cpp"]
+           "dvh_api.cpp", "dvh_validate.cpp", "dvh_comm.cpp"]
 # per-source flags: the band kernel's persistent forms without machine-level loop-invariant code motion (their loop
 # invariants, hoisted out of the loop over windows, spilled; csrc/dvh_band_persist.hip), the battery form with the
 # AMDGPU scheduler's register-pressure trackers (+2.1 % on the bench; the ICE form is slower with them)
@@ -23,6 +23,8 @@ EXTRA_FLAGS = {"dvh_band_persist.hip": ["-mllvm", "-disable-machine-licm", "-mll
                "dvh_kernels.hip": ["-mllvm", "-disable-machine-licm"]}
 INCLUDES = {"dvh_band_persist.hip": "dvh_band.hip",  # (a one-line source around another: its compile time)
             "dvh_band_persist_ice.hip": "dvh_band.hip"}
+# flags of every object (build() and build_variant()); bench.source_key() hashes them with EXTRA_FLAGS and the compiler
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result", "-Wno-unused-value"]
 HEADERS = ["dvh_internal.h", "dvh_device.h", "dvh_validate.h", "dvh_rng.h", "dvh_ziggurat.h", os.path.join("..", "..", "include", "dervet_hip.h")]
 
 
@@ -41,8 +43,7 @@ def build(force=False, verbose=False):
     if not force and not _stale():
         return LIB
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result",
-             "-Wno-unused-value"]
+    flags = list(FLAGS)
     objdir = os.path.join(HERE, "build_obj")
     os.makedirs(objdir, exist_ok=True)
     # longest first, so the pool's tail is short
@@ -78,8 +79,7 @@ def build_variant(out, defines, recompile=("dvh_band.hip", "dvh_band_persist.hip
     ``recompile`` (their objects go to build_obj/<name>/), every other object taken from the default build."""
     build()
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result",
-             "-Wno-unused-value", *defines]
+    flags = [*FLAGS, *defines]
     name = os.path.splitext(os.path.basename(out))[0]
     objdir = os.path.join(HERE, "build_obj", name)
     os.makedirs(objdir, exist_ok=True)
@@ -106,6 +106,24 @@ def build_variant(out, defines, recompile=("dvh_band.hip", "dvh_band_persist.hip
         sys.stderr.write(r.stdout + r.stderr)
         raise RuntimeError("hipcc failed linking variant " + name)
     return out
+
+
+def compiler_version():
+    """The hipcc / clang version string the objects are built with ("unknown" if hipcc cannot be run)."""
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    try:
+        r = subprocess.run([hipcc, "--version"], capture_output=True, text=True, timeout=60)
+        lines = [ln.strip() for ln in r.stdout.splitlines() if ln.strip()]
+        # HIP version + the clang line (drop the install-dir lines, which differ between boxes of one image)
+        return " | ".join(ln for ln in lines if not ln.startswith("InstalledDir")) or "unknown"
+    except (OSError, subprocess.SubprocessError):
+        return "unknown"
+
+
+def build_config():
+    """Everything besides the sources that decides the machine code: common and per-source flags, compiler."""
+    return {"flags": FLAGS, "extra_flags": {k: EXTRA_FLAGS[k] for k in sorted(EXTRA_FLAGS)},
+            "compiler": compiler_version()}
 
 
 if __name__ == "__main__":

@@ -229,6 +229,11 @@ class DegradationSweep:
             # only OPTIMAL dispatch is counted (an infeasible window's x is no SOE profile; VERDICT r04:
             # nor is an ITER_LIMIT one, which failed the KKT test) -- the others are counted in Degradation.skipped
             valid = ist[:, 0] == 0
+            if not valid.all():  #  a skipped window gets calendar loss only: say so, it biases wear low
+                import warnings
+                warnings.warn(f"degradation sweep, window position {k}: {int((~valid).sum())} of {len(valid)} windows "
+                              f"not OPTIMAL (statuses {sorted(set(int(v) for v in ist[~valid, 0]))}); their cycle wear "
+                              "is not counted (Degradation.skipped)", RuntimeWarning, stacklevel=2)
             deg = self.deg.update(ene, T * self.dt / 24.0, valid=valid,
                                   year=None if self.years is None else self.years[k])
             out.append(dict(k=k, iters=ist[:, 1], status=ist[:, 0], obj=obj, degradation=deg, capacity_before=cap,

@@ -165,6 +165,58 @@ def gather_rows(rows, group=None, counts=None, async_op=False):
     return torch.cat([out[r * kmax:r * kmax + n] for r, n in enumerate(counts)], dim=0)
 
 
+class LibraryGather:
+    """The result all-gather through libdervet_hip's own RCCL communicator (``dvh_comm_init`` / ``dvh_gather_results``,
+    include/dervet_hip.h): what ``gather_rows`` does over torch.distributed, with the collective inside the library, so
+    that a consumer without PyTorch can shard too.  torch.distributed (when present) only carries the 128-byte unique id
+    from rank 0 to the others (``from_torch``).  The gather runs on a stream of its own: ``gather(rows,
+    async_op=True)`` returns at once (the next solve runs beside it) and its ``wait()`` orders the caller's stream after
+    it."""
+
+    def __init__(self, solver, rank, world, uid):
+        import torch
+        self.solver, self.rank, self.world = solver, int(rank), int(world)
+        solver.comm_init(rank, world, uid)
+        self.stream = torch.cuda.Stream()
+
+    @classmethod
+    def from_torch(cls, solver, group=None):
+        """Rank 0 draws the id, torch.distributed broadcasts it (the launcher's role only)."""
+        import torch.distributed as dist
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        box = [solver.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0, group=group)
+        return cls(solver, rank, world, box[0])
+
+    def gather(self, rows, async_op=False):
+        import torch
+        pad = rows.contiguous()
+        out = torch.empty((self.world * pad.shape[0],) + tuple(pad.shape[1:]), dtype=pad.dtype, device=pad.device)
+        cur = torch.cuda.current_stream(pad.device)
+        self.stream.wait_stream(cur)  # the rows are ready before the gather reads them
+        self.solver.gather_results(pad, out, self.stream)
+        done = PendingLibraryGather(self.stream, out, pad)
+        return done if async_op else done.wait()
+
+
+class PendingLibraryGather:
+    """A library all-gather in flight: ``wait()`` makes the current stream wait for it and returns the rows (the input
+    stays referenced until then)."""
+
+    def __init__(self, stream, out, rows):
+        import torch
+        self._ev = torch.cuda.Event()
+        self._ev.record(stream)
+        self._out, self._rows = out, rows
+
+    def wait(self):
+        import torch
+        torch.cuda.current_stream(self._out.device).wait_event(self._ev)
+        self._ev.synchronize()
+        self._rows = None
+        return self._out
+
+
 def rows_to_numpy(rows, tmax=None):
     r = rows.detach().cpu().numpy()
     out = dict(obj=r[:, 0], primal_res_rel=r[:, 1], dual_res_rel=r[:, 2], gap_rel=r[:, 3],

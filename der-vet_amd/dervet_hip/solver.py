@@ -223,6 +223,37 @@ class BatchSolver:
         return [WindowResult(outs[k][0], outs[k][1], res[k].obj, res[k].status, res[k].iters, res[k].primal_res_rel,
                              res[k].dual_res_rel, res[k].gap_rel) for k in range(count)]
 
+    # ---- the result all-gather across ranks, through the library's own RCCL communicator (dvh_comm_*)
+    def comm_unique_id(self):
+        """128 bytes from ncclGetUniqueId (rank 0 draws it; the launcher hands it to every rank)."""
+        buf = ctypes.create_string_buffer(_lib.COMM_ID_BYTES)
+        self._check(self._lib.dvh_comm_unique_id(self._h, buf), "dvh_comm_unique_id")
+        return buf.raw
+
+    def comm_init(self, rank, world, uid):
+        if len(uid) != _lib.COMM_ID_BYTES:
+            raise ValueError(f"a communicator id has {_lib.COMM_ID_BYTES} bytes, got {len(uid)}")
+        self._check(self._lib.dvh_comm_init(self._h, int(rank), int(world), bytes(uid)), "dvh_comm_init")
+
+    def comm_info(self):
+        v = (ctypes.c_int32 * 2)()
+        self._check(self._lib.dvh_comm_info(self._h, v), "dvh_comm_info")
+        return int(v[0]), int(v[1])
+
+    def gather_results(self, rows, out, stream=None):
+        """out (device, world x rows' bytes) = every rank's ``rows`` (a contiguous device tensor) in rank order, enqueued
+        on ``stream`` (a torch stream or a hipStream_t; None = the solver's own stream)."""
+        if not rows.is_contiguous() or not out.is_contiguous():
+            raise ValueError("gather_results needs contiguous tensors")
+        nb = rows.numel() * rows.element_size()
+        world = self.comm_info()[1]
+        if world and out.numel() * out.element_size() != nb * world:
+            raise ValueError("out must hold world x the rows' bytes")
+        s = getattr(stream, "cuda_stream", stream)
+        self._check(self._lib.dvh_gather_results(self._h, ctypes.c_void_p(rows.data_ptr()), nb,
+                                                 ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(s or 0)),
+                    "dvh_gather_results")
+
     def solve_packed(self, pb, stream=None, sync=True):
         """Solve a device-resident packed batch (``dervet_hip.packed.PackedBatch`` of torch tensors)."""
         p = pb.as_ctypes()

@@ -68,16 +68,23 @@ def stitched_start(long, subs, sub_x, sub_y, dcm_duals=False):
         y0[a + Ts] = ys[Ts]
         a += Ts
     if long.J and dcm_duals:
-        # DCM duals: rows of the long window keyed by (global step, rank of the charge among those covering it)
-        sub_dual = {}
+        # DCM duals: rows of the long window keyed by (global step, rank of the charge among those covering it).  The
+        # rank identifies a charge only where both windows cover the step with the same number of charges (ADVICE r05:
+        # an extra or missing charge would shift the ranks); a step where the counts differ starts from 0 instead.
+        sub_dual, sub_count = {}, {}
         a = 0
         for s, g in enumerate(subs):
             ys = np.asarray(sub_y[s], np.float64)
             for t, k, r in _dcm_rows(g):
                 sub_dual[(a + t, k)] = ys[r]
+                sub_count[a + t] = sub_count.get(a + t, 0) + 1
             a += g.T
-        for t, k, r in _dcm_rows(long):
-            y0[r] = sub_dual.get((t, k), 0.0)
+        long_rows = list(_dcm_rows(long))
+        long_count = {}
+        for t, _, _ in long_rows:
+            long_count[t] = long_count.get(t, 0) + 1
+        for t, k, r in long_rows:
+            y0[r] = sub_dual.get((t, k), 0.0) if sub_count.get(t, 0) == long_count[t] else 0.0
     if long.J:
         K = sp.csr_matrix((long.data[0], long.indices, long.indptr), shape=(long.m, long.n))
         ge = K[long.m_eq:]

@@ -150,6 +150,22 @@ int dvh_destroy(dvh_handle* h);
 const char* dvh_last_error(const dvh_handle* h);
 int dvh_set_options(dvh_handle* h, const dvh_options* opts);
 
+/* ---- The result all-gather across ranks.  One process per GPU: the windows are sharded over the
+ * ranks with no traffic during the solve, then ONE all-gather returns every window's result row (objective,
+ * residuals, status, iterations, (scenario, window) tag, dispatch) to every rank.  Replaces the reference's serial
+ * case loop (dervet/DERVET.py:75-83).  RCCL is opened at run time (librccl.so.1 of /opt/rocm, or DVH_RCCL_LIB);
+ * DVH_ERR_UNSUPPORTED when it cannot be.
+ *   dvh_comm_unique_id: rank 0 draws the 128-byte id (ncclGetUniqueId) the launcher hands to every rank;
+ *   dvh_comm_init: joins rank `rank` of `world` on the handle's device (single-device handles only);
+ *   dvh_comm_info: {rank, world} (0, 0 without a communicator);
+ *   dvh_gather_results: out[world * bytes_per_rank] (device) = every rank's rows[bytes_per_rank] (device) in rank
+ *     order; asynchronous on `stream` (a hipStream_t; NULL = the handle's solver stream, i.e. after its solves). */
+#define DVH_COMM_ID_BYTES 128
+int dvh_comm_unique_id(dvh_handle* h, uint8_t* id);
+int dvh_comm_init(dvh_handle* h, int32_t rank, int32_t world, const uint8_t* id);
+int dvh_comm_info(const dvh_handle* h, int32_t* rank_world);
+int dvh_gather_results(dvh_handle* h, const void* rows, uint64_t bytes_per_rank, void* out, void* stream);
+
 /* Host buffers in / out.  Blocks until the batch is solved. */
 int dvh_solve_batch(dvh_handle* h, const dvh_lp* lps, int32_t count, dvh_result* out);
 

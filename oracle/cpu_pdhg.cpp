@@ -417,6 +417,15 @@ int dvh_last_chain_aborts(const dvh_handle*, int32_t* out) {
 const char* dvh_last_warning(const dvh_handle*) { return ""; }
 int dvh_set_kernel_path(dvh_handle*, int) { return DVH_OK; }
 int dvh_set_launch_order(dvh_handle*, const int32_t*, int32_t) { return DVH_OK; }
+// the result all-gather is a device collective (RCCL): no communicator in the CPU restatement
+int dvh_comm_unique_id(dvh_handle*, uint8_t*) { return DVH_ERR_UNSUPPORTED; }
+int dvh_comm_init(dvh_handle*, int32_t, int32_t, const uint8_t*) { return DVH_ERR_UNSUPPORTED; }
+int dvh_comm_info(const dvh_handle* h, int32_t* rw) {
+  if (!h || !rw) return DVH_ERR_ARG;
+  rw[0] = rw[1] = 0;
+  return DVH_OK;
+}
+int dvh_gather_results(dvh_handle*, const void*, uint64_t, void*, void*) { return DVH_ERR_UNSUPPORTED; }
 int dvh_outage_coverage(dvh_handle*, const dvh_outage_case*, int32_t, int32_t*, double*) { return DVH_ERR_UNSUPPORTED; }
 int dvh_outage_min_soe(dvh_handle*, const dvh_outage_case*, int32_t, const int32_t*, double*) {
   return DVH_ERR_UNSUPPORTED;

@@ -546,3 +546,29 @@ def test_install_batch_cases_saves_what_the_serial_case_loop_saves(case_batch):
     # re-installing without batch_cases restores the reference's solve
     dropin.install(mod, solver_factory=Counting)
     assert not getattr(mod.DERVET.solve, "dervet_hip_batched", False)
+
+
+def test_real_cvxpy_ecos_bb_round_trip_of_a_relaxed_window():
+    """the relaxed-MILP path hands CVXPY's own ECOS_BB inversion an ECOS-shaped solution.  cvxpy is absent
+    in this container, so this round trip is unverified here and the test skips; where cvxpy is
+    installed it runs one relaxed battery window through CvxpyExporter(relax_milp=True) -> a HiGHS stand-in for the
+    batched solve -> Problem.unpack_results, and checks the status and the objective against CVXPY's own LP value."""
+    cvx = pytest.importorskip("cvxpy")
+    T = 6
+    price = np.array([0.1, 0.3, 0.05, 0.4, 0.2, 0.1])
+    ch, dis, ene = cvx.Variable(T), cvx.Variable(T), cvx.Variable(T)
+    on = cvx.Variable(T, boolean=True)
+    cons = [ch >= 0, dis >= 0, ch <= 100 * on, dis <= 100 * (1 - on), ene >= 0, ene <= 400, ene[0] == 200,
+            ene[1:] == ene[:-1] + 0.9 * ch[:-1] - dis[:-1], ene[-1] + 0.9 * ch[-1] - dis[-1] == 200]
+    functions = {"energy": price @ (ch - dis)}
+    win = dropin.CvxpyExporter(relax_milp=True).export(functions, cons)
+    assert win is not None and getattr(win.ew, "relaxed", False)
+    r = _highs(win.lp)
+    prob, err = win.unpack(r)
+    assert err is None and prob.status in ("optimal", "optimal_inaccurate")
+    lp_on = cvx.Variable(T)
+    lp_cons = [ch >= 0, dis >= 0, ch <= 100 * lp_on, dis <= 100 * (1 - lp_on), lp_on >= 0, lp_on <= 1, ene >= 0,
+               ene <= 400, ene[0] == 200, ene[1:] == ene[:-1] + 0.9 * ch[:-1] - dis[:-1],
+               ene[-1] + 0.9 * ch[-1] - dis[-1] == 200]
+    relaxed_value = cvx.Problem(cvx.Minimize(price @ (ch - dis)), lp_cons).solve()
+    assert prob.value == pytest.approx(relaxed_value, rel=1e-6, abs=1e-6)

@@ -104,3 +104,21 @@ def test_monthly_sub_windows_carry_their_demand_charge_duals_over():
     for t, k, r in rows:
         assert y0[r] == want[(t, k)] and y_off[r] == 0.0
     np.testing.assert_array_equal(y0[:long.m_eq], y_off[:long.m_eq])
+
+
+def test_dcm_duals_only_where_both_windows_count_the_same_charges():
+    """the (step, rank) key identifies a charge only where both windows cover the step with the same number
+    of charges.  A monthly sub-window without its demand charge (no DCM rows) leaves its month's long-window rows at 0;
+    the other months still carry their duals over."""
+    long = _groups("year", True)[0]
+    subs = _groups("month", True)
+    subs[0] = _groups("month", False)[0]  # January without the demand charge
+    sub_y = [np.arange(g.m, dtype=np.float64) + 1e6 * (s + 1) for s, g in enumerate(subs)]
+    sub_x = [np.zeros(g.n) for g in subs]
+    _, y0 = stitched_start(long, subs, sub_x, sub_y, dcm_duals=True)
+    from dervet_hip.stitch import _dcm_rows
+    jan = subs[0].T
+    rows = _dcm_rows(long)
+    assert any(t < jan for t, _, _ in rows) and any(t >= jan for t, _, _ in rows)
+    for t, k, r in rows:
+        assert (y0[r] == 0.0) == (t < jan)
