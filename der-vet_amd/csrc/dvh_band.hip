@@ -71,9 +71,13 @@ __host__ __device__ inline size_t band_lds_doubles(int B, int S, bool ice, int L
 __host__ __device__ inline size_t band_ints_bytes(int B, int S) { return sizeof(int32_t) * (4 * (size_t)S * B + 4); }
 // The ints share the anchors' (kLfAnchors) or, in the other relieved forms, the check images' space
 __host__ __device__ constexpr bool band_ints_shared(int LF) { return (LF & kLfAnchors) || (LF && !(LF & kLfImages)); }
+// (round 6) the lane's DCM row indices, drow[S][B], kept in LDS from the set-up to the write-back instead of in VGPRs (held
+// across the iteration loop they were among the persistent form's spilled values, and each check's reload of a spilled
+// index waited for every global load issued before it)
+__host__ __device__ inline size_t band_drow_bytes(int B, int S) { return align16(sizeof(int32_t) * (size_t)S * B); }
 __host__ __device__ inline size_t band_lds_bytes(int B, int S, bool ice, int LF) {
   const size_t d = align16(sizeof(double) * band_lds_doubles(B, S, ice, LF));
-  return band_ints_shared(LF) ? d : d + align16(band_ints_bytes(B, S));
+  return (band_ints_shared(LF) ? d : d + align16(band_ints_bytes(B, S))) + band_drow_bytes(B, S);
 }
 
 // KKT pieces of one column / one row (out of line: the KKT check runs every 128 iterations, and inlined it
@@ -205,17 +209,35 @@ constexpr bool kF32Round = kF32Factors || DVH_BAND_F32F == -1;
 #define DVH_BAND_HDIV 1
 #endif
 constexpr bool kHalpernDiv = DVH_BAND_HDIV != 0;
-// DVH_BAND_PRIO (A/B): wave 0, whose primal half-step carries the tau column's reduction and update, raises its issue
-// priority (s_setprio) until the first barrier, so that the SIMD it shares with the other window's wave issues its
-// instructions first.
-#ifndef DVH_BAND_PRIO
-#define DVH_BAND_PRIO 0
+// kkt_prefetch (round 6): a KKT check reads the single-precision factors of the lane's columns and rows (Work::fc / fr,
+// 15 per lane) from the window's workspace.  Each load sat behind its opaque index (kept so that the check's address
+// arithmetic is not hoisted into the iteration loop) and was waited for before the next one was issued: 15 serialised
+// global-memory latencies per check (the ISA showed each global_load_dword followed by s_waitcnt vmcnt(0)).  Now the
+// indices and loads are issued together at the top of the check, one wait behind the image reads and the barrier.
+#ifndef DVH_BAND_KKT_PREFETCH
+#define DVH_BAND_KKT_PREFETCH 1
 #endif
-// DVH_BAND_EARLY_SOE (A/B): the waves other than wave 0 update the SOE rows of their lanes' first S - 1 steps in the
-// primal half-step, before the first barrier (those rows need only the lane's own columns), instead of after it: the
-// work fills their wait for wave 0 and shortens the dual half-step that follows.
-#ifndef DVH_BAND_EARLY_SOE
-#define DVH_BAND_EARLY_SOE 0
+// (the ICE form, at its 168-VGPR budget, spills 14 VGPRs more with the batched loads and runs config 5 slower: 111.9k vs
+// 114.7k windows/s, profiles/r06c_ab.log -- it keeps the per-use loads)
+#ifndef DVH_BAND_KKT_PREFETCH_ICE
+#define DVH_BAND_KKT_PREFETCH_ICE 0
+#endif
+template <bool ICE>
+constexpr bool kkt_prefetch() { return DVH_BAND_KKT_PREFETCH != 0 && (!ICE || DVH_BAND_KKT_PREFETCH_ICE != 0); }
+// DVH_BAND_PRIO (round 6, default 2): wave 0, whose primal half-step carries the tau column's reduction and update --
+// the iteration's critical path, on which the other three waves wait at the first barrier -- raises its issue priority
+// (s_setprio) until that barrier, so that the SIMD it shares with the other window's wave issues its instructions
+// first.  Measured (scripts/gpu_r06a.sh, profiles/r06a_ab.log): 0.979 -> 0.940 us per window-iteration per slot at a
+// fixed 1,024 iterations, bench 284.4k -> 292.9k windows/s, identical iterations and residuals; config 5 (the ICE form,
+// whose wave 0 of twelve carries the column) 108.3k -> 111.9k (profiles/r06c_ab.log).  0: off.
+#ifndef DVH_BAND_PRIO
+#define DVH_BAND_PRIO 2
+#endif
+// DVH_BAND_PRIO_DUAL (A/B): every wave raises its priority from the start of the dual half-step until its DCM rows'
+// tau partials are written (the values wave 0's next reduction waits for).  Measured and not kept: 292.0k vs 292.6k
+// windows/s (profiles/r06c_ab.log); s_setprio 3 instead of 2 for wave 0: 292.7k (same).
+#ifndef DVH_BAND_PRIO_DUAL
+#define DVH_BAND_PRIO_DUAL 0
 #endif
 // DVH_BAND_PROBE (A/B builds only, scripts/probe_band_latency.py): every wave accumulates the shader-clock cycles of
 // its iterations' four segments -- primal half-step, wait at the first barrier, dual half-step, wait at the second --
@@ -292,6 +314,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
   int32_t* ice_b = ice_a + SB;
   int32_t* ice_n = ice_b + SB;
   int32_t* flag = ice_n + SB;
+  int32_t* DRL = reinterpret_cast<int32_t*>(smem + band_lds_bytes(B, S, ICE, LF) - band_drow_bytes(B, S));  // [S][B]
 
   const int32_t* gkp = b.indptr + W.row;
   const int32_t* gkc = b.indices + W.nz;
@@ -458,6 +481,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
     q[s][0] = q[s][1] = 0.0;
     loe[s] = 0.0;
     drow[s] = -1;
+    DRL[s * B + tid] = -1;
     jt[s] = 0;
     ra[s] = rb[s] = -1;
     if (ICE)
@@ -488,6 +512,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
     const int dv = dcm[t];
     if (dv >= 0) {
       drow[s] = dv >> 3;
+      DRL[s * B + tid] = drow[s];
       jt[s] = dv & 7;
       for (int p = gkp[drow[s]]; p < gkp[drow[s] + 1]; ++p) {
         const int c = gkc[p];
@@ -1164,10 +1189,9 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
       }
     }
   };
-  auto iterate = [&](auto chk_tag, auto w0_tag, auto early_tag) __attribute__((always_inline)) {
+  auto iterate = [&](auto chk_tag, auto w0_tag) __attribute__((always_inline)) {
     constexpr bool CHECK = decltype(chk_tag)::value;
     constexpr bool W0 = decltype(w0_tag)::value;
-    constexpr bool EARLY = decltype(early_tag)::value;  // (DVH_BAND_EARLY_SOE) SOE rows of steps 0 .. S - 2 before the barrier
     if constexpr (W0 && DVH_BAND_PRIO) __builtin_amdgcn_s_setprio(DVH_BAND_PRIO);
     pstamp(4);  // (the check code since the last iteration, or the loop entry)
     if (kin - kbase >= kWave) {
@@ -1260,10 +1284,6 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
         kown_q(s, xb[s], kx[s]);
         if (s < S - 1) kfin_next(s, kx[s], xb[s < S - 1 ? s + 1 : s][2]);  // the next step is the lane's own
       }
-      if constexpr (EARLY) {  // (the SOE rows of steps 0 .. S - 2 need only the lane's own columns)
-#pragma unroll
-        for (int s = 0; s < S - 1; ++s) row_step(s, 0);
-      }
       if constexpr (W0 && kTauWaveSums) {
         tau_update(ta0, ca, cb, chk_tag);
       } else if constexpr (W0) {
@@ -1278,6 +1298,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
     pstamp(1);
     // ---------------- dual half-step
     {
+      if constexpr (DVH_BAND_PRIO_DUAL) __builtin_amdgcn_s_setprio(DVH_BAND_PRIO_DUAL);
       // every LDS read of the half-step first (the next lane's ene, the tau columns' x-bar), before any LDS store:
       // issued together, one wait instead of one per read
       const double xen = XE[tid + 1];
@@ -1294,8 +1315,9 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
         for (int r = 1; r < NR; ++r) row_step(s, r);
       }
       if (J > 0) tau_parts_of(y);
+      if constexpr (DVH_BAND_PRIO_DUAL) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
-      for (int s = EARLY ? S - 1 : 0; s < S; ++s) row_step(s, 0);
+      for (int s = 0; s < S; ++s) row_step(s, 0);
       YS[tid + 1] = y[S - 1][0];
       if (W0 || wid == 0) {  // init row (lane kInitLane): ene_0 = target
         if (ilane) {
@@ -1322,27 +1344,20 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
 
   using F = std::integral_constant<bool, false>;
   using Tt = std::integral_constant<bool, true>;
-  using Early = std::integral_constant<bool, (DVH_BAND_EARLY_SOE != 0 && S > 1)>;
-  // (DVH_BAND_EARLY_SOE) the waves that do not carry the single tau column's update, in windows with one tau column
-  const bool early = DVH_BAND_EARLY_SOE != 0 && S > 1 && J == 1 && wid != 0;
   pstamp(-1);
   while (it < o.max_iters) {
     if (--ck != 0) {
       if (w0)
-        iterate(F(), Tt(), F());
-      else if (early)
-        iterate(F(), F(), Early());
+        iterate(F(), Tt());
       else
-        iterate(F(), F(), F());
+        iterate(F(), F());
       continue;
     }
     ck = chk;
     if (w0)
-      iterate(Tt(), Tt(), F());
-    else if (early)
-      iterate(Tt(), F(), Early());
+      iterate(Tt(), Tt());
     else
-      iterate(Tt(), F(), F());
+      iterate(Tt(), F());
     // ---------------- check: fixed-point residual of z_k, restart test; every kkt_every-th check the relative
     // KKT error of T(z_k) in the unscaled space (as pdhg_ell_kernel)
     const bool last = it + chk > o.max_iters;
@@ -1373,6 +1388,35 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
       }
     }
     if (kkt) {
+      // (kkt_prefetch) the single-precision factors of the lane's columns and rows, loaded together first: one wait
+      // for all of them, behind the image reads and the barrier below
+      // (branch-free: a padding step / absent row loads the window's first entry and discards it; the indices are
+      // formed here from an opaque thread index, so that they are not hoisted out of the loop and held)
+      float fcl[S][NC], frl[S][NR], fspl = 1.0f;
+      if constexpr (kkt_prefetch<ICE>()) {
+        const int to = S * opaque(tid);
+        const float* fcw = w.fc + W.wn;
+        const float* frw = w.fr + W.wm;
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          const bool vs = to + s < T;
+#pragma unroll
+          for (int v = 0; v < NC; ++v) {
+            const int j = v < 3 ? v * T + to + s : (v == 3 ? CE : CO) + to + s;
+            const float f = fcw[vs ? j : 0];
+            fcl[s][v] = vs ? f : 1.0f;
+          }
+#pragma unroll
+          for (int r = 0; r < NR; ++r) {
+            const int i = r == 0 ? (vs ? to + s + 1 : -1) : r == 1 ? DRL[s * B + tid] : (vs ? (r == 2 ? ra[s] : rb[s]) : -1);
+            const float f = frw[i >= 0 ? i : 0];
+            frl[s][r] = i >= 0 ? f : 1.0f;
+          }
+        }
+        const int lo_ = (to / S) & (kWave - 1);  // (the lane, from the opaque thread index)
+        const float ft = fcw[tlane ? 3 * T + lo_ : 0], fi = frw[0];
+        fspl = tlane ? ft : ilane ? fi : 1.0f;
+      }
       // images of T(z_k) in XE / XT / YS / TP (rewritten from z after the check)
       double xp[S][NC], yp[S][NR];
       load_images(xp, yp);
@@ -1382,24 +1426,24 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
       if (tlane) XT[lane] = sp[5];
       if (J > 0) tau_parts_of(yp);
       lds_barrier();
-      auto col_kkt = [&](int j, double kt, double cj, double loj, double hij, double xj) {
-        const int jj = opaque(j);
+      auto col_kkt = [&](int j, double kt, double cj, double loj, double hij, double xj, float fpre) {
+        const float fd = kkt_prefetch<ICE>() ? fpre : w.fc[W.wn + opaque(j)];
         if constexpr (NRED > kRdx && DVH_KKT_RDX) {
-          const ColKktX r = col_kkt_fn_x<kkt_inline<ICE>()>(kt, cj, loj, hij, xj, w.fc[W.wn + jj]);
+          const ColKktX r = col_kkt_fn_x<kkt_inline<ICE>()>(kt, cj, loj, hij, xj, fd);
           acc[5] += r.rd2;
           acc[6] += r.cx;
           acc[8] += r.bt;
           acc[kRdx] += r.rdx;
         } else {
-          const ColKkt r = col_kkt_fn<kkt_inline<ICE>()>(kt, cj, loj, hij, xj, w.fc[W.wn + jj]);
+          const ColKkt r = col_kkt_fn<kkt_inline<ICE>()>(kt, cj, loj, hij, xj, fd);
           acc[5] += r.rd2;
           acc[6] += r.cx;
           acc[8] += r.bt;
         }
       };
-      auto row_kkt = [&](int i, double kv, double qi, double yi, bool ge) {
-        const int ii = opaque(i);
-        const RowKkt r = row_kkt_fn<kkt_inline<ICE>()>(kv, qi, yi, w.fr[W.wm + ii], ge);
+      auto row_kkt = [&](int i, double kv, double qi, double yi, bool ge, float fpre) {
+        const float fd = kkt_prefetch<ICE>() ? fpre : w.fr[W.wm + opaque(i)];
+        const RowKkt r = row_kkt_fn<kkt_inline<ICE>()>(kv, qi, yi, fd, ge);
         acc[4] += r.rp2;
         acc[7] += qi * yi;
         acc[9] += r.y2;
@@ -1413,15 +1457,15 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
 #pragma unroll
           for (int v = 0; v < NC; ++v) {
             if constexpr (BOX)  // the primed LP: box [0, 1]
-              col_kkt(col(s, v), kt[v], cof(s, v), 0.0, 1.0, xp[s][v]);
+              col_kkt(col(s, v), kt[v], cof(s, v), 0.0, 1.0, xp[s][v], fcl[s][v]);
             else
-              col_kkt(col(s, v), kt[v], cof(s, v), v == 2 ? loe[s] : 0.0, hib(s, v), xp[s][v]);
+              col_kkt(col(s, v), kt[v], cof(s, v), v == 2 ? loe[s] : 0.0, hib(s, v), xp[s][v], fcl[s][v]);
           }
         }
       }
       if (wid == 0 && J > 0) {
         const double ktt = tau_kt();
-        if (tlane) col_kkt(3 * T + lane, ktt, sp[2], sp[3], sp[4], sp[5]);
+        if (tlane) col_kkt(3 * T + lane, ktt, sp[2], sp[3], sp[4], sp[5], fspl);
       }
       const double xen = XE[tid + 1];
 #pragma unroll
@@ -1431,8 +1475,9 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
         kfin_next(s, kv, s == S - 1 ? xen : xp[s < S - 1 ? s + 1 : s][2]);
         kfin_tau(s, kv);
         const int t = t0 + s;
-        if (val[s]) row_kkt(t + 1, kv[0], qv(s, 0), yp[s][0], false);
-        if (drow[s] >= 0) row_kkt(drow[s], kv[1], qv(s, 1), yp[s][1], true);
+        if (val[s]) row_kkt(t + 1, kv[0], qv(s, 0), yp[s][0], false, frl[s][0]);
+        const int dr_ = DRL[s * B + tid];
+        if (dr_ >= 0) row_kkt(dr_, kv[1], qv(s, 1), yp[s][1], true, frl[s][1]);
         if constexpr (LI) {  // this check's T(z_k), unscaled, as the outputs
           if (val[s]) {
 #pragma unroll
@@ -1448,11 +1493,11 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
           }
         }
         if (ICE && val[s]) {
-          row_kkt(ra[s], kv[2], rhs(s, 2), yp[s][2], true);
-          row_kkt(rb[s], kv[3], rhs(s, 3), yp[s][3], true);
+          row_kkt(ra[s], kv[2], rhs(s, 2), yp[s][2], true, frl[s][NR > 2 ? 2 : 0]);
+          row_kkt(rb[s], kv[3], rhs(s, 3), yp[s][3], true, frl[s][NR > 3 ? 3 : 0]);
         }
       }
-      if (ilane) row_kkt(0, sp[4] * XE[0], sp[3], sp[2], false);
+      if (ilane) row_kkt(0, sp[4] * XE[0], sp[3], sp[2], false, fspl);
     }
     if constexpr (GATE) {
       if (kkt) {  // the KKT sums in the slots after the restart sums' (red is not reused before a barrier)
@@ -1563,7 +1608,8 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
       }
     }
     yo_g[t + 1] = YP[s * B + tid] * drf(t + 1);
-    if (drow[s] >= 0) yo_g[drow[s]] = YP[(S + s) * B + tid] * drf(drow[s]);
+    const int dr_ = DRL[s * B + tid];
+    if (dr_ >= 0) yo_g[dr_] = YP[(S + s) * B + tid] * drf(dr_);
     if (ICE) {
       yo_g[ra[s]] = YP[(2 * S + s) * B + tid] * drf(ra[s]);
       yo_g[rb[s]] = YP[(3 * S + s) * B + tid] * drf(rb[s]);
