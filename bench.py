@@ -91,6 +91,15 @@ def pmc_profiles(count, launches):
     return out
 
 
+def outputs_sha(dev):
+    """SHA-256 of the batch's outputs (x, y, stats, istats), in that order, as host bytes."""
+    import hashlib
+    h = hashlib.sha256()
+    for t in (dev.x, dev.y, dev.stats, dev.istats):
+        h.update(t.detach().cpu().numpy().tobytes())
+    return h.hexdigest()
+
+
 def stream_copy_gbps(dev, gib=2.0, reps=10):
     """Measured HBM copy ceiling on this GPU (torch device-to-device copy, read + write bytes / time)."""
     n = int(gib * 2 ** 30 / 8)
@@ -314,6 +323,12 @@ def main():
                          "features, regularised toward the inverse-distance weights by LAM (dervet_hip.sweep."
                          "affine_weights); <= 0: inverse-distance weights")
     ap.add_argument("--no-cold-ref", action="store_true", help="skip the untimed all-cold reference solve")
+    ap.add_argument("--sha", action="store_true", help="add the SHA-256 of the last step's x / y / stats / istats "
+                    "(bit-identity of two library builds on the same batch)")
+    ap.add_argument("--warm-options", default="", help="seeded schedule: dvh_options of the warm phase as JSON "
+                    "(default: sweep.WARM_OPTIONS)")
+    ap.add_argument("--seed-options", default="", help="seeded schedule: dvh_options of the cold seed phase as JSON "
+                    "(default: sweep.SEED_OPTIONS)")
     ap.add_argument("--kkt-predict", type=int, default=4,
                     help="dvh_options.kkt_predict for cold solves (--schedule cold and the cold reference; the seeded "
                          "schedule's phases use sweep.SEED_OPTIONS / WARM_OPTIONS); 0 = every due KKT check runs")
@@ -437,6 +452,9 @@ def main():
             raise SystemExit(f"bench.py: unequal windows per rank {per_rank} under weak scaling")
 
     pending = None  # the previous step's all-gather, still in flight (--overlap-gather)
+    # the seeded schedule's check options (None: sweep.WARM_OPTIONS / SEED_OPTIONS)
+    warm_opts = json.loads(args.warm_options) if args.warm_options else None
+    seed_opts = json.loads(args.seed_options) if args.seed_options else None
     # the all-gather through the library's own RCCL communicator (dvh_comm_init / dvh_gather_results; torch.distributed
     # only carries the unique id); DVH_GATHER=torch keeps torch.distributed's, and gloo rehearsals always use it
     lib_gather = None
@@ -453,7 +471,7 @@ def main():
     def step():
         nonlocal gathered, pending
         if sweep is not None:
-            phase["timing"], phase["paths"] = sweep.solve(solver, dev)
+            phase["timing"], phase["paths"] = sweep.solve(solver, dev, warm_options=warm_opts, seed_options=seed_opts)
         else:
             solver.solve_packed(dev)
         if dist is not None:
@@ -527,6 +545,8 @@ def main():
     schedule = {"kind": args.schedule}
     if sweep is not None:
         ns = sweep.n_seed
+        from dervet_hip.sweep import SEED_OPTIONS
+        schedule.update(warm_options=warm_opts or WARM_OPTIONS, seed_options=seed_opts or SEED_OPTIONS)
         schedule.update(seed_stride=args.seed_stride, blend=sweep.blend, seed_windows=ns, iters_mean_seed=round(float(iters[:ns].mean()), 1),
                         iters_mean_warm=round(float(iters[ns:].mean()), 1) if count > ns else None,
                         pdhg_launches_per_step=2 if count > ns else 1)
@@ -617,7 +637,7 @@ def main():
                    "scenarios_per_gpu": S, "windows_per_gpu": count, "eps_rel_kkt": 1e-6, **opts,
                    "schedule": (f"seeded (1 in {args.seed_stride} scenarios cold, the rest warm from the "
                                 f"inverse-distance-weighted blend of the {sweep.blend} nearest seeds in (log E/load, "
-                                f"duration, PV/load); warm phase {WARM_OPTIONS})" if sweep is not None else "cold"),
+                                f"duration, PV/load); warm phase {warm_opts or WARM_OPTIONS})" if sweep is not None else "cold"),
                    "parallelism": f"dp{world} (independent windows, 1 RCCL all-gather of results)"},
         "scenario_years_per_s": round(value / 12.0, 2),
         "iters_mean": round(float(iters.mean()), 1),
@@ -630,6 +650,7 @@ def main():
         "kernel_path": ks,
         "roofline": roofline,
         "schedule": schedule,
+        "outputs_sha256": outputs_sha(dev) if args.sha else None,
         "cpu_baseline": cpu,
         "gather": gather or None,
         "parity": parity,

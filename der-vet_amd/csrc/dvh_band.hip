@@ -233,6 +233,13 @@ constexpr bool kkt_prefetch() { return DVH_BAND_KKT_PREFETCH != 0 && (!ICE || DV
 #ifndef DVH_BAND_PRIO
 #define DVH_BAND_PRIO 2
 #endif
+// (DVH_BAND_PRIO_SETUP, A/B, off) the same for the set-up's tau reductions on wave 0 (every scaling pass and power-iteration
+// step): measured slower, 290.2k vs 292.3k windows/s (profiles/r06i_prio_setup.log) -- there the raised wave takes issue
+// slots from the other window's iterations
+#ifndef DVH_BAND_PRIO_SETUP
+#define DVH_BAND_PRIO_SETUP 0
+#endif
+constexpr bool kPrioSetup = DVH_BAND_PRIO_SETUP != 0;
 // DVH_BAND_PRIO_DUAL (A/B): every wave raises its priority from the start of the dual half-step until its DCM rows'
 // tau partials are written (the values wave 0's next reduction waits for).  Measured and not kept: 292.0k vs 292.6k
 // windows/s (profiles/r06c_ab.log); s_setprio 3 instead of 2 for wave 0: 292.7k (same).
@@ -609,6 +616,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
     if (ilane) nsp = fabs(kin0) * fsp * XE[0];
     __syncthreads();
     if (wid == 0) {
+      if (DVH_BAND_PRIO && kPrioSetup) __builtin_amdgcn_s_setprio(DVH_BAND_PRIO);
       for (int j = 0; j < J; ++j) {
         double a = TP[j * B + lane];
 #pragma unroll
@@ -626,6 +634,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
     }
     if (tlane || ilane) fsp *= factor(nsp);
     __syncthreads();  // every read of this pass's XE / YS / XT / TP is done
+    if (DVH_BAND_PRIO && kPrioSetup && wid == 0) __builtin_amdgcn_s_setprio(0);
   }
   {  // the KKT checks unscale with single-precision copies of the factors: a window whose factors leave
      // [2^-100, 2^100] (far inside float's normal range) goes to the ELL / generic path, which keeps them in double
@@ -914,6 +923,8 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
 #pragma unroll
       for (int r = 0; r < NR; ++r) wr[s][r] = 0.0;
     for (int pi = 0; pi <= P; ++pi) {
+      // (DVH_BAND_PRIO) wave 0's tau reduction is this step's critical path too, up to the first barrier
+      if (DVH_BAND_PRIO && kPrioSetup && wid == 0) __builtin_amdgcn_s_setprio(DVH_BAND_PRIO);
       if (pi > 0) {
         const double ysp = YS[tid];
 #pragma unroll
@@ -935,6 +946,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
       XE[tid] = vc[0][2];
       if (wid == 0 && lane < J) XT[lane] = vtau;
       __syncthreads();
+      if (DVH_BAND_PRIO && kPrioSetup && wid == 0) __builtin_amdgcn_s_setprio(0);
       const double xen = XE[tid + 1];
 #pragma unroll
       for (int s = 0; s < S; ++s) {
@@ -1582,8 +1594,10 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
       YS[tid + 1] = y[S - 1][0];
       if (ilane) YS[0] = sp[0];
       if (J > 0) tau_parts_of(y);
+      lds_barrier();
     }
-    lds_barrier();
+    // (a restart check that neither restarts nor checks KKT rewrote no shared value: the next iteration reads what the
+    // check iteration wrote before its barriers, and `red` is next written two barriers later -- no barrier here)
   }
   // outputs: the last check's T(z_k), unscaled (the lean form wrote them at that check)
 #pragma unroll

@@ -48,6 +48,18 @@ constexpr int kCB = kChainB;  // threads (and maximum steps) per segment
 #define DVH_CHAIN_TAU_WAVE 1
 #endif
 constexpr int kTauWave = DVH_CHAIN_TAU_WAVE;  // the wave holding the tau slots (wave 0 holds the init / ghost row)
+// DVH_CHAIN_PRIO (round 6, A/B, off): s_setprio for the waves whose primal half-step ends in a hand-off (as the band
+// kernel's wave 0, DVH_BAND_PRIO), until they have published.  DVH_CHAIN_KKT_PREFETCH (A/B, off): a KKT check's factor
+// loads issued together at the top of the check (as the band kernel's).  Measured and not kept
+// (profiles/r06f_chain_ab.log): config 3 DCM + PV 6.6 / 6.6 windows/s with prefetch / + priority against 6.8 without
+// (the prefetched doubles raise the spills 25 -> 36 VGPRs around the out-of-line KKT helpers), medium annual 1,526 /
+// 1,522 against 1,610: the team kernel runs one segment per CU, so there is no other workgroup to take issue slots from.
+#ifndef DVH_CHAIN_PRIO
+#define DVH_CHAIN_PRIO 0
+#endif
+#ifndef DVH_CHAIN_KKT_PREFETCH
+#define DVH_CHAIN_KKT_PREFETCH 0
+#endif
 static_assert(kTauWave >= 0 && kTauWave < kCB / kWave, "the tau wave exists");
 constexpr int kJSeg = kChainJSeg;  // tau columns per segment
 // granule offsets inside a segment's area (p = round parity)
@@ -1200,6 +1212,10 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
         }
       };
       double own = 0.0;
+      // (DVH_CHAIN_PRIO) the waves whose primal work ends in a hand-off -- the tau wave's partials, wave 0's first ene
+      // (down), the last step's wave (up) -- issue first on their SIMDs until they have published
+      const bool hot = DVH_CHAIN_PRIO && (wid == kTauWave || wid == 0 || wid == wl);
+      if (hot) __builtin_amdgcn_s_setprio(DVH_CHAIN_PRIO);
       // ---------------- primal half-step (reflected Halpern, rho = 1)
       {
         if (wid == kTauWave) {
@@ -1223,6 +1239,7 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
         }
         XE[tid] = xb[2];
         publish_b(xb);
+        if (hot) __builtin_amdgcn_s_setprio(0);
         kown(xb, kx);
 #ifdef DVH_CHAIN_TAU_IN_PRIMAL  // A/B: the round-3 placement
         if (wid == kTauWave) tau_step(own);
@@ -1296,6 +1313,25 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
 #pragma unroll
       for (int u = 4; u < kNRed; ++u) acc[u] = 0.0;
       if (kkt) {
+        // (DVH_CHAIN_KKT_PREFETCH) the lane's factors first, branch-free (a padding step / absent row loads entry 0 and
+        // discards it), from indices formed here from an opaque thread index: they arrive during the exchange below
+        double dcl[NC], drl[NR], dspl = 1.0;
+        if constexpr (DVH_CHAIN_KKT_PREFETCH) {
+          const int to = opaque(tid);
+          const bool vo = to < L;
+          const int tg = t0 + to;  // (this segment's first step + the lane)
+#pragma unroll
+          for (int v = 0; v < NC; ++v) {
+            const double dv = dcv[vo ? v * T + tg : 0];
+            dcl[v] = vo ? dv : 1.0;
+          }
+          const double d0 = drv[vo ? tg + 1 : 0];
+          drl[0] = vo ? d0 : 1.0;
+          const double d1 = drv[drow >= 0 ? drow : 0];
+          drl[1] = drow >= 0 ? d1 : 1.0;
+          const double dt_ = dcv[tlane ? 3 * T + jg0 : 0], di_ = drv[0];
+          dspl = tlane ? dt_ : ilane ? di_ : 1.0;
+        }
         // images of T(z_k); the next segment's first-ene image and the tau image totals come by exchange (the
         // ghost row's image is local)
         double xp[NC], yp[NR];
@@ -1330,15 +1366,15 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
         }
         lds_barrier();
         if (misc[0]) break;
-        auto col_kkt = [&](int j, double kt, double cj, double loj, double hij, double xj) {
-          const ColKktC r = col_kkt_c(kt, cj, loj, hij, xj, dcv[opaque(j)]);
+        auto col_kkt = [&](int j, double kt, double cj, double loj, double hij, double xj, double dpre) {
+          const ColKktC r = col_kkt_c(kt, cj, loj, hij, xj, DVH_CHAIN_KKT_PREFETCH ? dpre : dcv[opaque(j)]);
           acc[5] += r.rd2;
           acc[6] += r.cx;
           acc[8] += r.bt;
           if (DVH_KKT_RDX) acc[kRdx] += r.rdx;
         };
-        auto row_kkt = [&](int i, double kv, double qi, double yi, bool ge) {
-          const RowKktC r = row_kkt_c(kv, qi, yi, drv[opaque(i)], ge);
+        auto row_kkt = [&](int i, double kv, double qi, double yi, bool ge, double dpre) {
+          const RowKktC r = row_kkt_c(kv, qi, yi, DVH_CHAIN_KKT_PREFETCH ? dpre : drv[opaque(i)], ge);
           acc[4] += r.rp2;
           acc[7] += qi * yi;
           acc[9] += r.y2;
@@ -1347,15 +1383,15 @@ __global__ __launch_bounds__(kCB, 3) void pdhg_chain_kernel(const Batch b, const
         ktr(yp, YS[tid], kt);
         if (val) {
 #pragma unroll
-          for (int v = 0; v < NC; ++v) col_kkt(col(v), kt[v], cof(v), v == 2 ? loe : 0.0, hib(v), xp[v]);
+          for (int v = 0; v < NC; ++v) col_kkt(col(v), kt[v], cof(v), v == 2 ? loe : 0.0, hib(v), xp[v], dcl[v]);
         }
-        if (tlane && town) col_kkt(3 * T + jg0, XK[lane], sp[2], sp[3], sp[4], sp[5]);
+        if (tlane && town) col_kkt(3 * T + jg0, XK[lane], sp[2], sp[3], sp[4], sp[5], dspl);
         double kv[NR];
         kown(xp, kv);
         kfin(kv, XE[tid + 1]);
-        if (val) row_kkt(t + 1, kv[0], q[0], yp[0], false);
-        if (drow >= 0) row_kkt(drow, kv[1], q[1], yp[1], true);
-        if (ilane) row_kkt(0, sp[4] * XE[0], sp[3], sp[2], false);
+        if (val) row_kkt(t + 1, kv[0], q[0], yp[0], false, drl[0]);
+        if (drow >= 0) row_kkt(drow, kv[1], q[1], yp[1], true, drl[1]);
+        if (ilane) row_kkt(0, sp[4] * XE[0], sp[3], sp[2], false, dspl);
       }
       if (kkt) {
         block_sum1<B, kNRed, true>(acc, red);

@@ -1,0 +1,9 @@
+#!/bin/bash
+# wave-0 priority over the set-up's tau reductions (scaling passes, power iteration) too, A/B on the bench
+set -o pipefail
+O=gpurun_out/r06i; mkdir -p $O
+for L in cur ps0 cur ps0 cur ps0; do
+  if [ $L = cur ]; then unset DVH_LIB; else export DVH_LIB=ab_libs/lib_$L.so; fi
+  timeout -k 10 300 python -u bench.py --no-cpu --no-cold-ref --steps 10 --warmup 3 > $O/bench_$L.log 2>&1 || { echo "$L bench failed"; tail -20 $O/bench_$L.log; exit 1; }
+  echo $L bench $(tail -1 $O/bench_$L.log | python -c "import sys,json; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['iters_mean'], d['max_primal_res_rel'])")
+done
