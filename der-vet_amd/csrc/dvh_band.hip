@@ -243,6 +243,21 @@ constexpr bool kPrioSetup = DVH_BAND_PRIO_SETUP != 0;
 // DVH_BAND_PRIO_DUAL (A/B): every wave raises its priority from the start of the dual half-step until its DCM rows'
 // tau partials are written (the values wave 0's next reduction waits for).  Measured and not kept: 292.0k vs 292.6k
 // windows/s (profiles/r06c_ab.log); s_setprio 3 instead of 2 for wave 0: 292.7k (same).
+// DVH_BAND_PIN_BLEND (A/B): wave 0 finishes the iteration's Halpern blends (x = ca x-bar + cb x-anchor, and the rows')
+// before the second barrier, where it waits for the others anyway, instead of after it: the compiler sank them past the
+// barrier, to the head of wave 0's next primal half-step -- in front of the tau reduction, at normal priority.
+// Measured (profiles/r06j_pin_blend.log): bench 293.1k -> 298.1k windows/s, 0.939 -> 0.930 us per window-iteration per
+// slot at a fixed 1,024 iterations, identical iterations and residuals.
+#ifndef DVH_BAND_PIN_BLEND
+#define DVH_BAND_PIN_BLEND 1
+#endif
+// DVH_BAND_LATE_SOE (A/B): the waves without the tau column update the SOE rows of their lanes' steps 0 .. S - 2 after the
+// second barrier instead of before it (those duals are read only by the lane's own next primal half-step), so that they
+// reach the barrier -- which wave 0's next tau reduction waits behind -- sooner.  Measured and not kept: bench 298.7k vs
+// 297.9k windows/s (within the run-to-run spread), config 5 unchanged (profiles/r06k_late_soe.log).
+#ifndef DVH_BAND_LATE_SOE
+#define DVH_BAND_LATE_SOE 0
+#endif
 #ifndef DVH_BAND_PRIO_DUAL
 #define DVH_BAND_PRIO_DUAL 0
 #endif
@@ -1329,7 +1344,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
       if (J > 0) tau_parts_of(y);
       if constexpr (DVH_BAND_PRIO_DUAL) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
-      for (int s = 0; s < S; ++s) row_step(s, 0);
+      for (int s = (DVH_BAND_LATE_SOE && !W0) ? S - 1 : 0; s < S; ++s) row_step(s, 0);
       YS[tid + 1] = y[S - 1][0];
       if (W0 || wid == 0) {  // init row (lane kInitLane): ene_0 = target
         if (ilane) {
@@ -1350,7 +1365,20 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
     ++it;
     ++kin;
     pstamp(2);
+    if constexpr (W0 && DVH_BAND_PIN_BLEND) {  // (see DVH_BAND_PIN_BLEND) this iteration's blends before the barrier
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+#pragma unroll
+        for (int v = 0; v < NC; ++v) asm volatile("" ::"v"(x[s][v]));
+#pragma unroll
+        for (int r = 0; r < NR; ++r) asm volatile("" ::"v"(y[s][r]));
+      }
+    }
     lds_barrier();
+    if constexpr (DVH_BAND_LATE_SOE && !W0) {  // (DVH_BAND_LATE_SOE) the lane-local SOE rows, after the barrier
+#pragma unroll
+      for (int s = 0; s < S - 1; ++s) row_step(s, 0);
+    }
     pstamp(3);
   };
 
