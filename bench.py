@@ -157,8 +157,9 @@ def roofline_object(alg, pdhg_s, prof, kname, launches, copy_gbps):
 
 # the full-population certification of the bench kernel: every one of the 120,000 windows, seeded and cold, re-solved
 # by HiGHS on the host (scripts/certify_dump.py + scripts/certify_highs.py)
-CERTIFICATION = ("profiles/r05z5_certify.json (all 120,000 windows vs HiGHS, seeded with blended warm starts and cold; "
-                 "final round-5 library: box steps rescaled at restarts, KKT helpers inlined, scheduler options)")
+CERTIFICATION = ("profiles/r06z_certify.json (all 120,000 windows vs HiGHS, seeded with blended warm starts and cold: "
+                 "every window optimal, max 9.72e-7 / 9.78e-7; final round-6 library: wave-0 issue priority, pinned "
+                 "blends, batched KKT factor loads)")
 
 
 def _free_port():
