@@ -255,6 +255,20 @@ constexpr bool kPrioSetup = DVH_BAND_PRIO_SETUP != 0;
 // second barrier instead of before it (those duals are read only by the lane's own next primal half-step), so that they
 // reach the barrier -- which wave 0's next tau reduction waits behind -- sooner.  Measured and not kept: bench 298.7k vs
 // 297.9k windows/s (within the run-to-run spread), config 5 unchanged (profiles/r06k_late_soe.log).
+// DVH_BAND_PIN_KX (A/B): the waves without the tau column finish their primal half-step's own-column K x-bar (x-bar =
+// 2 p - x, then K x-bar - q of their rows) before the first barrier, where they wait for wave 0 anyway, instead of after
+// it: the compiler sank that work into their dual half-step, which is the critical path into the second barrier.
+// Measured (profiles/r06l_pin_kx.log): config 5 (the ICE form: eleven such waves) 116.5k -> 126.0k windows/s; the bench
+// 298.2k -> 298.6k, within its spread, at 25 instead of 15 spilled VGPRs.  1 (default): the ICE form only; 2: every form.
+#ifndef DVH_BAND_PIN_KX
+#define DVH_BAND_PIN_KX 1
+#endif
+// DVH_BAND_LATE_ICE: the same waves update the two ICE rows' duals (read only by the lane's own next primal
+// half-step) after the second barrier instead of before it.  Measured (profiles/r06m_late_ice.log): config 5
+// 126.0k -> 127.9-128.4k windows/s.
+#ifndef DVH_BAND_LATE_ICE
+#define DVH_BAND_LATE_ICE 1
+#endif
 #ifndef DVH_BAND_LATE_SOE
 #define DVH_BAND_LATE_SOE 0
 #endif
@@ -1320,6 +1334,12 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
       }
     }
     pstamp(0);
+    if constexpr (!W0 && (DVH_BAND_PIN_KX > 1 || (DVH_BAND_PIN_KX == 1 && ICE))) {  // (DVH_BAND_PIN_KX) K x-bar first
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+#pragma unroll
+        for (int r = 0; r < NR; ++r) asm volatile("" ::"v"(kx[s][r]));
+    }
     lds_barrier();
     if constexpr (W0 && DVH_BAND_PRIO) __builtin_amdgcn_s_setprio(0);
     pstamp(1);
@@ -1339,7 +1359,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
       for (int s = 0; s < S; ++s) {
         kx[s][1] = fma(kd[s][2], xtv[s], kx[s][1]);  // kfin_tau
 #pragma unroll
-        for (int r = 1; r < NR; ++r) row_step(s, r);
+        for (int r = 1; r < ((DVH_BAND_LATE_ICE && ICE && !W0) ? 2 : NR); ++r) row_step(s, r);
       }
       if (J > 0) tau_parts_of(y);
       if constexpr (DVH_BAND_PRIO_DUAL) __builtin_amdgcn_s_setprio(0);
@@ -1378,6 +1398,12 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
     if constexpr (DVH_BAND_LATE_SOE && !W0) {  // (DVH_BAND_LATE_SOE) the lane-local SOE rows, after the barrier
 #pragma unroll
       for (int s = 0; s < S - 1; ++s) row_step(s, 0);
+    }
+    if constexpr (DVH_BAND_LATE_ICE && ICE && !W0) {  // (DVH_BAND_LATE_ICE) the ICE rows, after the barrier
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+#pragma unroll
+        for (int r = 2; r < NR; ++r) row_step(s, r);
     }
     pstamp(3);
   };
