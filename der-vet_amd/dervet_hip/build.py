@@ -2,6 +2,7 @@
 
 Usage: python -m dervet_hip.build   (or dervet_hip.build.build())
 """
+import json
 import os
 import subprocess
 import sys
@@ -10,6 +11,10 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "..", "csrc")
 LIB = os.path.join(HERE, "libdervet_hip.so")
+# the build configuration the library was linked with (flags and compiler string), written by build(): bench.py keys
+# its PMC profiles to it without running hipcc from a process that may already hold the GPU (under rocprofv3 --pmc it
+# does, and the GPU box refuses an exec from such a process)
+BUILDINFO = os.path.join(HERE, "libdervet_hip.buildinfo.json")
 SOURCES = ["dvh_kernels.hip", "dvh_band.hip", "dvh_band_persist.hip", "dvh_band_persist_ice.hip", "dvh_chain.hip", "dvh_build.hip", "dvh_sweep.hip", "dvh_series.hip", "dvh_route.hip", "dvh_large.hip", "dvh_outage.hip",
            "dvh_api.cpp", "dvh_validate.cpp", "dvh_comm.cpp"]
 # per-source flags: the band kernel's persistent forms without machine-level loop-invariant code motion (their loop
@@ -41,6 +46,8 @@ def build(force=False, verbose=False):
     """Compile every source to an object in parallel (the ELL / band instantiations make dvh_kernels.hip the long
     pole, ~2 min), then link.  Each kernel is launched from its own translation unit, so no -fgpu-rdc."""
     if not force and not _stale():
+        if not os.path.exists(BUILDINFO):
+            _write_buildinfo()
         return LIB
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     flags = list(FLAGS)
@@ -70,7 +77,15 @@ def build(force=False, verbose=False):
         sys.stderr.write(r.stdout + r.stderr)
         raise RuntimeError("hipcc failed linking libdervet_hip.so")
     os.replace(LIB + ".tmp", LIB)
+    _write_buildinfo()
     return LIB
+
+
+def _write_buildinfo():
+    cfg = _current_config(compiler_version())
+    with open(BUILDINFO + ".tmp", "w") as f:
+        json.dump(cfg, f, sort_keys=True)
+    os.replace(BUILDINFO + ".tmp", BUILDINFO)
 
 
 def build_variant(out, defines, recompile=("dvh_band.hip", "dvh_band_persist.hip", "dvh_band_persist_ice.hip"),
@@ -120,10 +135,22 @@ def compiler_version():
         return "unknown"
 
 
+def _current_config(compiler):
+    return {"flags": FLAGS, "extra_flags": {k: EXTRA_FLAGS[k] for k in sorted(EXTRA_FLAGS)}, "compiler": compiler}
+
+
 def build_config():
-    """Everything besides the sources that decides the machine code: common and per-source flags, compiler."""
-    return {"flags": FLAGS, "extra_flags": {k: EXTRA_FLAGS[k] for k in sorted(EXTRA_FLAGS)},
-            "compiler": compiler_version()}
+    """Everything besides the sources that decides the machine code: common and per-source flags, compiler.  The
+    compiler string is the one build() recorded with the library when its flags are the current ones; hipcc is asked
+    only when there is no such record."""
+    try:
+        with open(BUILDINFO) as f:
+            rec = json.load(f)
+        if rec == _current_config(rec.get("compiler")) and rec.get("compiler"):
+            return rec
+    except (OSError, ValueError):
+        pass
+    return _current_config(compiler_version())
 
 
 if __name__ == "__main__":
