@@ -1385,7 +1385,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
     ++it;
     ++kin;
     pstamp(2);
-    if constexpr ((W0 || DVH_BAND_PIN_BLEND > 1) && DVH_BAND_PIN_BLEND) {  // (DVH_BAND_PIN_BLEND) blends before the barrier
+    if constexpr (W0 && DVH_BAND_PIN_BLEND) {  // (see DVH_BAND_PIN_BLEND) this iteration's blends before the barrier
 #pragma unroll
       for (int s = 0; s < S; ++s) {
 #pragma unroll
