@@ -295,9 +295,36 @@ __device__ __forceinline__ double fma_clamp01(double a, double b, double c) {
   return r;
 }
 
+// DVH_BAND_UWIN: the window index and its descriptor's offsets are read through v_readfirstlane, so that they and every
+// address formed from them (the window's CSR, costs, bounds, outputs, workspace) are scalar.  Loaded as they are -- with
+// vector loads, since the kernel writes global memory the compiler does not treat the descriptors as constant -- they sat
+// in VGPR pairs, and the base addresses the set-up and the write-back use were spilled.
+#ifndef DVH_BAND_UWIN
+#define DVH_BAND_UWIN 1
+#endif
+// DVH_BAND_USCAL: the check path's wave-uniform doubles (the fixed-point residual and the restart test's r0 / rprev, the
+// KKT objectives and ratios, the gate's state) through v_readfirstlane, and the residuals' denominators formed where they
+// are used: held in SGPR pairs between checks instead of VGPR pairs.  1 (default): the ICE form only -- at its 168-VGPR
+// budget spilled VGPRs 41 -> 19, config 5 +1.3 %; in the battery form (spills 2 -> 0) the bench ran 1.8 % slower
+// (profiles/r06r_uscal.log); 2: every form.
+#ifndef DVH_BAND_USCAL
+#define DVH_BAND_USCAL 1
+#endif
+template <bool ICE>
+__device__ __forceinline__ double usc(double v) {
+  return (DVH_BAND_USCAL > 1 || (DVH_BAND_USCAL == 1 && ICE)) ? uniform(v) : v;
+}
+// a uniform double the optimiser must re-read where it is used (so that what is formed from it is not hoisted out of the
+// iteration loop into a long-lived VGPR pair)
+template <bool ICE>
+__device__ __forceinline__ double sgpr_fresh(double v) {
+  if constexpr (DVH_BAND_USCAL > 1 || (DVH_BAND_USCAL == 1 && ICE)) asm volatile("" : "+s"(v));
+  return v;
+}
 template <int B, int S, bool ICE, int LF, int WPS, bool GATE, bool BOX>
-__device__ __forceinline__ void band_window(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, const int k,
+__device__ __forceinline__ void band_window(const Batch& b, const Work& w, const Chunk& ch, const Opts& o, const int k_in,
                                             const int tid) {
+  const int k = DVH_BAND_UWIN ? __builtin_amdgcn_readfirstlane(k_in) : k_in;
   static_assert(!BOX || !(LF & kLfImages), "the box form keeps the check images in LDS");
   constexpr int NW = B / kWave;
   constexpr int SB = S * B;        // step capacity
@@ -305,7 +332,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
   constexpr int NR = ICE ? 4 : 2;  // rows per step: SOE, DCM (, ICE rated, ICE minimum)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int kl = k - ch.first;
-  const WinOff W = win_offsets(b, ch, k);
+  const WinOff W = DVH_BAND_UWIN ? uniform_win(win_offsets(b, ch, k)) : win_offsets(b, ch, k);
   const int n = W.n, m = W.m, meq = W.meq;
   const int lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   double* scal = w.scal + (int64_t)kl * kScal;
@@ -1447,7 +1474,7 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
       block_sum1<B, 4, true>(acc4, red);
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc[u] = acc4[u];
-      r = sqrt(pw * acc[0] + acc[2] / pw);
+      r = usc<ICE>(sqrt(pw * acc[0] + acc[2] / pw));
       if (kkt && !last && kkt_gate_skip(o, gate, r)) {
         kkt = false;
         ++gate.skip;
@@ -1582,11 +1609,12 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc[u] = acc4[u];
     }
-    if constexpr (!GATE) r = sqrt(pw * acc[0] + acc[2] / pw);
+    if constexpr (!GATE) r = usc<ICE>(sqrt(pw * acc[0] + acc[2] / pw));
     if (kkt) {
-      const double pobj = acc[6] + c0, dobj = acc[7] + acc[8] + c0;
-      const double pres = sqrt(acc[4]) / (1.0 + qnorm), dres = sqrt(acc[5]) / (1.0 + cnorm);
-      const double gap = fabs(pobj - dobj) / (1.0 + fabs(pobj) + fabs(dobj));
+      const double pobj = usc<ICE>(acc[6] + c0), dobj = usc<ICE>(acc[7] + acc[8] + c0);
+      const double pres = usc<ICE>(sqrt(acc[4]) / (1.0 + sgpr_fresh<ICE>(qnorm)));
+      const double dres = usc<ICE>(sqrt(acc[5]) / (1.0 + sgpr_fresh<ICE>(cnorm)));
+      const double gap = usc<ICE>(fabs(pobj - dobj) / (1.0 + fabs(pobj) + fabs(dobj)));
       if (tid == 0) {
         fin[0] = pobj;
         fin[1] = pres;
@@ -1597,7 +1625,10 @@ __device__ __forceinline__ void band_window(const Batch& b, const Work& w, const
         status = kOptimal;
         break;
       }
-      if constexpr (GATE) gate.note(pres, dres, gap, o.eps, r);
+      if constexpr (GATE) {
+        gate.note(pres, dres, gap, o.eps, r);
+        gate.q = usc<ICE>(gate.q);
+      }
       if (!(isfinite(pobj) && isfinite(dobj))) {
         status = kNumerical;
         break;

@@ -218,6 +218,30 @@ __device__ __forceinline__ WinOff win_offsets(const Batch& b, const Chunk& ch, i
   return o;
 }
 
+// A wave-uniform 64-bit value made scalar (v_readfirstlane of both halves), and a window's offsets likewise: read with
+// vector loads (the kernels write global memory, so the compiler does not treat the descriptors as constant), they and
+// every address formed from them would sit in VGPR pairs.
+__device__ __forceinline__ int64_t uniform_i64(int64_t v) {
+  const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(unsigned long long)v);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)((unsigned long long)v >> 32));
+  return (int64_t)(((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ WinOff uniform_win(WinOff o) {
+  o.n = __builtin_amdgcn_readfirstlane(o.n);
+  o.m = __builtin_amdgcn_readfirstlane(o.m);
+  o.meq = __builtin_amdgcn_readfirstlane(o.meq);
+  o.nnz = __builtin_amdgcn_readfirstlane(o.nnz);
+  o.row = uniform_i64(o.row);
+  o.nz = uniform_i64(o.nz);
+  o.on = uniform_i64(o.on);
+  o.om = uniform_i64(o.om);
+  o.wn = uniform_i64(o.wn);
+  o.wm = uniform_i64(o.wm);
+  o.wz = uniform_i64(o.wz);
+  o.wtr = uniform_i64(o.wtr);
+  return o;
+}
+
 // LDS f64 load / store at an absolute LDS byte address (precomputed once in a VGPR, so a gather is a single
 // ds_read_b64 with no address arithmetic in the loop).
 typedef __attribute__((address_space(3))) double lds_f64;
