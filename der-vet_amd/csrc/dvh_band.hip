@@ -251,10 +251,11 @@ constexpr bool kPrioSetup = DVH_BAND_PRIO_SETUP != 0;
 #ifndef DVH_BAND_PIN_BLEND
 #define DVH_BAND_PIN_BLEND 1
 #endif
-// DVH_BAND_LATE_SOE (A/B): the waves without the tau column update the SOE rows of their lanes' steps 0 .. S - 2 after the
+// DVH_BAND_LATE_SOE: the waves without the tau column update the SOE rows of their lanes' steps 0 .. S - 2 after the
 // second barrier instead of before it (those duals are read only by the lane's own next primal half-step), so that they
-// reach the barrier -- which wave 0's next tau reduction waits behind -- sooner.  Measured and not kept: bench 298.7k vs
-// 297.9k windows/s (within the run-to-run spread), config 5 unchanged (profiles/r06k_late_soe.log).
+// reach the barrier -- which wave 0's next tau reduction waits behind -- sooner.  With 15 spilled VGPRs it was within the
+// bench's spread (298.7k vs 297.9k, profiles/r06k_late_soe.log); with the spills gone (DVH_BAND_UWIN) bench 300.1k ->
+// 304.6k windows/s, config 5 unchanged (profiles/r06s_ab.log).
 // DVH_BAND_PIN_KX (A/B): the waves without the tau column finish their primal half-step's own-column K x-bar (x-bar =
 // 2 p - x, then K x-bar - q of their rows) before the first barrier, where they wait for wave 0 anyway, instead of after
 // it: the compiler sank that work into their dual half-step, which is the critical path into the second barrier.
@@ -270,7 +271,7 @@ constexpr bool kPrioSetup = DVH_BAND_PRIO_SETUP != 0;
 #define DVH_BAND_LATE_ICE 1
 #endif
 #ifndef DVH_BAND_LATE_SOE
-#define DVH_BAND_LATE_SOE 0
+#define DVH_BAND_LATE_SOE 1
 #endif
 #ifndef DVH_BAND_PRIO_DUAL
 #define DVH_BAND_PRIO_DUAL 0

@@ -158,7 +158,10 @@ def _nearest(fr, fs):
 # iterations, PDHG time of the schedule 376.6 -> 357.2 ms; every other restart / weight setting tried was slower.
 # Round 2: KKT at every restart check, but a due check is skipped while its predicted outcome is > 4x eps
 # (dvh_options.kkt_predict; a KKT check costs ~6 iterations): PDHG 550 -> 527 ms on the bench batch, 2,073 -> 2,038
-# warm iterations (profiles/r02zy_kkt_predict.log).
+# warm iterations (profiles/r02zy_kkt_predict.log).  Round 6: with the cheaper iteration the period was re-measured
+# (profiles/r06u_check_period.log, r06w_check_period.log): 56 / 64 / 68 / 72 / 76 / 80 -> 298k / 306k / 309k / 308k /
+# 305k / 297k windows/s on one box, but at 68 and at 72 one of the 120,000 bench windows stops 1.40e-6 from HiGHS's
+# objective (the KKT test passes at a check that lands elsewhere; profiles/r06x_check_period_72.log): 64 stays.
 WARM_OPTIONS = {"check_every": 64, "kkt_every": 1, "kkt_predict": 4}
 # dvh_options for the cold seed phase: the defaults (checks every 32, KKT every 4th) with the same KKT gate: on the
 # bench's 120,000 windows all cold, PDHG 864.6 -> 824.6 ms at unchanged iterations (profiles/r02zzb_cold_kkt_predict.log)
