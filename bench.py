@@ -159,7 +159,7 @@ def roofline_object(alg, pdhg_s, prof, kname, launches, copy_gbps):
 # by HiGHS on the host (scripts/certify_dump.py + scripts/certify_highs.py)
 CERTIFICATION = ("profiles/r06z_certify.json (all 120,000 windows vs HiGHS, seeded with blended warm starts and cold: "
                  "every window optimal, max 9.72e-7 / 9.78e-7; final round-6 library: wave-0 issue priority, pinned "
-                 "blends, batched KKT factor loads)")
+                 "blends, batched KKT factor loads, scalar window offsets, late lane-local SOE rows)")
 
 
 def _free_port():
