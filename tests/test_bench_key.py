@@ -39,3 +39,21 @@ def test_committed_pmc_profiles_carry_the_current_key():
     for name in ("pdhg_traffic", "pdhg_valu"):
         with open(os.path.join(ROOT, "profiles", name + ".json")) as f:
             assert json.load(f)["source_key"] == key, name
+
+
+def test_build_config_reads_the_recorded_compiler_and_ignores_a_stale_record(tmp_path, monkeypatch):
+    """build() records the build configuration with the library; build_config() uses the recorded compiler string only
+    while the recorded flags are the current ones (so bench.py forms its key without running hipcc from a process that
+    may hold the GPU), and asks hipcc otherwise."""
+    rec = tmp_path / "buildinfo.json"
+    monkeypatch.setattr(build, "BUILDINFO", str(rec))
+    monkeypatch.setattr(build, "compiler_version", lambda: "hipcc (asked)")
+    cur = {"flags": build.FLAGS, "extra_flags": {k: build.EXTRA_FLAGS[k] for k in sorted(build.EXTRA_FLAGS)},
+           "compiler": "hipcc (recorded)"}
+    rec.write_text(json.dumps(cur))
+    assert build.build_config()["compiler"] == "hipcc (recorded)"
+    stale = dict(cur, flags=cur["flags"] + ["-DSTALE"])
+    rec.write_text(json.dumps(stale))
+    assert build.build_config()["compiler"] == "hipcc (asked)"
+    rec.unlink()
+    assert build.build_config()["compiler"] == "hipcc (asked)"
