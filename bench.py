@@ -361,6 +361,7 @@ def main():
                          "rank count differs from the GPUs it would report")
     if args.dry_run:
         return dry_run(args, world, rank)
+    source_key()  # (cached now, before this process touches the GPU: without the build's record it runs hipcc)
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (the solver has no CPU fallback)")
     # RCCL over xGMI; DVH_BENCH_BACKEND=gloo only to rehearse several ranks on one GPU (RCCL refuses that)
