@@ -463,16 +463,9 @@ def main():
     if dist is not None and backend == "nccl" and os.environ.get("DVH_GATHER", "library") == "library":
         # every rank forms the communicator or none uses it: a rank whose RCCL could not be opened (the same image on
         # every rank, so in practice all or none) reports it, and the ranks agree before the first gather
-        err = None
-        try:
-            lib_gather = parallel.LibraryGather.from_torch(solver)
-        except (RuntimeError, OSError) as e:
-            err = str(e)
-        ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=f"cuda:{local}")
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        if int(ok.item()) == 0:
-            lib_gather = None
-            gather["library_error"] = err or "another rank could not form the library's communicator"
+        lib_gather, err = parallel.agreed_library_gather(solver, device=f"cuda:{local}")
+        if lib_gather is None:
+            gather["library_error"] = err
             if rank == 0:
                 print(f"bench.py: library all-gather unavailable ({gather['library_error']}); torch.distributed's "
                       "all-gather is used", file=sys.stderr, flush=True)

@@ -199,6 +199,26 @@ class LibraryGather:
         return done if async_op else done.wait()
 
 
+def agreed_library_gather(solver, device="cpu", group=None, make=None):
+    """The library's all-gather on every rank, or on none: each rank tries to form the communicator
+    (``LibraryGather.from_torch``, or ``make()``), and one MIN all-reduce of the outcome over torch.distributed decides
+    before the first gather, so that no rank gathers through RCCL while another uses torch.distributed's all-gather.
+    Returns (LibraryGather or None, the reason it is None or None).  ``device``: where the all-reduce's flag lives
+    (the rank's GPU for the nccl backend, "cpu" for gloo)."""
+    import torch
+    import torch.distributed as dist
+    lib, err = None, None
+    try:
+        lib = make() if make is not None else LibraryGather.from_torch(solver, group)
+    except (RuntimeError, OSError) as e:
+        err = str(e) or type(e).__name__
+    ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=device)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+    if int(ok.item()) == 0:
+        return None, err or "another rank could not form the library's communicator"
+    return lib, None
+
+
 class PendingLibraryGather:
     """A library all-gather in flight: ``wait()`` makes the current stream wait for it and returns the rows (the input
     stays referenced until then)."""

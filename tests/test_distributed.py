@@ -218,3 +218,35 @@ def test_two_rank_async_gather_overlapping_the_next_step(tmp_path):
         assert torch.equal(g[step, :5, 1], torch.full((5,), 100.0 * step, dtype=torch.float64))
         assert torch.equal(g[step, 5:, 1], torch.full((5,), 100.0 * step + 1, dtype=torch.float64))
         assert torch.equal(g[step, :, 0], torch.cat([torch.arange(5.0), torch.arange(5.0) + 10]).double())
+
+
+def _agree_worker(rank, world, port, fail_rank, out):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def make():  # stands in for LibraryGather.from_torch: fails on fail_rank (RCCL not openable there)
+        if rank == fail_rank:
+            raise RuntimeError("RCCL could not be opened (test)")
+        return ("library gather of rank", rank)
+
+    lib, err = parallel.agreed_library_gather(None, device="cpu", make=make)
+    torch.save({"lib": lib, "err": err}, f"{out}.{rank}")
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail_rank", [-1, 0, 1])
+def test_ranks_agree_on_the_library_gather(tmp_path, fail_rank):
+    """bench.py's N > 1 all-gather: the library's communicator on every rank or on none -- a rank that cannot form it
+    makes every rank fall back to torch.distributed's all-gather (never a mixed pair of collectives)."""
+    out = str(tmp_path / "agree")
+    mp.spawn(_agree_worker, args=(2, _free_port(), fail_rank, out), nprocs=2, join=True)
+    got = [torch.load(f"{out}.{r}", weights_only=False) for r in range(2)]
+    if fail_rank < 0:
+        assert [g["lib"] for g in got] == [("library gather of rank", 0), ("library gather of rank", 1)]
+        assert all(g["err"] is None for g in got)
+    else:
+        assert all(g["lib"] is None for g in got)
+        assert "RCCL could not be opened" in got[fail_rank]["err"]
+        assert "another rank" in got[1 - fail_rank]["err"]
